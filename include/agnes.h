@@ -1,0 +1,327 @@
+/*
+ * agnes.h — C ABI of the MI355X-native Agnes vote-tally engine.
+ *
+ * This header is the drop-in boundary for ONE hot path of Liamsi/agnes
+ * (reference mounted read-only at /root/reference, Rust, GPL-3.0, clean-room):
+ *
+ *   ConsensusExecutor::apply_msg, Vote arm      src/consensus_executor.rs:61-69
+ *     -> VoteExecutor::apply(vote, weight)       src/vote_executor.rs:20-23
+ *        -> RoundVotes::add_vote                 src/round_votes.rs:92-97
+ *           -> VoteCount::add_vote / is_quorum   src/round_votes.rs:31-33,48-67
+ *        -> VoteExecutor::to_event               src/vote_executor.rs:26-36
+ *     -> State::apply(round, event)              src/state_machine.rs:174-214
+ *
+ * batched one instance (height x validator-set x round set) per wave on the GPU.
+ * Plain C: POD structs, pointers and sizes, integer status codes.  No torch,
+ * no C++ types, nothing unwinds across the boundary.
+ *
+ * Integer semantics: every weight / total is int64 with two's-complement
+ * WRAPPING arithmetic (the reference's release-build behaviour of i64 `+`/`*`,
+ * round_votes.rs:32,52,55,62).  Results are bit-exact with the reference on
+ * every input, including overflowing ones.
+ */
+#ifndef AGNES_H
+#define AGNES_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AGNES_ABI_VERSION 1u
+
+/* ---------------------------------------------------------------------------
+ * Status codes (reference never fails, state_machine.rs:212; these report
+ * boundary misuse only).
+ * ------------------------------------------------------------------------- */
+#define AGNES_OK 0
+#define AGNES_E_INVALID (-1)     /* bad argument / null pointer / size mismatch   */
+#define AGNES_E_UNSUPPORTED (-2) /* configuration outside what the engine handles */
+#define AGNES_E_DEVICE (-3)      /* HIP runtime error                            */
+#define AGNES_E_NOMEM (-4)       /* allocation failed                            */
+#define AGNES_E_NODEVICE (-5)    /* no GPU visible: the engine has NO CPU fallback */
+
+/* ---------------------------------------------------------------------------
+ * Value / vote vocabulary (src/lib.rs:3-39)
+ *
+ * `Value` is a zero-sized struct in the reference (lib.rs:3-4).  Here it is a
+ * 32-bit label `value_id`; `Option<Value>::None` (a nil vote) is AGNES_NIL.
+ * ------------------------------------------------------------------------- */
+#define AGNES_NIL 0xFFFFFFFFu
+
+#define AGNES_PREVOTE 0u   /* VoteType::Prevote   lib.rs:17 */
+#define AGNES_PRECOMMIT 1u /* VoteType::Precommit lib.rs:18 */
+
+/* Thresh, round_votes.rs:22-28 */
+#define AGNES_THRESH_INIT 0u
+#define AGNES_THRESH_ANY 1u
+#define AGNES_THRESH_NIL 2u
+#define AGNES_THRESH_VALUE 3u
+
+/* Step, state_machine.rs:14-21 */
+#define AGNES_STEP_NEW_ROUND 0u
+#define AGNES_STEP_PROPOSE 1u
+#define AGNES_STEP_PREVOTE 2u
+#define AGNES_STEP_PRECOMMIT 3u
+#define AGNES_STEP_COMMIT 4u
+
+/* Event, state_machine.rs:96-110 (same order as the Rust enum) */
+#define AGNES_EV_NEW_ROUND 0u
+#define AGNES_EV_NEW_ROUND_PROPOSER 1u
+#define AGNES_EV_PROPOSAL 2u
+#define AGNES_EV_PROPOSAL_INVALID 3u
+#define AGNES_EV_POLKA_ANY 4u
+#define AGNES_EV_POLKA_NIL 5u
+#define AGNES_EV_POLKA_VALUE 6u
+#define AGNES_EV_PRECOMMIT_ANY 7u
+#define AGNES_EV_PRECOMMIT_VALUE 8u
+#define AGNES_EV_ROUND_SKIP 9u
+#define AGNES_EV_TIMEOUT_PROPOSE 10u
+#define AGNES_EV_TIMEOUT_PREVOTE 11u
+#define AGNES_EV_TIMEOUT_PRECOMMIT 12u
+#define AGNES_EV_NONE 0xFFu /* Option<Event>::None */
+
+/* Message, state_machine.rs:118-124 */
+#define AGNES_MSG_NONE 0u
+#define AGNES_MSG_NEW_ROUND 1u
+#define AGNES_MSG_PROPOSAL 2u
+#define AGNES_MSG_VOTE 3u
+#define AGNES_MSG_TIMEOUT 4u
+#define AGNES_MSG_DECISION 5u
+
+/* TimeoutStep, state_machine.rs:159-163 */
+#define AGNES_TIMEOUT_PROPOSE 0u
+#define AGNES_TIMEOUT_PREVOTE 1u
+#define AGNES_TIMEOUT_PRECOMMIT 2u
+
+/* ---------------------------------------------------------------------------
+ * POD mirrors of the reference types
+ * ------------------------------------------------------------------------- */
+
+/* Vote, lib.rs:22-27 (+ value label).  Copy in the reference; passed by pointer. */
+typedef struct agnes_vote {
+    int64_t round;     /* Vote.round (i64)                    */
+    uint32_t value;    /* Vote.value: label or AGNES_NIL      */
+    uint8_t typ;       /* AGNES_PREVOTE / AGNES_PRECOMMIT     */
+    uint8_t pad[3];
+} agnes_vote;
+
+/* Event, state_machine.rs:96-110 */
+typedef struct agnes_event {
+    int64_t round;     /* round argument of State::apply (state_machine.rs:174)   */
+    int64_t pol_round; /* Event::Proposal(pol_round, _) only                     */
+    uint32_t value;    /* NewRoundProposer / Proposal / PolkaValue / PrecommitValue */
+    uint8_t kind;      /* AGNES_EV_*                                              */
+    uint8_t pad[3];
+} agnes_event;
+
+/* Message, state_machine.rs:118-163 (Proposal lib.rs:8-13, Timeout :152-155) */
+typedef struct agnes_message {
+    int64_t round;        /* NewRound(r) / Proposal.round / Vote.round / Timeout.round / Decision.round */
+    int64_t pol_round;    /* Proposal.pol_round                                     */
+    uint32_t value;       /* Proposal / Vote (AGNES_NIL = None) / Decision value    */
+    uint8_t kind;         /* AGNES_MSG_*                                            */
+    uint8_t vote_type;    /* Vote.typ                                               */
+    uint8_t timeout_step; /* Timeout.step                                           */
+    uint8_t pad;
+} agnes_message;
+
+/* State, state_machine.rs:24-31 (Copy).  64-byte device/host record.
+ * `decided`/`decision_*` are an extension recording Message::Decision
+ * (the reference leaves that to the consumer, consensus_executor.rs:46-48). */
+typedef struct agnes_state {
+    int64_t height;         /* State.height                      */
+    int64_t round;          /* State.round                       */
+    int64_t locked_round;   /* State.locked: Option<RoundValue>  */
+    int64_t valid_round;    /* State.valid:  Option<RoundValue>  */
+    int64_t decision_round; /* extension                         */
+    uint32_t locked_value;
+    uint32_t valid_value;
+    uint32_t decision_value; /* extension */
+    uint8_t step;            /* AGNES_STEP_*                     */
+    uint8_t locked_present;  /* Option::is_some                  */
+    uint8_t valid_present;
+    uint8_t decided; /* extension */
+    uint8_t pad[8];
+} agnes_state;
+
+/* ---------------------------------------------------------------------------
+ * Per-vote result code (1 byte per input vote; the dense hot-path output)
+ *
+ *   bits 0..2  tally event  (VoteExecutor::apply -> Option<Event>, vote_executor.rs:20-36)
+ *   bit  3     RoundSkip    (+1/3 distinct validators of the vote's round; extension)
+ *   bits 4..7  message(s) State::apply produced for this vote (state machine on)
+ * ------------------------------------------------------------------------- */
+#define AGNES_CODE_NONE 0u
+#define AGNES_CODE_POLKA_ANY 1u       /* (Prevote, Thresh::Any)     */
+#define AGNES_CODE_POLKA_NIL 2u       /* (Prevote, Thresh::Nil)     */
+#define AGNES_CODE_POLKA_VALUE 3u     /* (Prevote, Thresh::Value)   */
+#define AGNES_CODE_PRECOMMIT_ANY 4u   /* (Precommit, Thresh::Any)   */
+#define AGNES_CODE_PRECOMMIT_VALUE 5u /* (Precommit, Thresh::Value) */
+#define AGNES_CODE_INVALID 6u  /* field out of range / wrong instance: vote ignored        */
+#define AGNES_CODE_REJECTED 7u /* DEDUP mode: not the first vote of (round,type,validator) */
+#define AGNES_CODE_EVENT_MASK 0x07u
+#define AGNES_CODE_SKIP 0x08u
+#define AGNES_CODE_MSG_SHIFT 4
+
+/* message nibble (all carry round = the vote's round; value = the event's value) */
+#define AGNES_VMSG_NONE 0u
+#define AGNES_VMSG_TIMEOUT_PREVOTE 1u   /* Timeout{r, Prevote}   (arm 6, :196)  */
+#define AGNES_VMSG_TIMEOUT_PRECOMMIT 2u /* Timeout{r, Precommit} (arm 12, :208) */
+#define AGNES_VMSG_PRECOMMIT_NIL 3u     /* Vote precommit(r, None)   (:197)     */
+#define AGNES_VMSG_PRECOMMIT_VALUE 4u   /* Vote precommit(r, Some v) (:198)     */
+#define AGNES_VMSG_DECISION 5u          /* Decision{r, v}            (:211)     */
+#define AGNES_VMSG_NEW_ROUND 6u         /* NewRound(r)               (:210)     */
+#define AGNES_VMSG_NEW_ROUND_TIMEOUT_PRECOMMIT 7u /* RoundSkip then PrecommitAny   */
+#define AGNES_VMSG_NEW_ROUND_DECISION 8u          /* RoundSkip then PrecommitValue */
+
+/* ---------------------------------------------------------------------------
+ * Batch configuration
+ * ------------------------------------------------------------------------- */
+#define AGNES_MODE_REFERENCE 0u /* every vote counts (round_votes.rs:48-56; test :120-122 relies on it) */
+#define AGNES_MODE_DEDUP 1u     /* first vote of (instance, round, type, validator) wins; rest REJECTED */
+
+#define AGNES_FLAG_ROUND_SKIP 0x1u      /* emit RoundSkip (+1/3) — producer absent in the reference */
+#define AGNES_FLAG_STATE_MACHINE 0x2u   /* apply events to per-instance State (apply_msg :61-69)     */
+#define AGNES_FLAG_DISTINCT_VALUES 0x4u /* compare value labels in prevote() (:241); default: ZST, all equal */
+
+typedef struct agnes_config {
+    uint32_t mode;       /* AGNES_MODE_*                                            */
+    uint32_t flags;      /* AGNES_FLAG_*                                            */
+    uint32_t max_rounds; /* votes with round >= max_rounds are INVALID (1..256)      */
+    uint32_t reserved;
+} agnes_config;
+
+/* Canonical structure-of-arrays vote batch: 14 bytes per vote.
+ * Votes of one instance are CONTIGUOUS and in arrival order:
+ *   instance i owns votes [offsets[i], offsets[i+1]).
+ * Each instance is the reference's per-height executor pair (VoteExecutor +
+ * State), one independent VoteExecutor per (instance, round). */
+typedef struct agnes_vote_batch {
+    const uint32_t* instance;  /* n_votes — must equal the owning segment's index  */
+    const uint8_t* round;      /* n_votes — Vote.round                             */
+    const uint8_t* type;       /* n_votes — Vote.typ                               */
+    const uint32_t* value;     /* n_votes — Vote.value (AGNES_NIL = None)          */
+    const uint32_t* validator; /* n_votes — index into the instance's power set    */
+    const uint64_t* offsets;   /* n_instances + 1                                  */
+    const uint32_t* instance_set; /* optional n_instances; NULL -> instance % n_sets */
+    const int64_t* weight;     /* optional n_votes: caller-supplied weight (vote_executor.rs:20)
+                                   instead of the power-table gather                */
+    uint64_t n_votes;
+    uint32_t n_instances;
+    uint32_t reserved;
+} agnes_vote_batch;
+
+/* ---------------------------------------------------------------------------
+ * Scalar mirror of the reference API (the shape a Rust FFI binds; runs on the
+ * GPU through the batch engine — there is no CPU implementation behind it).
+ * ------------------------------------------------------------------------- */
+typedef struct agnes_ve agnes_ve;
+
+/* VoteExecutor::new(height, total_weight)            vote_executor.rs:13-16 */
+agnes_ve* agnes_ve_new(int64_t height, int64_t total_weight);
+/* VoteExecutor::apply(&mut self, vote, weight) -> Option<Event>
+ * vote_executor.rs:20-23.  Returns 1 and fills *out on Some(event), 0 on None,
+ * <0 on error.  Every round of vote->round gets its own tally (the reference
+ * keeps only round 0, vote_executor.rs:9,14 "TODO: more rounds"; rounds must be
+ * 0..255). */
+int agnes_ve_apply(agnes_ve* ve, const agnes_vote* vote, int64_t weight, agnes_event* out);
+void agnes_ve_free(agnes_ve* ve);
+
+/* State::new(height)                                  state_machine.rs:35-43 */
+void agnes_state_init(int64_t height, agnes_state* out);
+/* State::apply(self, round, event) -> (State, Option<Message>)
+ * state_machine.rs:174-214.  Returns 1 when a message was produced, 0 if
+ * None, <0 on error.  Runs on the GPU. */
+int agnes_state_apply(const agnes_state* in, int64_t round, const agnes_event* ev, uint32_t flags,
+                      agnes_state* out, agnes_message* msg);
+
+/* ---------------------------------------------------------------------------
+ * Batch engine (the hot path).  All array pointers passed to agnes_tally /
+ * agnes_apply_events are DEVICE pointers on the context's device.
+ * ------------------------------------------------------------------------- */
+typedef struct agnes_ctx agnes_ctx;
+
+int agnes_ctx_create(int device, agnes_ctx** out);
+void agnes_ctx_destroy(agnes_ctx* ctx);
+int agnes_ctx_device(const agnes_ctx* ctx);
+
+/* Upload the validator power table (Validator.voting_power, validators.rs:5-8)
+ * as int64 power[n_sets][n_vals] (HOST pointer).  totals (HOST, optional,
+ * n_sets) is the total_weight of VoteExecutor::new (vote_executor.rs:13); NULL
+ * means the wrapping sum of the set's powers. */
+int agnes_upload_power(agnes_ctx* ctx, const int64_t* power, uint32_t n_sets, uint32_t n_vals,
+                       const int64_t* totals);
+
+/* Tally a batch: per-vote codes (device, n_votes bytes); optional per-instance
+ * State array (device, n_instances, read and written in place) used when
+ * AGNES_FLAG_STATE_MACHINE is set.  `stream` is a hipStream_t (NULL = default).
+ * Asynchronous: returns after enqueueing.  Bad votes never fail the call; they
+ * get AGNES_CODE_INVALID and are counted by agnes_last_error_count. */
+int agnes_tally(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
+                uint8_t* codes, agnes_state* states, void* stream);
+
+/* Number of votes coded AGNES_CODE_INVALID by the most recent agnes_tally on
+ * this context (synchronises the context's stream). */
+int agnes_last_error_count(agnes_ctx* ctx, uint64_t* out);
+
+/* Bytes of dynamic LDS one wave needs for cfg with n_vals validators per set;
+ * > 0 on success, < 0 when the configuration is unsupported. */
+int64_t agnes_lds_bytes_per_wave(const agnes_config* cfg, uint32_t n_vals);
+
+/* Batched State::apply over explicit event lists (state_machine.rs:183-322):
+ * instance i applies events [ev_offsets[i], ev_offsets[i+1]) in order to
+ * states[i]; msgs[k] receives the Option<Message> of event k (kind 0 = None).
+ * All pointers DEVICE.  One instance per lane. */
+int agnes_apply_events(agnes_ctx* ctx, agnes_state* states, uint32_t n_instances,
+                       const uint64_t* ev_offsets, const agnes_event* events, agnes_message* msgs,
+                       uint32_t flags, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Synthetic workload generator (counter-based splitmix64; identical on host
+ * and device, see agnes_amd/csrc/agnes_gen.h).  Not part of the hot path.
+ * ------------------------------------------------------------------------- */
+typedef struct agnes_gen_params {
+    uint64_t seed;
+    uint32_t n_instances;
+    uint32_t n_vals;          /* validators per set                             */
+    uint32_t rounds_min;      /* rounds per instance ~ U[rounds_min, rounds_max] */
+    uint32_t rounds_max;
+    uint32_t nil_permille;    /* base votes that are nil                         */
+    uint32_t dup_permille;    /* extra exact duplicates per round (of 2*n_vals)  */
+    uint32_t equiv_permille;  /* extra equivocating votes per round              */
+    uint32_t higher_permille; /* extra votes tagged round+1 per round            */
+    uint32_t order;           /* AGNES_ORDER_*                                   */
+    uint32_t instance_base;   /* global id of local instance 0 (sharding)        */
+} agnes_gen_params;
+
+#define AGNES_ORDER_SHUFFLED 0u /* random permutation of each round's votes       */
+#define AGNES_ORDER_PHASED 1u   /* each round: shuffled prevotes, then precommits */
+#define AGNES_ORDER_SORTED 2u   /* each round: prevotes by validator, then precommits */
+
+/* votes per instance (all instances of one params share the per-round count) */
+uint64_t agnes_gen_instance_votes(const agnes_gen_params* p, uint32_t local_instance);
+/* host: offsets[n_instances+1] */
+int agnes_gen_offsets(const agnes_gen_params* p, uint64_t* offsets);
+/* device: fill the SoA columns of a batch whose offsets are already on device */
+int agnes_gen_votes_device(agnes_ctx* ctx, const agnes_gen_params* p, const uint64_t* d_offsets,
+                           uint64_t n_votes, uint32_t* instance, uint8_t* round, uint8_t* type,
+                           uint32_t* value, uint32_t* validator, void* stream);
+
+#define AGNES_POWER_UNIFORM 0u /* U[lo, hi]                                   */
+#define AGNES_POWER_ZIPF 1u    /* floor(hi / (rank+1)^1.1), rank a hashed permutation */
+#define AGNES_POWER_EQUAL 2u   /* all == lo                                   */
+/* host: power[n_sets][n_vals] */
+int agnes_gen_power(uint64_t seed, uint32_t n_sets, uint32_t n_vals, uint32_t kind, int64_t lo,
+                    int64_t hi, int64_t* power);
+
+/* ABI probe */
+uint32_t agnes_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* AGNES_H */
