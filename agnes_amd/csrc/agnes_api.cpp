@@ -1,0 +1,412 @@
+/*
+ * agnes_api.cpp — host side of the C ABI declared in include/agnes.h.
+ *
+ * Owns device residency (power tables, per-set quorum constants, error
+ * counters) and enqueues the gfx950 kernels of agnes_kernels.hip.  Every
+ * compute entry point — including the scalar mirrors of VoteExecutor::apply
+ * and State::apply — runs on the GPU; without a visible device they return
+ * AGNES_E_NODEVICE.  Nothing here throws across the boundary.
+ */
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/agnes.h"
+#include "agnes_gen_host.h"
+#include "agnes_internal.h"
+
+struct agnes_ctx {
+    int device = 0;
+    int num_cus = 256;
+    int64_t* d_power = nullptr;
+    uint32_t* d_power32 = nullptr;
+    agnes_set_info* d_sets = nullptr;
+    uint32_t n_sets = 0;
+    uint32_t n_vals = 0;
+    unsigned long long* d_err = nullptr;
+    hipStream_t last_stream = nullptr;
+};
+
+namespace {
+
+int status_of(hipError_t e) {
+    if (e == hipSuccess) return AGNES_OK;
+    if (e == hipErrorOutOfMemory) return AGNES_E_NOMEM;
+    if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return AGNES_E_NODEVICE;
+    return AGNES_E_DEVICE;
+}
+
+#define AGNES_TRY(expr)                              \
+    do {                                             \
+        hipError_t e_ = (expr);                      \
+        if (e_ != hipSuccess) return status_of(e_);  \
+    } while (0)
+
+void free_power(agnes_ctx* c) {
+    if (c->d_power) (void)hipFree(c->d_power);
+    if (c->d_power32) (void)hipFree(c->d_power32);
+    if (c->d_sets) (void)hipFree(c->d_sets);
+    c->d_power = nullptr;
+    c->d_power32 = nullptr;
+    c->d_sets = nullptr;
+    c->n_sets = c->n_vals = 0;
+}
+
+int64_t wadd(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+
+/* quorum constants of one set (see agnes_internal.h) */
+agnes_set_info set_info(const int64_t* pw, uint32_t n_vals, int64_t total) {
+    agnes_set_info si{};
+    si.total = total;
+    int64_t mn = 0, mx = 0;
+    for (uint32_t v = 0; v < n_vals; ++v) {
+        mn = v == 0 || pw[v] < mn ? pw[v] : mn;
+        mx = v == 0 || pw[v] > mx ? pw[v] : mx;
+    }
+    const bool fast = mn >= 0 && mx < (1ll << 31) && total >= 0 && total <= INT64_MAX / 2;
+    si.fast = fast ? 1u : 0u;
+    if (fast) {
+        const uint64_t t2 = (uint64_t)(2 * total) / 3u, t1 = (uint64_t)total / 3u;
+        si.q2 = t2 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)t2;
+        si.q1 = t1 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)t1;
+        si.maxpow = (uint32_t)mx;
+    }
+    return si;
+}
+
+bool cfg_ok(const agnes_config* cfg) {
+    return cfg && cfg->max_rounds >= 1 && cfg->max_rounds <= 256 && cfg->mode <= AGNES_MODE_DEDUP &&
+           (cfg->flags & ~(AGNES_FLAG_ROUND_SKIP | AGNES_FLAG_STATE_MACHINE |
+                           AGNES_FLAG_DISTINCT_VALUES)) == 0;
+}
+
+/* ---- scalar mirror: one process-wide context ---- */
+std::mutex g_mu;
+agnes_ctx* g_ctx = nullptr;
+
+int scalar_ctx(agnes_ctx** out) {
+    if (!g_ctx) {
+        const char* d = std::getenv("AGNES_DEVICE");
+        int rc = agnes_ctx_create(d ? std::atoi(d) : 0, &g_ctx);
+        if (rc != AGNES_OK) {
+            g_ctx = nullptr;
+            return rc;
+        }
+    }
+    *out = g_ctx;
+    return AGNES_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+uint32_t agnes_abi_version(void) { return AGNES_ABI_VERSION; }
+
+int agnes_ctx_create(int device, agnes_ctx** out) {
+    if (!out) return AGNES_E_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return AGNES_E_NODEVICE;
+    if (device < 0 || device >= n) return AGNES_E_INVALID;
+    AGNES_TRY(hipSetDevice(device));
+    agnes_ctx* c = new (std::nothrow) agnes_ctx();
+    if (!c) return AGNES_E_NOMEM;
+    c->device = device;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+        cus > 0)
+        c->num_cus = cus;
+    hipError_t e = hipMalloc(&c->d_err, sizeof(unsigned long long));
+    if (e != hipSuccess) {
+        delete c;
+        return status_of(e);
+    }
+    (void)hipMemset(c->d_err, 0, sizeof(unsigned long long));
+    *out = c;
+    return AGNES_OK;
+}
+
+void agnes_ctx_destroy(agnes_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    free_power(c);
+    if (c->d_err) (void)hipFree(c->d_err);
+    delete c;
+}
+
+int agnes_ctx_device(const agnes_ctx* c) { return c ? c->device : AGNES_E_INVALID; }
+
+int agnes_upload_power(agnes_ctx* c, const int64_t* power, uint32_t n_sets, uint32_t n_vals,
+                       const int64_t* totals) {
+    if (!c || n_sets == 0 || (n_vals && !power) || (n_vals == 0 && !totals)) return AGNES_E_INVALID;
+    AGNES_TRY(hipSetDevice(c->device));
+    AGNES_TRY(hipDeviceSynchronize());
+    free_power(c);
+    const uint64_t n = (uint64_t)n_sets * n_vals;
+    std::vector<agnes_set_info> sets(n_sets);
+    std::vector<uint32_t> p32(n);
+    for (uint32_t s = 0; s < n_sets; ++s) {
+        const int64_t* row = power + (uint64_t)s * n_vals;
+        int64_t t = 0;
+        if (totals) t = totals[s];
+        else
+            for (uint32_t v = 0; v < n_vals; ++v) t = wadd(t, row[v]);
+        sets[s] = set_info(row, n_vals, t);
+        for (uint32_t v = 0; v < n_vals; ++v) p32[(uint64_t)s * n_vals + v] = (uint32_t)row[v];
+    }
+    const size_t pb = (size_t)(n ? n : 1);
+    AGNES_TRY(hipMalloc(&c->d_power, pb * sizeof(int64_t)));
+    AGNES_TRY(hipMalloc(&c->d_power32, pb * sizeof(uint32_t)));
+    AGNES_TRY(hipMalloc(&c->d_sets, n_sets * sizeof(agnes_set_info)));
+    if (n) {
+        AGNES_TRY(hipMemcpy(c->d_power, power, n * sizeof(int64_t), hipMemcpyHostToDevice));
+        AGNES_TRY(hipMemcpy(c->d_power32, p32.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
+    AGNES_TRY(hipMemcpy(c->d_sets, sets.data(), n_sets * sizeof(agnes_set_info),
+                        hipMemcpyHostToDevice));
+    c->n_sets = n_sets;
+    c->n_vals = n_vals;
+    return AGNES_OK;
+}
+
+int64_t agnes_lds_bytes_per_wave(const agnes_config* cfg, uint32_t n_vals) {
+    if (!cfg_ok(cfg)) return AGNES_E_INVALID;
+    const int64_t b = agnes_lds_per_wave(cfg->mode, cfg->flags, cfg->max_rounds, n_vals);
+    return b > AGNES_MAX_LDS_PER_WAVE ? AGNES_E_UNSUPPORTED : b;
+}
+
+static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b,
+                      uint8_t* codes, agnes_state* states, agnes_carry_rec* carry,
+                      const agnes_set_info* sets, uint32_t n_sets, hipStream_t st) {
+    if (!c || !cfg_ok(cfg) || !b || !b->offsets) return AGNES_E_INVALID;
+    if (b->n_votes && (!codes || !b->instance || !b->round || !b->type || !b->value ||
+                       !b->validator))
+        return AGNES_E_INVALID;
+    if ((cfg->flags & AGNES_FLAG_STATE_MACHINE) && !states) return AGNES_E_INVALID;
+    const int64_t lpw = agnes_lds_bytes_per_wave(cfg, c->n_vals);
+    if (lpw < 0) return (int)lpw;
+    AGNES_TRY(hipSetDevice(c->device));
+    AGNES_TRY(hipMemsetAsync(c->d_err, 0, sizeof(unsigned long long), st));
+    agnes_tally_args a;
+    std::memset(&a, 0, sizeof(a));
+    a.vb = *b;
+    a.power = c->d_power;
+    a.power32 = c->d_power32;
+    a.sets = sets;
+    a.n_sets = n_sets;
+    a.n_vals = c->n_vals;
+    a.max_rounds = cfg->max_rounds;
+    a.flags = cfg->flags;
+    a.codes = codes;
+    a.states = (cfg->flags & AGNES_FLAG_STATE_MACHINE) ? states : nullptr;
+    a.carry = carry;
+    a.n_invalid = c->d_err;
+    c->last_stream = st;
+    return status_of(agnes_launch_tally(&a, cfg->mode, c->num_cus, st));
+}
+
+int agnes_tally(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint8_t* codes,
+                agnes_state* states, void* stream) {
+    if (!c) return AGNES_E_INVALID;
+    return tally_impl(c, cfg, b, codes, states, nullptr, c->d_sets, c->n_sets,
+                      (hipStream_t)stream);
+}
+
+int agnes_last_error_count(agnes_ctx* c, uint64_t* out) {
+    if (!c || !out) return AGNES_E_INVALID;
+    AGNES_TRY(hipSetDevice(c->device));
+    AGNES_TRY(hipStreamSynchronize(c->last_stream));
+    unsigned long long v = 0;
+    AGNES_TRY(hipMemcpy(&v, c->d_err, sizeof(v), hipMemcpyDeviceToHost));
+    *out = v;
+    return AGNES_OK;
+}
+
+int agnes_apply_events(agnes_ctx* c, agnes_state* states, uint32_t n, const uint64_t* off,
+                       const agnes_event* ev, agnes_message* msgs, uint32_t flags, void* stream) {
+    if (!c || (n && (!states || !off))) return AGNES_E_INVALID;
+    AGNES_TRY(hipSetDevice(c->device));
+    c->last_stream = (hipStream_t)stream;
+    return status_of(agnes_launch_apply_events(states, n, off, ev, msgs, flags, (hipStream_t)stream));
+}
+
+/* ---------------- generator ---------------- */
+
+uint64_t agnes_gen_instance_votes(const agnes_gen_params* p, uint32_t i) {
+    if (!agnes_gen_params_ok(p)) return 0;
+    return agnes_gen_host_instance_votes(p, i);
+}
+
+int agnes_gen_offsets(const agnes_gen_params* p, uint64_t* offsets) {
+    return agnes_gen_host_offsets(p, offsets);
+}
+
+int agnes_gen_power(uint64_t seed, uint32_t n_sets, uint32_t n_vals, uint32_t kind, int64_t lo,
+                    int64_t hi, int64_t* power) {
+    return agnes_gen_host_power(seed, n_sets, n_vals, kind, lo, hi, power);
+}
+
+int agnes_gen_votes_device(agnes_ctx* c, const agnes_gen_params* p, const uint64_t* d_offsets,
+                           uint64_t n_votes, uint32_t* instance, uint8_t* round, uint8_t* type,
+                           uint32_t* value, uint32_t* validator, void* stream) {
+    if (!c || !agnes_gen_params_ok(p) || !d_offsets) return AGNES_E_INVALID;
+    if (n_votes && (!instance || !round || !type || !value || !validator)) return AGNES_E_INVALID;
+    AGNES_TRY(hipSetDevice(c->device));
+    c->last_stream = (hipStream_t)stream;
+    return status_of(agnes_launch_gen(p, d_offsets, n_votes, instance, round, type, value,
+                                      validator, (hipStream_t)stream));
+}
+
+/* ---------------- scalar mirror ---------------- */
+
+struct agnes_ve {
+    int64_t height;
+    int64_t total;
+    unsigned char* dev; /* one allocation, layout below */
+};
+
+/* device block of a VoteExecutor: [set_info 24][carry 2x24][offsets 16][weight 8]
+ * [instance 4][value 4][validator 4][round 1][type 1][code 1][pad] */
+namespace {
+constexpr size_t VE_SET = 0, VE_CARRY = 24, VE_OFF = 72, VE_W = 88, VE_INST = 96, VE_VAL = 100,
+                 VE_VIDX = 104, VE_ROUND = 108, VE_TYPE = 109, VE_CODE = 110, VE_BYTES = 128;
+}
+
+agnes_ve* agnes_ve_new(int64_t height, int64_t total_weight) {
+    std::lock_guard<std::mutex> g(g_mu);
+    agnes_ctx* c = nullptr;
+    if (scalar_ctx(&c) != AGNES_OK) return nullptr;
+    if (hipSetDevice(c->device) != hipSuccess) return nullptr;
+    agnes_ve* ve = new (std::nothrow) agnes_ve();
+    if (!ve) return nullptr;
+    ve->height = height;
+    ve->total = total_weight;
+    if (hipMalloc(&ve->dev, VE_BYTES) != hipSuccess) {
+        delete ve;
+        return nullptr;
+    }
+    unsigned char host[VE_BYTES];
+    std::memset(host, 0, sizeof(host));
+    agnes_set_info si = set_info(nullptr, 0, total_weight);
+    si.fast = 0; /* caller weights: always the wrapping i64 path */
+    std::memcpy(host + VE_SET, &si, sizeof(si));
+    const uint64_t off[2] = {0, 1};
+    std::memcpy(host + VE_OFF, off, sizeof(off));
+    if (hipMemcpy(ve->dev, host, VE_BYTES, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(ve->dev);
+        delete ve;
+        return nullptr;
+    }
+    return ve;
+}
+
+int agnes_ve_apply(agnes_ve* ve, const agnes_vote* vote, int64_t weight, agnes_event* out) {
+    if (!ve || !vote || vote->typ > 1) return AGNES_E_INVALID;
+    std::lock_guard<std::mutex> g(g_mu);
+    agnes_ctx* c = nullptr;
+    int rc = scalar_ctx(&c);
+    if (rc != AGNES_OK) return rc;
+    AGNES_TRY(hipSetDevice(c->device));
+    /* the reference executor ignores vote.round: one RoundVotes at round 0
+     * (vote_executor.rs:9,14) — so the vote is tallied as round 0 */
+    unsigned char stage[VE_BYTES - VE_W];
+    std::memset(stage, 0, sizeof(stage));
+    const uint32_t inst = 0, vidx = 0;
+    std::memcpy(stage + (VE_W - VE_W), &weight, 8);
+    std::memcpy(stage + (VE_INST - VE_W), &inst, 4);
+    std::memcpy(stage + (VE_VAL - VE_W), &vote->value, 4);
+    std::memcpy(stage + (VE_VIDX - VE_W), &vidx, 4);
+    stage[VE_TYPE - VE_W] = vote->typ;
+    AGNES_TRY(hipMemcpy(ve->dev + VE_W, stage, VE_CODE - VE_W, hipMemcpyHostToDevice));
+    agnes_vote_batch b;
+    std::memset(&b, 0, sizeof(b));
+    b.instance = (const uint32_t*)(ve->dev + VE_INST);
+    b.round = ve->dev + VE_ROUND;
+    b.type = ve->dev + VE_TYPE;
+    b.value = (const uint32_t*)(ve->dev + VE_VAL);
+    b.validator = (const uint32_t*)(ve->dev + VE_VIDX);
+    b.offsets = (const uint64_t*)(ve->dev + VE_OFF);
+    b.weight = (const int64_t*)(ve->dev + VE_W);
+    b.n_votes = 1;
+    b.n_instances = 1;
+    agnes_config cfg = {AGNES_MODE_REFERENCE, 0u, 1u, 0u};
+    const uint32_t saved_nv = c->n_vals;
+    c->n_vals = 0; /* no power table: validator unused */
+    rc = tally_impl(c, &cfg, &b, ve->dev + VE_CODE, nullptr, (agnes_carry_rec*)(ve->dev + VE_CARRY),
+                    (const agnes_set_info*)(ve->dev + VE_SET), 1u, nullptr);
+    c->n_vals = saved_nv;
+    if (rc != AGNES_OK) return rc;
+    unsigned char back[VE_BYTES];
+    AGNES_TRY(hipMemcpy(back, ve->dev, VE_BYTES, hipMemcpyDeviceToHost));
+    const uint32_t code = back[VE_CODE] & AGNES_CODE_EVENT_MASK;
+    if (code == AGNES_CODE_NONE) return 0;
+    if (code > AGNES_CODE_PRECOMMIT_VALUE) return AGNES_E_DEVICE;
+    agnes_carry_rec cr;
+    std::memcpy(&cr, back + VE_CARRY + vote->typ * sizeof(agnes_carry_rec), sizeof(cr));
+    if (out) {
+        std::memset(out, 0, sizeof(*out));
+        out->kind = (uint8_t)(code + 3u); /* CODE_POLKA_ANY(1) .. -> EV_POLKA_ANY(4) .. */
+        out->round = vote->round;         /* apply_event(v.round, ..), consensus_executor.rs:68 */
+        out->value = (code == AGNES_CODE_POLKA_VALUE || code == AGNES_CODE_PRECOMMIT_VALUE)
+                         ? cr.value
+                         : 0u;
+    }
+    return 1;
+}
+
+void agnes_ve_free(agnes_ve* ve) {
+    if (!ve) return;
+    std::lock_guard<std::mutex> g(g_mu);
+    if (g_ctx) (void)hipSetDevice(g_ctx->device);
+    if (ve->dev) (void)hipFree(ve->dev);
+    delete ve;
+}
+
+void agnes_state_init(int64_t height, agnes_state* out) {
+    if (!out) return;
+    std::memset(out, 0, sizeof(*out)); /* State::new, state_machine.rs:35-43 */
+    out->height = height;
+    out->round = 0;
+    out->step = AGNES_STEP_NEW_ROUND;
+}
+
+int agnes_state_apply(const agnes_state* in, int64_t round, const agnes_event* ev, uint32_t flags,
+                      agnes_state* out, agnes_message* msg) {
+    if (!in || !ev || !out) return AGNES_E_INVALID;
+    std::lock_guard<std::mutex> g(g_mu);
+    agnes_ctx* c = nullptr;
+    int rc = scalar_ctx(&c);
+    if (rc != AGNES_OK) return rc;
+    AGNES_TRY(hipSetDevice(c->device));
+    struct Blk {
+        agnes_state s;
+        agnes_event e;
+        uint64_t off[2];
+        agnes_message m;
+    } h;
+    std::memset(&h, 0, sizeof(h));
+    h.s = *in;
+    h.e = *ev;
+    h.e.round = round;
+    h.off[0] = 0;
+    h.off[1] = 1;
+    Blk* d = nullptr;
+    AGNES_TRY(hipMalloc(&d, sizeof(Blk)));
+    hipError_t e = hipMemcpy(d, &h, sizeof(Blk), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = agnes_launch_apply_events(&d->s, 1u, d->off, &d->e, &d->m, flags, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(&h, d, sizeof(Blk), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return status_of(e);
+    *out = h.s;
+    if (msg) *msg = h.m;
+    return h.m.kind != AGNES_MSG_NONE ? 1 : 0;
+}
+
+} // extern "C"

@@ -1,0 +1,65 @@
+/*
+ * agnes_internal.h — engine-internal declarations shared by the kernels
+ * (agnes_kernels.hip) and the host C ABI (agnes_api.cpp).
+ */
+#ifndef AGNES_INTERNAL_H
+#define AGNES_INTERNAL_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/agnes.h"
+
+/* Per power set, precomputed on the host at upload (agnes_upload_power).
+ * fast == 1 when every power is in [0, 2^31) and 0 <= total <= i64::MAX/2:
+ * then, for sums s < 2^31, `3*s > 2*total` (round_votes.rs:32) is exactly
+ * `s > q2` with q2 = min(floor(2*total/3), 2^32-1), and the +1/3 RoundSkip test
+ * `3*s > total` is `s > q1`, q1 = min(floor(total/3), 2^32-1). */
+typedef struct agnes_set_info {
+    int64_t total;
+    uint32_t q2;
+    uint32_t q1;
+    uint32_t maxpow;
+    uint32_t fast;
+} agnes_set_info;
+
+/* Carried VoteCount of one (instance, round, type): round_votes.rs:15-19 */
+typedef struct agnes_carry_rec {
+    int64_t value_w;
+    int64_t nil_w;
+    uint32_t value;
+    uint32_t pad;
+} agnes_carry_rec;
+
+typedef struct agnes_tally_args {
+    agnes_vote_batch vb;
+    const int64_t* power;       /* [n_sets][n_vals] */
+    const uint32_t* power32;    /* low 32 bits, used by fast instances */
+    const agnes_set_info* sets; /* [n_sets] */
+    uint32_t n_sets;
+    uint32_t n_vals;
+    uint32_t max_rounds;
+    uint32_t flags;
+    uint8_t* codes;
+    agnes_state* states;
+    agnes_carry_rec* carry; /* optional [n_instances][2*max_rounds], in/out */
+    unsigned long long* n_invalid;
+} agnes_tally_args;
+
+/* bytes of dynamic LDS one wave uses */
+int64_t agnes_lds_per_wave(uint32_t mode, uint32_t flags, uint32_t max_rounds, uint32_t n_vals);
+
+/* launchers (agnes_kernels.hip) — enqueue only */
+hipError_t agnes_launch_tally(const agnes_tally_args* a, uint32_t mode, int num_cus,
+                              hipStream_t stream);
+hipError_t agnes_launch_apply_events(agnes_state* states, uint32_t n, const uint64_t* off,
+                                     const agnes_event* ev, agnes_message* msgs, uint32_t flags,
+                                     hipStream_t stream);
+hipError_t agnes_launch_gen(const agnes_gen_params* p, const uint64_t* d_offsets, uint64_t n_votes,
+                            uint32_t* instance, uint8_t* round, uint8_t* type, uint32_t* value,
+                            uint32_t* validator, hipStream_t stream);
+
+#define AGNES_WAVES_PER_BLOCK 4
+#define AGNES_MAX_LDS_PER_WAVE (36 * 1024)
+
+#endif

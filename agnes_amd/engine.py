@@ -1,0 +1,180 @@
+"""Batch engine: device residency (torch tensors as HIP allocations) + the C ABI.
+
+The hot path is `Engine.tally`: one call tallies a whole batch of instances on
+the GPU (agnes_tally).  PyTorch is only plumbing here — device memory,
+streams, torch.distributed — never the compute.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import abi
+from .lib import AgnesError, check, load
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _stream_handle(stream) -> C.c_void_p:
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return C.c_void_p(stream.cuda_stream)
+
+
+@dataclass
+class DeviceBatch:
+    """Canonical 14-byte SoA vote batch resident in HBM (include/agnes.h)."""
+
+    instance: torch.Tensor   # int32 view of u32
+    round: torch.Tensor      # uint8
+    type: torch.Tensor       # uint8
+    value: torch.Tensor      # int32 view of u32 (AGNES_NIL = -1)
+    validator: torch.Tensor  # int32 view of u32
+    offsets: torch.Tensor    # int64 view of u64, n_instances + 1
+    instance_set: Optional[torch.Tensor] = None
+    weight: Optional[torch.Tensor] = None  # int64
+    n_votes: int = 0
+
+    @property
+    def n_instances(self) -> int:
+        return self.offsets.numel() - 1
+
+    @property
+    def device(self) -> torch.device:
+        return self.offsets.device
+
+    def c(self) -> abi.VoteBatch:
+        return abi.VoteBatch(self.instance.data_ptr(), self.round.data_ptr(),
+                             self.type.data_ptr(), self.value.data_ptr(),
+                             self.validator.data_ptr(), self.offsets.data_ptr(),
+                             None if self.instance_set is None else self.instance_set.data_ptr(),
+                             None if self.weight is None else self.weight.data_ptr(),
+                             self.n_votes, self.n_instances, 0)
+
+    @staticmethod
+    def from_host(hb, device) -> "DeviceBatch":
+        """hb: any object with numpy fields instance/round/type/value/validator/offsets."""
+        def t(a, dt):
+            return torch.from_numpy(np.ascontiguousarray(a).view(dt)).to(device)
+        return DeviceBatch(
+            t(hb.instance, np.int32), t(hb.round, np.uint8), t(hb.type, np.uint8),
+            t(hb.value, np.int32), t(hb.validator, np.int32), t(hb.offsets, np.int64),
+            None if getattr(hb, "instance_set", None) is None else t(hb.instance_set, np.int32),
+            None if getattr(hb, "weight", None) is None else t(hb.weight, np.int64),
+            int(hb.offsets[-1]))
+
+    def to_host(self) -> dict:
+        def h(x, dt):
+            return x.cpu().numpy().view(dt)
+        return dict(instance=h(self.instance, np.uint32), round=h(self.round, np.uint8),
+                    type=h(self.type, np.uint8), value=h(self.value, np.uint32),
+                    validator=h(self.validator, np.uint32), offsets=h(self.offsets, np.uint64))
+
+
+def states_to_device(states: np.ndarray, device) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(states, dtype=abi.STATE_DTYPE).view(np.uint8)).to(device)
+
+
+def states_to_host(t: torch.Tensor) -> np.ndarray:
+    return t.cpu().numpy().view(abi.STATE_DTYPE).copy()
+
+
+class Engine:
+    """One context per GPU (agnes_ctx)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        self.device_index = device
+        self.device = torch.device("cuda", device)
+        h = C.c_void_p()
+        check(self.lib.agnes_ctx_create(device, C.byref(h)), "agnes_ctx_create")
+        self.ctx = h
+        self.n_sets = 0
+        self.n_vals = 0
+
+    def close(self):
+        if self.ctx:
+            self.lib.agnes_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- residency ----------------------------------------------------------
+    def upload_power(self, power: np.ndarray, totals: Optional[np.ndarray] = None):
+        power = np.ascontiguousarray(power, dtype=np.int64)
+        if power.ndim != 2:
+            raise ValueError("power must be [n_sets][n_vals]")
+        tot = None if totals is None else np.ascontiguousarray(totals, dtype=np.int64)
+        check(self.lib.agnes_upload_power(self.ctx, power.ctypes.data, power.shape[0],
+                                          power.shape[1], None if tot is None else tot.ctypes.data),
+              "agnes_upload_power")
+        self.n_sets, self.n_vals = power.shape
+
+    # -- hot path -----------------------------------------------------------
+    def tally(self, cfg: abi.Config, batch: DeviceBatch, codes: torch.Tensor,
+              states: Optional[torch.Tensor] = None, stream=None):
+        if codes.dtype != torch.uint8 or codes.numel() < batch.n_votes:
+            raise ValueError("codes must be a uint8 tensor of n_votes")
+        if states is not None and states.numel() < 64 * batch.n_instances:
+            raise ValueError("states must hold n_instances 64-byte records")
+        b = batch.c()
+        check(self.lib.agnes_tally(self.ctx, C.byref(cfg), C.byref(b), _ptr(codes), _ptr(states),
+                                   _stream_handle(stream)), "agnes_tally")
+
+    def last_error_count(self) -> int:
+        v = C.c_uint64(0)
+        check(self.lib.agnes_last_error_count(self.ctx, C.byref(v)), "agnes_last_error_count")
+        return int(v.value)
+
+    def lds_bytes_per_wave(self, cfg: abi.Config) -> int:
+        return int(self.lib.agnes_lds_bytes_per_wave(C.byref(cfg), self.n_vals))
+
+    def apply_events(self, states: torch.Tensor, ev_offsets: torch.Tensor, events: torch.Tensor,
+                     msgs: torch.Tensor, flags: int = 0, stream=None):
+        n = ev_offsets.numel() - 1
+        check(self.lib.agnes_apply_events(self.ctx, _ptr(states), n, _ptr(ev_offsets),
+                                          _ptr(events), _ptr(msgs), flags,
+                                          _stream_handle(stream)), "agnes_apply_events")
+
+    # -- synthetic workloads ------------------------------------------------
+    def gen_offsets(self, p: abi.GenParams) -> np.ndarray:
+        off = np.zeros(p.n_instances + 1, dtype=np.uint64)
+        check(self.lib.agnes_gen_offsets(C.byref(p), off.ctypes.data), "agnes_gen_offsets")
+        return off
+
+    def gen_batch(self, p: abi.GenParams, stream=None) -> DeviceBatch:
+        off = self.gen_offsets(p)
+        n = int(off[-1])
+        dev = self.device
+        b = DeviceBatch(
+            torch.empty(n, dtype=torch.int32, device=dev),
+            torch.empty(n, dtype=torch.uint8, device=dev),
+            torch.empty(n, dtype=torch.uint8, device=dev),
+            torch.empty(n, dtype=torch.int32, device=dev),
+            torch.empty(n, dtype=torch.int32, device=dev),
+            torch.from_numpy(off.view(np.int64)).to(dev), n_votes=n)
+        check(self.lib.agnes_gen_votes_device(
+            self.ctx, C.byref(p), _ptr(b.offsets), n, _ptr(b.instance), _ptr(b.round),
+            _ptr(b.type), _ptr(b.value), _ptr(b.validator), _stream_handle(stream)),
+            "agnes_gen_votes_device")
+        return b
+
+    def gen_power(self, seed: int, n_sets: int, n_vals: int, kind: int, lo: int,
+                  hi: int) -> np.ndarray:
+        pw = np.zeros((n_sets, n_vals), dtype=np.int64)
+        check(self.lib.agnes_gen_power(seed, n_sets, n_vals, kind, lo, hi, pw.ctypes.data),
+              "agnes_gen_power")
+        return pw
+
+
+__all__ = ["Engine", "DeviceBatch", "AgnesError", "states_to_device", "states_to_host"]

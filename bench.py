@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""Agnes vote-tally bench: votes tallied/sec on MI355X (BASELINE.json metric).
+
+One step = one pass of the fused hot path (agnes_tally: ingest -> weight gather
+-> ordered tally -> quorum -> event -> State::apply) over one batch of
+synthetic votes already resident in HBM, plus the per-height State::new reset
+of the batch's instances (a device copy, timed).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
+
+N > 1: launched by torch.distributed.run, one rank per GPU; instances shard
+with no data-path collective (c2/c4: every rank its own batch = weak scaling;
+c3: the 1M-instance batch split over ranks = strong scaling).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from agnes_amd import abi  # noqa: E402
+from agnes_amd.engine import Engine, states_to_device  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
+BYTES_PER_VOTE = 15            # 14 B canonical SoA in + 1 B code out
+
+WORKLOADS = {
+    # BASELINE configs[1] = C2, timed over 100 batched heights
+    "c2": dict(desc="C2x100: 10k instances x 100 weighted validators x 1 round, 100 heights "
+                    "per batch, 80/20 value/nil, shuffled",
+               gen=dict(n_instances=10_000 * 100, n_vals=100, rounds_min=1, rounds_max=1,
+                        nil_permille=200),
+               power=(abi.POWER_UNIFORM, 1, 1000, 1), mode=abi.MODE_REFERENCE,
+               flags=abi.FLAG_STATE_MACHINE, max_rounds=1, scaling="weak"),
+    "c3": dict(desc="C3: 1M instances x 150 validators x 1..4 rounds, 30% nil, 1024 power sets, "
+                    "sharded over ranks",
+               gen=dict(n_instances=1_000_000, n_vals=150, rounds_min=1, rounds_max=4,
+                        nil_permille=300),
+               power=(abi.POWER_UNIFORM, 1, 1000, 1024), mode=abi.MODE_REFERENCE,
+               flags=abi.FLAG_STATE_MACHINE, max_rounds=4, scaling="strong"),
+    "c4": dict(desc="C4: C3 shape per rank (125k instances), Zipf power, 10% dup + 10% "
+                    "equivocation + 5% next-round votes, DEDUP + RoundSkip",
+               gen=dict(n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4,
+                        nil_permille=300, dup_permille=100, equiv_permille=100,
+                        higher_permille=50),
+               power=(abi.POWER_ZIPF, 1, 1_000_000, 1024), mode=abi.MODE_DEDUP,
+               flags=abi.FLAG_STATE_MACHINE | abi.FLAG_ROUND_SKIP, max_rounds=5, scaling="weak"),
+}
+
+
+def dist_env():
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return rank, world, local
+
+
+def start_states(n: int) -> np.ndarray:
+    """Every instance past NewRoundProposer + Proposal of round 0 (Prevote step)."""
+    return abi.new_states(n, height=1, step=abi.STEP_PREVOTE, round_=0)
+
+
+def make_shard(w: dict, rank: int, world: int):
+    g = dict(w["gen"])
+    if w["scaling"] == "strong":
+        n = g["n_instances"]
+        lo, hi = n * rank // world, n * (rank + 1) // world
+        g["n_instances"], base = hi - lo, lo
+    else:
+        base = rank * g["n_instances"]
+    return abi.gen_params(seed=0xA6E5, instance_base=base, **g), base
+
+
+def cpu_baseline(eng, cfg, batch, power, states0, set_of_instance):
+    """The checker (oracle/, scalar C, pthreads over instances) on the same batch."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as ol  # test infrastructure: the CPU baseline leg only
+    h = batch.to_host()
+    n_inst = len(h["offsets"]) - 1
+    # bounded sample: up to 1M instances (the whole c2 batch: ~2e8 votes, a few s per core-pass)
+    limit = min(n_inst, 1_000_000)
+    off = h["offsets"][: limit + 1]
+    nv = int(off[-1])
+    hb = ol.HostBatch(h["instance"][:nv], h["round"][:nv], h["type"][:nv], h["value"][:nv],
+                      h["validator"][:nv], off.copy(), set_of_instance[:limit].copy())
+    threads = max(1, min(16, os.cpu_count() or 1))
+    best = None
+    for _ in range(3):
+        t0 = time.perf_counter()
+        codes, _, _ = ol.tally(cfg, hb, power, None, states0[:limit], threads=threads)
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    return {"value": nv / best, "unit": "votes/s", "cores": threads, "kind": "port",
+            "sample": f"first {limit} instances ({nv} votes) of the same batch, "
+                      f"oracle/agnes_oracle.c orc_tally_mt, best of 3",
+            "codes_prefix": codes}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--check", action="store_true", help="compare the CPU sample with the GPU codes")
+    args = ap.parse_args()
+
+    rank, world, local = dist_env()
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    w = WORKLOADS[args.config]
+    eng = Engine(local)
+    p, base = make_shard(w, rank, world)
+    kind, lo, hi, n_sets = w["power"]
+    power = eng.gen_power(0xA6E5, n_sets, p.n_vals, kind, lo, hi)
+    eng.upload_power(power)
+    stream = torch.cuda.current_stream()
+    batch = eng.gen_batch(p)
+    # global instance -> power set (instance mod n_sets, with the shard's global ids)
+    set_of = ((np.arange(p.n_instances, dtype=np.int64) + base) % n_sets).astype(np.uint32)
+    batch.instance_set = torch.from_numpy(set_of.view(np.int32)).to(eng.device)
+    cfg = abi.config(w["mode"], w["flags"], w["max_rounds"])
+    st0_host = start_states(p.n_instances)
+    st0 = states_to_device(st0_host, eng.device)
+    states = torch.empty_like(st0)
+    codes = torch.empty(batch.n_votes, dtype=torch.uint8, device=eng.device)
+    torch.cuda.synchronize()
+
+    def step(ev_pair=None):
+        states.copy_(st0, non_blocking=True)          # State::new for this batch of heights
+        if ev_pair:
+            ev_pair[0].record(stream)
+        eng.tally(cfg, batch, codes, states, stream)
+        if ev_pair:
+            ev_pair[1].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if eng.last_error_count() != 0:
+        raise SystemExit("bench batch has invalid votes")
+
+    pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+             for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(pairs[k])
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=eng.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        nv = torch.tensor([batch.n_votes], dtype=torch.int64, device=eng.device)
+        dist.all_reduce(nv)
+        total_votes_step = int(nv.item())
+        dist.barrier()
+    else:
+        total_votes_step = batch.n_votes
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in pairs]))
+
+    if rank == 0:
+        ms_per_step = elapsed * 1e3 / args.steps
+        value = total_votes_step * args.steps / elapsed
+        achieved = BYTES_PER_VOTE * batch.n_votes / (kernel_ms * 1e-3) / 1e9
+        out = {
+            "metric": "votes_tallied_per_sec",
+            "value": value,
+            "unit": "votes/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": w["scaling"],
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic (counter-based splitmix64 streams, agnes_gen.h; random powers)",
+            "config": {"workload": w["desc"], "config": args.config,
+                       "instances_per_gpu": p.n_instances, "validators": p.n_vals,
+                       "votes_per_gpu_per_step": batch.n_votes,
+                       "mode": "DEDUP" if w["mode"] else "REFERENCE",
+                       "flags": w["flags"], "parallelism": f"instance-sharded x{world}"},
+            "kernel_ms": kernel_ms,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "agnes::tally_kernel",
+                         "bytes_per_vote": BYTES_PER_VOTE},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            cb = cpu_baseline(eng, cfg, batch, power, st0_host, set_of)
+            prefix = cb.pop("codes_prefix")
+            if args.check:
+                g = codes[: len(prefix)].cpu().numpy()
+                # the bench codes come from the LAST step; states were reset each step
+                out["cpu_check_equal"] = bool(np.array_equal(g, prefix))
+            out["cpu_baseline"] = cb
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

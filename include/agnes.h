@@ -224,9 +224,11 @@ typedef struct agnes_ve agnes_ve;
 agnes_ve* agnes_ve_new(int64_t height, int64_t total_weight);
 /* VoteExecutor::apply(&mut self, vote, weight) -> Option<Event>
  * vote_executor.rs:20-23.  Returns 1 and fills *out on Some(event), 0 on None,
- * <0 on error.  Every round of vote->round gets its own tally (the reference
- * keeps only round 0, vote_executor.rs:9,14 "TODO: more rounds"; rounds must be
- * 0..255). */
+ * <0 on error.  Exactly the reference executor: ONE RoundVotes for every vote,
+ * vote->round is not consulted by the tally (vote_executor.rs:9,14
+ * "TODO: more rounds"); out->round is set to vote->round, the round
+ * apply_msg passes to State::apply (consensus_executor.rs:68).  The batch
+ * engine (agnes_tally) keeps one executor per (instance, round) instead. */
 int agnes_ve_apply(agnes_ve* ve, const agnes_vote* vote, int64_t weight, agnes_event* out);
 void agnes_ve_free(agnes_ve* ve);
 

@@ -1,0 +1,348 @@
+"""Parity of the HIP engine (through the C ABI) against the CPU checker.
+
+Bar: bit-exact per-vote codes, final per-instance states and invalid counts.
+Oracle-checked sizes run in seconds; the full-size case adds size-independent
+properties (determinism, shard == whole, message/state consistency).
+"""
+import ctypes as C
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle_lib as ol
+from agnes_amd import abi
+from agnes_amd.engine import DeviceBatch, Engine, states_to_device, states_to_host
+from agnes_amd.lib import load
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+REF = json.load(open(os.path.join(GOLD, "reference_tests.json")))
+REGRESS = json.load(open(os.path.join(GOLD, "regress_small.json")))
+EV_BY_NAME = {n: i for i, n in enumerate(abi.EVENT_NAMES)}
+
+
+@pytest.fixture(scope="module")
+def eng():
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+def run_both(eng, cfg, hb, power, totals=None, states=None, threads=8):
+    """Tally hb on the GPU and on the checker; return both results."""
+    if power is not None:
+        eng.upload_power(power, totals)
+    db = DeviceBatch.from_host(hb, eng.device)
+    codes = torch.zeros(max(hb.n_votes, 1), dtype=torch.uint8, device=eng.device)
+    dst = None if states is None else states_to_device(states, eng.device)
+    eng.tally(cfg, db, codes, dst)
+    torch.cuda.synchronize()
+    g_codes = codes[:hb.n_votes].cpu().numpy()
+    g_bad = eng.last_error_count()
+    g_states = None if dst is None else states_to_host(dst)
+    o_codes, o_states, o_bad = ol.tally(cfg, hb, power, totals, states, threads=threads)
+    return (g_codes, g_states, g_bad), (o_codes, o_states, o_bad)
+
+
+def assert_same(g, o):
+    gc, gs, gb = g
+    oc, os_, ob = o
+    if not np.array_equal(gc, oc):
+        bad = np.nonzero(gc != oc)[0]
+        k = bad[0]
+        raise AssertionError(f"{len(bad)} codes differ; first at {k}: gpu {gc[k]:#x} oracle {oc[k]:#x}")
+    assert gb == ob
+    if os_ is not None:
+        assert gs.tobytes() == os_.tobytes()
+
+
+# --------------------------------------------------- the reference's own tests
+
+
+def test_add_votes_through_scalar_mirror():
+    """round_votes.rs:107-132 through agnes_ve_apply (VoteExecutor::apply):
+    thresholds Init, Init, Any, Value  ==  events None, None, PolkaAny, PolkaValue."""
+    L = load()
+    g = REF["add_votes"]
+    ve = L.agnes_ve_new(1, g["total"])
+    assert ve
+    got = []
+    for t, v in g["votes"]:
+        vote = abi.Vote(0, abi.NIL if v is None else v, t)
+        ev = abi.Event()
+        rc = L.agnes_ve_apply(ve, C.byref(vote), g["weight"], C.byref(ev))
+        assert rc in (0, 1)
+        got.append(None if rc == 0 else abi.EVENT_NAMES[ev.kind])
+    L.agnes_ve_free(ve)
+    assert got == [None, None, "PolkaAny", "PolkaValue"]
+
+
+@pytest.mark.parametrize("name", ["c1_value", "c1_nil", "c1_mixed"])
+def test_c1_traces_through_scalar_mirror(name):
+    L = load()
+    g = REF[name]
+    ve = L.agnes_ve_new(1, g["total"])
+    got = []
+    for t, v in g["votes"]:
+        ev = abi.Event()
+        rc = L.agnes_ve_apply(ve, C.byref(abi.Vote(0, abi.NIL if v is None else v, t)),
+                              g["weight"], C.byref(ev))
+        got.append(None if rc == 0 else abi.EVENT_NAMES[ev.kind])
+        if rc == 1 and ev.kind in (abi.EV_POLKA_VALUE, abi.EV_PRECOMMIT_VALUE):
+            assert ev.value == v
+    L.agnes_ve_free(ve)
+    assert got == g["events"]
+
+
+def test_happy_case_through_scalar_mirror():
+    """state_machine.rs:331-345 through agnes_state_apply."""
+    L = load()
+    g = REF["happy_case"]
+    s = abi.StateRec()
+    L.agnes_state_init(g["height"], C.byref(s))
+    for ev, want in zip(g["events"], g["messages"]):
+        e = abi.Event(ev["round"], ev.get("pol_round", 0), ev.get("value", 0), EV_BY_NAME[ev["kind"]])
+        out, m = abi.StateRec(), abi.Message()
+        rc = L.agnes_state_apply(C.byref(s), ev["round"], C.byref(e), 0, C.byref(out), C.byref(m))
+        assert rc == 1
+        assert abi.MSG_NAMES[m.kind] == want["kind"] and m.round == want["round"]
+        assert m.value == want["value"]
+        s = out
+    assert abi.STEP_NAMES[s.step] == "Commit"
+
+
+def test_scalar_mirror_wrapping_i64():
+    """Rust release i64 wrap: 3*w overflows, compare signed (round_votes.rs:32)."""
+    L = load()
+    big = (1 << 62) + 5
+    for total in [4, -7, (1 << 62), -(1 << 63)]:
+        ve = L.agnes_ve_new(1, total)
+        rv = ol.RoundVotes(1, 0, total)
+        for k, (t, v, w) in enumerate([(0, 3, big), (0, abi.NIL, -big), (0, 3, big), (1, 3, 1),
+                                       (1, abi.NIL, (1 << 63) - 1), (0, abi.NIL, 2)]):
+            ev = abi.Event()
+            rc = L.agnes_ve_apply(ve, C.byref(abi.Vote(0, v, t)), w, C.byref(ev))
+            oe, _ = rv.ve_apply(t, v, w)
+            assert (abi.EV_NONE if rc == 0 else ev.kind) == oe, (total, k)
+        L.agnes_ve_free(ve)
+
+
+def test_c1_batch_with_state_machine(eng):
+    """BASELINE config C1: 4 equal-power validators, polka -> decision."""
+    g = REF["c1_value"]
+    n = len(g["votes"])
+    hb = ol.batch_from_lists([0] * n, [0] * n, [t for t, _ in g["votes"]], [v for _, v in g["votes"]],
+                             [k % 4 for k in range(n)], [0, n])
+    st = ol.state_new(1)
+    st, _ = ol.state_apply(st, 0, abi.Event(0, 0, 7, abi.EV_NEW_ROUND_PROPOSER))
+    st, _ = ol.state_apply(st, 0, abi.Event(0, -1, 7, abi.EV_PROPOSAL))
+    st0 = np.frombuffer(bytes(st), dtype=abi.STATE_DTYPE).copy()
+    cfg = abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 1)
+    g_, o_ = run_both(eng, cfg, hb, np.ones((1, 4), np.int64), states=st0)
+    assert_same(g_, o_)
+    msgs = [int(c) >> 4 for c in g_[0]]
+    assert msgs == [0, 0, abi.VMSG_PRECOMMIT_VALUE, 0, 0, 0, abi.VMSG_DECISION, 0]
+
+
+@pytest.mark.parametrize("case", REGRESS, ids=[c["name"] for c in REGRESS])
+def test_regress_fixtures(eng, case):
+    from test_oracle_golden import _states_from_json
+    hb = ol.batch_from_lists(case["instance"], case["round"], case["type"], case["value"],
+                             case["validator"], case["offsets"])
+    cfg = abi.config(case["mode"], case["flags"], case["max_rounds"])
+    st_in = _states_from_json(case["states_in"]) if "states_in" in case else None
+    g, o = run_both(eng, cfg, hb, np.array(case["power"], np.int64),
+                    np.array(case["totals"], np.int64), st_in)
+    assert g[0].tolist() == case["codes"]
+    assert_same(g, o)
+
+
+# ----------------------------------------------------------- generated configs
+
+CONFIGS = {
+    # name: (gen params, power (kind, lo, hi, n_sets), cfg)
+    "c2_small": (dict(n_instances=2000, n_vals=100, rounds_min=1, rounds_max=1, nil_permille=200),
+                 (abi.POWER_UNIFORM, 1, 1000, 1), (abi.MODE_REFERENCE, 0, 1)),
+    "c2_sm": (dict(n_instances=2000, n_vals=100, rounds_min=1, rounds_max=1, nil_permille=200),
+              (abi.POWER_UNIFORM, 1, 1000, 1), (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 1)),
+    "c3_small": (dict(n_instances=3000, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300),
+                 (abi.POWER_UNIFORM, 1, 1000, 1024),
+                 (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 4)),
+    "c4_small": (dict(n_instances=3000, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300,
+                      dup_permille=100, equiv_permille=100, higher_permille=50),
+                 (abi.POWER_ZIPF, 1, 1000000, 1024),
+                 (abi.MODE_DEDUP, abi.FLAG_ROUND_SKIP | abi.FLAG_STATE_MACHINE, 5)),
+    "c4_ref_skip": (dict(n_instances=1500, n_vals=150, rounds_min=1, rounds_max=4,
+                         nil_permille=300, dup_permille=100, equiv_permille=100,
+                         higher_permille=50),
+                    (abi.POWER_ZIPF, 1, 1000000, 64),
+                    (abi.MODE_REFERENCE, abi.FLAG_ROUND_SKIP | abi.FLAG_STATE_MACHINE, 5)),
+    "phased_dedup": (dict(n_instances=1000, n_vals=77, rounds_min=2, rounds_max=3, nil_permille=500,
+                          dup_permille=200, order=abi.ORDER_PHASED),
+                     (abi.POWER_UNIFORM, 0, 50, 7), (abi.MODE_DEDUP, abi.FLAG_STATE_MACHINE, 3)),
+    "sorted_tiny_sets": (dict(n_instances=4000, n_vals=3, rounds_min=1, rounds_max=8,
+                              nil_permille=100, order=abi.ORDER_SORTED),
+                         (abi.POWER_EQUAL, 1, 1, 1),
+                         (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 8)),
+    "wide_huge_powers": (dict(n_instances=500, n_vals=40, rounds_min=1, rounds_max=2,
+                              nil_permille=400, dup_permille=300),
+                         (abi.POWER_UNIFORM, (1 << 61), (1 << 62), 3),
+                         (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 2)),
+    "wide_negative_powers": (dict(n_instances=500, n_vals=40, rounds_min=1, rounds_max=2,
+                                  nil_permille=400),
+                             (abi.POWER_UNIFORM, -30, 100, 3),
+                             (abi.MODE_DEDUP, abi.FLAG_ROUND_SKIP | abi.FLAG_STATE_MACHINE, 3)),
+    "many_rounds": (dict(n_instances=200, n_vals=20, rounds_min=30, rounds_max=60,
+                         nil_permille=300, higher_permille=100),
+                    (abi.POWER_UNIFORM, 1, 100, 5),
+                    (abi.MODE_DEDUP, abi.FLAG_ROUND_SKIP | abi.FLAG_STATE_MACHINE, 61)),
+}
+
+
+def _make(name, seed=0xA6E5):
+    gp, (kind, lo, hi, n_sets), (mode, flags, R) = CONFIGS[name]
+    p = abi.gen_params(seed=seed, **gp)
+    hb = ol.gen_batch(p)
+    power = ol.gen_power(seed, n_sets, gp["n_vals"], kind, lo, hi)
+    return p, hb, power, abi.config(mode, flags, R)
+
+
+def _start_states(n, rounds=1, seed=1):
+    """Instances already past NewRoundProposer + Proposal at round 0 (Prevote step)."""
+    st = abi.new_states(n, 1, abi.STEP_PREVOTE, 0)
+    rng = np.random.default_rng(seed)
+    k = rng.random(n)
+    st["step"][k < 0.1] = abi.STEP_NEW_ROUND
+    st["step"][(k >= 0.1) & (k < 0.15)] = abi.STEP_PRECOMMIT
+    st["round"][k > 0.95] = 1
+    return st
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_generated_parity(eng, name):
+    p, hb, power, cfg = _make(name)
+    states = _start_states(p.n_instances) if cfg.flags & abi.FLAG_STATE_MACHINE else None
+    g, o = run_both(eng, cfg, hb, power, None, states)
+    assert_same(g, o)
+    # the stream must actually exercise the path
+    ev = g[0] & abi.CODE_EVENT_MASK
+    assert (ev != 0).any()
+
+
+def test_device_generator_equals_host_generator(eng):
+    p, hb, _, _ = _make("c4_small")
+    db = eng.gen_batch(p)
+    torch.cuda.synchronize()
+    h = db.to_host()
+    for f in ["instance", "round", "type", "value", "validator", "offsets"]:
+        assert np.array_equal(h[f], getattr(hb, f)), f
+
+
+def test_invalid_votes_counted(eng):
+    p, hb, power, cfg = _make("c2_small")
+    rng = np.random.default_rng(5)
+    idx = rng.choice(hb.n_votes, 500, replace=False)
+    hb.validator[idx[:200]] = 100 + idx[:200] % 7     # out of range
+    hb.round[idx[200:300]] = 9                          # >= max_rounds
+    hb.type[idx[300:400]] = 2                           # bad type
+    hb.instance[idx[400:]] += 1                         # wrong segment
+    g, o = run_both(eng, cfg, hb, power)
+    assert_same(g, o)
+    assert g[2] == 500
+
+
+def test_caller_weights_and_instance_sets(eng):
+    p, hb, power, cfg = _make("c3_small")
+    rng = np.random.default_rng(9)
+    hb.instance_set = rng.integers(0, 1024, hb.n_instances, dtype=np.uint32)
+    hb.instance_set[:10] = 5000  # unknown set -> invalid
+    g, o = run_both(eng, cfg, hb, power, None, _start_states(hb.n_instances))
+    assert_same(g, o)
+    hb.weight = rng.integers(-(1 << 62), 1 << 62, hb.n_votes, dtype=np.int64)
+    hb.instance_set = None
+    cfg2 = abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 4)
+    st = _start_states(hb.n_instances)
+    g, o = run_both(eng, cfg2, hb, power, None, st)
+    assert_same(g, o)
+
+
+def test_apply_events_batch(eng):
+    rng = np.random.default_rng(3)
+    n = 3000
+    counts = rng.integers(0, 40, n)
+    off = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+    m = int(off[-1])
+    ev = np.zeros(m, abi.EVENT_DTYPE)
+    ev["kind"] = rng.integers(0, 13, m)
+    ev["round"] = rng.integers(-1, 4, m)
+    ev["pol_round"] = rng.integers(-2, 4, m)
+    ev["value"] = rng.integers(0, 3, m)
+    st = abi.new_states(n, 1)
+    for flags in (0, abi.FLAG_DISTINCT_VALUES):
+        o_st, o_msgs = ol.apply_events(st, off, ev, flags)
+        d_st = states_to_device(st, eng.device)
+        d_off = torch.from_numpy(off.view(np.int64)).to(eng.device)
+        d_ev = torch.from_numpy(ev.view(np.uint8)).to(eng.device)
+        d_msg = torch.zeros(m * 24, dtype=torch.uint8, device=eng.device)
+        eng.apply_events(d_st, d_off, d_ev, d_msg, flags)
+        torch.cuda.synchronize()
+        assert states_to_host(d_st).tobytes() == o_st.tobytes()
+        assert d_msg.cpu().numpy().tobytes() == o_msgs.tobytes()
+
+
+def test_determinism_and_sharding(eng):
+    """Same input twice -> identical bytes; a shard of instances tallied alone
+    equals the same instances inside the whole batch (instances independent)."""
+    p, _, power, cfg = _make("c4_small")
+    eng.upload_power(power)
+    whole = eng.gen_batch(p)
+    st = _start_states(p.n_instances)
+    outs = []
+    for _ in range(2):
+        codes = torch.zeros(whole.n_votes, dtype=torch.uint8, device=eng.device)
+        dst = states_to_device(st, eng.device)
+        eng.tally(cfg, whole, codes, dst)
+        outs.append((codes.cpu().numpy(), states_to_host(dst)))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert outs[0][1].tobytes() == outs[1][1].tobytes()
+    # shard = instances [1000, 2000) generated with instance_base
+    p2 = abi.gen_params(**{f: getattr(p, f) for f, _ in abi.GenParams._fields_})
+    p2.n_instances, p2.instance_base = 1000, 1000
+    shard = eng.gen_batch(p2)
+    codes = torch.zeros(shard.n_votes, dtype=torch.uint8, device=eng.device)
+    sh_set = torch.arange(1000, 2000, dtype=torch.int32, device=eng.device) % 1024
+    shard.instance_set = sh_set
+    dst = states_to_device(st[1000:2000], eng.device)
+    eng.tally(cfg, shard, codes, dst)
+    torch.cuda.synchronize()
+    off = whole.offsets.cpu().numpy()
+    assert np.array_equal(codes.cpu().numpy(), outs[0][0][off[1000]:off[2000]])
+    assert states_to_host(dst).tobytes() == outs[0][1][1000:2000].tobytes()
+
+
+@pytest.mark.slow
+def test_full_c2_height_parity(eng):
+    """BASELINE C2 at full size: 10k instances x 100 validators, one height."""
+    p = abi.gen_params(seed=0xA6E5, n_instances=10000, n_vals=100, nil_permille=200)
+    hb = ol.gen_batch(p)
+    power = ol.gen_power(0xA6E5, 1, 100, abi.POWER_UNIFORM, 1, 1000)
+    cfg = abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 1)
+    g, o = run_both(eng, cfg, hb, power, None, _start_states(10000), threads=16)
+    assert_same(g, o)
+
+
+@pytest.mark.slow
+def test_c3_shard_parity(eng):
+    """BASELINE C3 per-GPU shard: 125k instances (1M / 8) x 150 validators x 1..4 rounds."""
+    p = abi.gen_params(seed=0xA6E5, n_instances=125000, n_vals=150, rounds_min=1, rounds_max=4,
+                       nil_permille=300)
+    hb = ol.gen_batch(p)
+    power = ol.gen_power(0xA6E5, 1024, 150, abi.POWER_UNIFORM, 1, 1000)
+    cfg = abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 4)
+    g, o = run_both(eng, cfg, hb, power, None, _start_states(125000), threads=16)
+    assert_same(g, o)
