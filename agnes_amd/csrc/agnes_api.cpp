@@ -145,6 +145,7 @@ int agnes_ctx_device(const agnes_ctx* c) { return c ? c->device : AGNES_E_INVALI
 int agnes_upload_power(agnes_ctx* c, const int64_t* power, uint32_t n_sets, uint32_t n_vals,
                        const int64_t* totals) {
     if (!c || n_sets == 0 || (n_vals && !power) || (n_vals == 0 && !totals)) return AGNES_E_INVALID;
+    if ((uint64_t)n_sets * n_vals >= (1ull << 32)) return AGNES_E_UNSUPPORTED; /* 32-bit row bases */
     AGNES_TRY(hipSetDevice(c->device));
     AGNES_TRY(hipDeviceSynchronize());
     free_power(c);
@@ -207,6 +208,21 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     a.states = (cfg->flags & AGNES_FLAG_STATE_MACHINE) ? states : nullptr;
     a.carry = carry;
     a.n_invalid = c->d_err;
+    /* DEDUP / RoundSkip tables tag entries with (instance epoch, local vote index):
+     * the local index of any vote is < n_votes, so it needs bit_length(n_votes - 1) bits */
+    if (cfg->mode == AGNES_MODE_DEDUP || (cfg->flags & AGNES_FLAG_ROUND_SKIP)) {
+        if (b->n_votes > (1ull << 31)) return AGNES_E_UNSUPPORTED;
+        uint32_t lb = 1;
+        while (lb < 31 && (1ull << lb) < b->n_votes) ++lb;
+        /* test hook: spend fewer bits on epochs to exercise table recycling */
+        if (const char* d = std::getenv("AGNES_DEBUG_EPOCH_SHIFT")) {
+            const int v = std::atoi(d);
+            if (v > (int)lb && v <= 31) lb = (uint32_t)v;
+        }
+        a.epoch_shift = lb;
+    } else {
+        a.epoch_shift = 31;
+    }
     c->last_stream = st;
     return status_of(agnes_launch_tally(&a, cfg->mode, c->num_cus, st));
 }
@@ -265,41 +281,95 @@ int agnes_gen_votes_device(agnes_ctx* c, const agnes_gen_params* p, const uint64
 
 /* ---------------- scalar mirror ---------------- */
 
-struct agnes_ve {
-    int64_t height;
-    int64_t total;
-    unsigned char* dev; /* one allocation, layout below */
+/* One GPU-resident executor pair (prevotes, precommits) + a 1-vote batch.
+ * device block: [set_info 24][carry 3x24][offsets 16][weight 8][instance 4]
+ *               [value 4][validator 4][round 1][type 1][code 1][pad] */
+namespace {
+constexpr size_t SX_SET = 0, SX_CARRY = 24, SX_OFF = 96, SX_W = 112, SX_INST = 120, SX_VAL = 124,
+                 SX_VIDX = 128, SX_ROUND = 132, SX_TYPE = 133, SX_CODE = 134, SX_BYTES = 144;
+
+struct ScalarExec {
+    unsigned char* dev = nullptr;
 };
 
-/* device block of a VoteExecutor: [set_info 24][carry 2x24][offsets 16][weight 8]
- * [instance 4][value 4][validator 4][round 1][type 1][code 1][pad] */
-namespace {
-constexpr size_t VE_SET = 0, VE_CARRY = 24, VE_OFF = 72, VE_W = 88, VE_INST = 96, VE_VAL = 100,
-                 VE_VIDX = 104, VE_ROUND = 108, VE_TYPE = 109, VE_CODE = 110, VE_BYTES = 128;
+bool sx_init(ScalarExec* x, int64_t total) {
+    agnes_ctx* c = nullptr;
+    if (scalar_ctx(&c) != AGNES_OK) return false;
+    if (hipSetDevice(c->device) != hipSuccess) return false;
+    if (hipMalloc(&x->dev, SX_BYTES) != hipSuccess) return false;
+    unsigned char host[SX_BYTES];
+    std::memset(host, 0, sizeof(host));
+    agnes_set_info si = set_info(nullptr, 0, total);
+    si.fast = 0; /* caller weights: always the wrapping i64 path */
+    std::memcpy(host + SX_SET, &si, sizeof(si));
+    const uint64_t off[2] = {0, 1};
+    std::memcpy(host + SX_OFF, off, sizeof(off));
+    if (hipMemcpy(x->dev, host, SX_BYTES, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(x->dev);
+        x->dev = nullptr;
+        return false;
+    }
+    return true;
 }
 
-agnes_ve* agnes_ve_new(int64_t height, int64_t total_weight) {
-    std::lock_guard<std::mutex> g(g_mu);
+/* Tally one vote on the GPU against executor record `slot` (0 prevotes,
+ * 1 precommits) as vote type `as_type`; returns the vote's code byte and the
+ * executor's last value label. */
+int sx_add(ScalarExec* x, uint32_t slot, uint32_t as_type, uint32_t value, int64_t weight,
+           uint32_t* code, uint32_t* label) {
     agnes_ctx* c = nullptr;
-    if (scalar_ctx(&c) != AGNES_OK) return nullptr;
-    if (hipSetDevice(c->device) != hipSuccess) return nullptr;
+    int rc = scalar_ctx(&c);
+    if (rc != AGNES_OK) return rc;
+    AGNES_TRY(hipSetDevice(c->device));
+    unsigned char stage[SX_CODE - SX_W];
+    std::memset(stage, 0, sizeof(stage));
+    std::memcpy(stage + (SX_W - SX_W), &weight, 8);
+    std::memcpy(stage + (SX_VAL - SX_W), &value, 4);
+    stage[SX_TYPE - SX_W] = (uint8_t)as_type;
+    AGNES_TRY(hipMemcpy(x->dev + SX_W, stage, sizeof(stage), hipMemcpyHostToDevice));
+    agnes_vote_batch b;
+    std::memset(&b, 0, sizeof(b));
+    b.instance = (const uint32_t*)(x->dev + SX_INST);
+    b.round = x->dev + SX_ROUND;
+    b.type = x->dev + SX_TYPE;
+    b.value = (const uint32_t*)(x->dev + SX_VAL);
+    b.validator = (const uint32_t*)(x->dev + SX_VIDX);
+    b.offsets = (const uint64_t*)(x->dev + SX_OFF);
+    b.weight = (const int64_t*)(x->dev + SX_W);
+    b.n_votes = 1;
+    b.n_instances = 1;
+    agnes_config cfg = {AGNES_MODE_REFERENCE, 0u, 1u, 0u};
+    const uint32_t saved_nv = c->n_vals;
+    c->n_vals = 0; /* no power table: the validator index is unused */
+    agnes_carry_rec* carry = (agnes_carry_rec*)(x->dev + SX_CARRY) + slot;
+    rc = tally_impl(c, &cfg, &b, x->dev + SX_CODE, nullptr, carry,
+                    (const agnes_set_info*)(x->dev + SX_SET), 1u, nullptr);
+    c->n_vals = saved_nv;
+    if (rc != AGNES_OK) return rc;
+    unsigned char back[SX_BYTES];
+    AGNES_TRY(hipMemcpy(back, x->dev, SX_BYTES, hipMemcpyDeviceToHost));
+    agnes_carry_rec cr;
+    std::memcpy(&cr, back + SX_CARRY + (slot + as_type) * sizeof(agnes_carry_rec), sizeof(cr));
+    *code = back[SX_CODE];
+    *label = cr.value;
+    return AGNES_OK;
+}
+} // namespace
+
+struct agnes_ve {
+    ScalarExec x;
+};
+
+struct agnes_rv {
+    ScalarExec x;
+};
+
+agnes_ve* agnes_ve_new(int64_t height, int64_t total_weight) {
+    (void)height; /* stored but never read by the reference either (round_votes.rs:75) */
+    std::lock_guard<std::mutex> g(g_mu);
     agnes_ve* ve = new (std::nothrow) agnes_ve();
     if (!ve) return nullptr;
-    ve->height = height;
-    ve->total = total_weight;
-    if (hipMalloc(&ve->dev, VE_BYTES) != hipSuccess) {
-        delete ve;
-        return nullptr;
-    }
-    unsigned char host[VE_BYTES];
-    std::memset(host, 0, sizeof(host));
-    agnes_set_info si = set_info(nullptr, 0, total_weight);
-    si.fast = 0; /* caller weights: always the wrapping i64 path */
-    std::memcpy(host + VE_SET, &si, sizeof(si));
-    const uint64_t off[2] = {0, 1};
-    std::memcpy(host + VE_OFF, off, sizeof(off));
-    if (hipMemcpy(ve->dev, host, VE_BYTES, hipMemcpyHostToDevice) != hipSuccess) {
-        (void)hipFree(ve->dev);
+    if (!sx_init(&ve->x, total_weight)) {
         delete ve;
         return nullptr;
     }
@@ -309,53 +379,19 @@ agnes_ve* agnes_ve_new(int64_t height, int64_t total_weight) {
 int agnes_ve_apply(agnes_ve* ve, const agnes_vote* vote, int64_t weight, agnes_event* out) {
     if (!ve || !vote || vote->typ > 1) return AGNES_E_INVALID;
     std::lock_guard<std::mutex> g(g_mu);
-    agnes_ctx* c = nullptr;
-    int rc = scalar_ctx(&c);
-    if (rc != AGNES_OK) return rc;
-    AGNES_TRY(hipSetDevice(c->device));
     /* the reference executor ignores vote.round: one RoundVotes at round 0
-     * (vote_executor.rs:9,14) — so the vote is tallied as round 0 */
-    unsigned char stage[VE_BYTES - VE_W];
-    std::memset(stage, 0, sizeof(stage));
-    const uint32_t inst = 0, vidx = 0;
-    std::memcpy(stage + (VE_W - VE_W), &weight, 8);
-    std::memcpy(stage + (VE_INST - VE_W), &inst, 4);
-    std::memcpy(stage + (VE_VAL - VE_W), &vote->value, 4);
-    std::memcpy(stage + (VE_VIDX - VE_W), &vidx, 4);
-    stage[VE_TYPE - VE_W] = vote->typ;
-    AGNES_TRY(hipMemcpy(ve->dev + VE_W, stage, VE_CODE - VE_W, hipMemcpyHostToDevice));
-    agnes_vote_batch b;
-    std::memset(&b, 0, sizeof(b));
-    b.instance = (const uint32_t*)(ve->dev + VE_INST);
-    b.round = ve->dev + VE_ROUND;
-    b.type = ve->dev + VE_TYPE;
-    b.value = (const uint32_t*)(ve->dev + VE_VAL);
-    b.validator = (const uint32_t*)(ve->dev + VE_VIDX);
-    b.offsets = (const uint64_t*)(ve->dev + VE_OFF);
-    b.weight = (const int64_t*)(ve->dev + VE_W);
-    b.n_votes = 1;
-    b.n_instances = 1;
-    agnes_config cfg = {AGNES_MODE_REFERENCE, 0u, 1u, 0u};
-    const uint32_t saved_nv = c->n_vals;
-    c->n_vals = 0; /* no power table: validator unused */
-    rc = tally_impl(c, &cfg, &b, ve->dev + VE_CODE, nullptr, (agnes_carry_rec*)(ve->dev + VE_CARRY),
-                    (const agnes_set_info*)(ve->dev + VE_SET), 1u, nullptr);
-    c->n_vals = saved_nv;
+     * (vote_executor.rs:9,14); the engine tallies the vote in that executor */
+    uint32_t code = 0, label = 0;
+    const int rc = sx_add(&ve->x, 0u, vote->typ, vote->value, weight, &code, &label);
     if (rc != AGNES_OK) return rc;
-    unsigned char back[VE_BYTES];
-    AGNES_TRY(hipMemcpy(back, ve->dev, VE_BYTES, hipMemcpyDeviceToHost));
-    const uint32_t code = back[VE_CODE] & AGNES_CODE_EVENT_MASK;
+    code &= AGNES_CODE_EVENT_MASK;
     if (code == AGNES_CODE_NONE) return 0;
     if (code > AGNES_CODE_PRECOMMIT_VALUE) return AGNES_E_DEVICE;
-    agnes_carry_rec cr;
-    std::memcpy(&cr, back + VE_CARRY + vote->typ * sizeof(agnes_carry_rec), sizeof(cr));
     if (out) {
         std::memset(out, 0, sizeof(*out));
-        out->kind = (uint8_t)(code + 3u); /* CODE_POLKA_ANY(1) .. -> EV_POLKA_ANY(4) .. */
+        out->kind = (uint8_t)(code + 3u); /* CODE_POLKA_ANY(1).. -> EV_POLKA_ANY(4).. */
         out->round = vote->round;         /* apply_event(v.round, ..), consensus_executor.rs:68 */
-        out->value = (code == AGNES_CODE_POLKA_VALUE || code == AGNES_CODE_PRECOMMIT_VALUE)
-                         ? cr.value
-                         : 0u;
+        out->value = (code == AGNES_CODE_POLKA_VALUE || code == AGNES_CODE_PRECOMMIT_VALUE) ? label : 0u;
     }
     return 1;
 }
@@ -364,8 +400,48 @@ void agnes_ve_free(agnes_ve* ve) {
     if (!ve) return;
     std::lock_guard<std::mutex> g(g_mu);
     if (g_ctx) (void)hipSetDevice(g_ctx->device);
-    if (ve->dev) (void)hipFree(ve->dev);
+    if (ve->x.dev) (void)hipFree(ve->x.dev);
     delete ve;
+}
+
+agnes_rv* agnes_rv_new(int64_t height, int64_t round, int64_t total) {
+    (void)height;
+    (void)round; /* RoundVotes.height/.round are never read (round_votes.rs:75-76) */
+    std::lock_guard<std::mutex> g(g_mu);
+    agnes_rv* rv = new (std::nothrow) agnes_rv();
+    if (!rv) return nullptr;
+    if (!sx_init(&rv->x, total)) {
+        delete rv;
+        return nullptr;
+    }
+    return rv;
+}
+
+int agnes_rv_add_vote(agnes_rv* rv, const agnes_vote* vote, int64_t weight, uint32_t* value) {
+    if (!rv || !vote || vote->typ > 1) return AGNES_E_INVALID;
+    std::lock_guard<std::mutex> g(g_mu);
+    /* tallied as a prevote against the vote type's own executor record: the
+     * prevote event codes are in bijection with Thresh (vote_executor.rs:29-31) */
+    uint32_t code = 0, label = 0;
+    const int rc = sx_add(&rv->x, vote->typ, 0u, vote->value, weight, &code, &label);
+    if (rc != AGNES_OK) return rc;
+    switch (code & AGNES_CODE_EVENT_MASK) {
+    case AGNES_CODE_NONE: return (int)AGNES_THRESH_INIT;
+    case AGNES_CODE_POLKA_ANY: return (int)AGNES_THRESH_ANY;
+    case AGNES_CODE_POLKA_NIL: return (int)AGNES_THRESH_NIL;
+    case AGNES_CODE_POLKA_VALUE:
+        if (value) *value = label;
+        return (int)AGNES_THRESH_VALUE;
+    default: return AGNES_E_DEVICE;
+    }
+}
+
+void agnes_rv_free(agnes_rv* rv) {
+    if (!rv) return;
+    std::lock_guard<std::mutex> g(g_mu);
+    if (g_ctx) (void)hipSetDevice(g_ctx->device);
+    if (rv->x.dev) (void)hipFree(rv->x.dev);
+    delete rv;
 }
 
 void agnes_state_init(int64_t height, agnes_state* out) {

@@ -44,6 +44,8 @@ typedef struct agnes_tally_args {
     agnes_state* states;
     agnes_carry_rec* carry; /* optional [n_instances][2*max_rounds], in/out */
     unsigned long long* n_invalid;
+    uint32_t epoch_shift; /* bits of a vote's index inside its instance (DEDUP/SKIP tables) */
+    uint32_t pad_;
 } agnes_tally_args;
 
 /* bytes of dynamic LDS one wave uses */

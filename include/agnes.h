@@ -232,6 +232,14 @@ agnes_ve* agnes_ve_new(int64_t height, int64_t total_weight);
 int agnes_ve_apply(agnes_ve* ve, const agnes_vote* vote, int64_t weight, agnes_event* out);
 void agnes_ve_free(agnes_ve* ve);
 
+/* RoundVotes (round_votes.rs:74-97): the tally layer below VoteExecutor.
+ * agnes_rv_add_vote returns the Thresh (AGNES_THRESH_*) of RoundVotes::add_vote
+ * (round_votes.rs:92-97) and, for Thresh::Value, its value in *value; <0 on error. */
+typedef struct agnes_rv agnes_rv;
+agnes_rv* agnes_rv_new(int64_t height, int64_t round, int64_t total);
+int agnes_rv_add_vote(agnes_rv* rv, const agnes_vote* vote, int64_t weight, uint32_t* value);
+void agnes_rv_free(agnes_rv* rv);
+
 /* State::new(height)                                  state_machine.rs:35-43 */
 void agnes_state_init(int64_t height, agnes_state* out);
 /* State::apply(self, round, event) -> (State, Option<Message>)

@@ -325,6 +325,48 @@ def test_determinism_and_sharding(eng):
     assert states_to_host(dst).tobytes() == outs[0][1][1000:2000].tobytes()
 
 
+def _ragged_batch(seed, n_inst, n_vals, max_rounds, lengths):
+    """Instances with the given vote counts (0 allowed), random fields."""
+    rng = np.random.default_rng(seed)
+    lens = rng.choice(lengths, n_inst)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    n = int(off[-1])
+    inst = np.repeat(np.arange(n_inst, dtype=np.uint32), lens)
+    rnd = rng.integers(0, max_rounds, n).astype(np.uint8)
+    typ = rng.integers(0, 2, n).astype(np.uint8)
+    val = np.where(rng.random(n) < 0.3, abi.NIL, rng.integers(0, 3, n)).astype(np.uint32)
+    vid = rng.integers(0, n_vals, n).astype(np.uint32)
+    return ol.batch_from_lists(inst, rnd, typ, val, vid, off)
+
+
+@pytest.mark.parametrize("mode,flags", [
+    (abi.MODE_REFERENCE, 0),
+    (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE),
+    (abi.MODE_DEDUP, abi.FLAG_STATE_MACHINE | abi.FLAG_ROUND_SKIP),
+    (abi.MODE_REFERENCE, abi.FLAG_ROUND_SKIP | abi.FLAG_STATE_MACHINE)])
+def test_ragged_tiny_and_empty_instances(eng, mode, flags):
+    """Many instance boundaries per 64-vote chunk, zero-length instances,
+    instances longer than a chunk: the lane->instance map and the carries."""
+    hb = _ragged_batch(21, 20000, 9, 3, [0, 0, 1, 2, 3, 5, 8, 13, 63, 64, 65, 130, 200])
+    power = ol.gen_power(21, 13, 9, abi.POWER_UNIFORM, 1, 20)
+    cfg = abi.config(mode, flags, 3)
+    st = _start_states(hb.n_instances) if flags & abi.FLAG_STATE_MACHINE else None
+    g, o = run_both(eng, cfg, hb, power, None, st)
+    assert_same(g, o)
+
+
+def test_epoch_table_recycling(eng, monkeypatch):
+    """DEDUP/RoundSkip tables tag entries with per-instance epochs; with few
+    epoch bits the tables are cleared every 3 instances (chunks cut there)."""
+    monkeypatch.setenv("AGNES_DEBUG_EPOCH_SHIFT", "30")
+    hb = _ragged_batch(5, 6000, 11, 2, [0, 1, 4, 9, 40, 70, 150])
+    power = ol.gen_power(5, 4, 11, abi.POWER_UNIFORM, 1, 9)
+    cfg = abi.config(abi.MODE_DEDUP, abi.FLAG_ROUND_SKIP | abi.FLAG_STATE_MACHINE, 2)
+    g, o = run_both(eng, cfg, hb, power, None, _start_states(hb.n_instances))
+    assert_same(g, o)
+    assert (g[0] & 7 == abi.CODE_REJECTED).any()
+
+
 @pytest.mark.slow
 def test_full_c2_height_parity(eng):
     """BASELINE C2 at full size: 10k instances x 100 validators, one height."""
