@@ -30,6 +30,9 @@ struct agnes_ctx {
     uint32_t n_vals = 0;
     unsigned long long* d_err = nullptr;
     hipStream_t last_stream = nullptr;
+    bool all_fast = false;     /* every set inside the u32 fast domain */
+    uint32_t* d_list = nullptr; /* [list_cap] deferred instances + 1 counter */
+    uint32_t list_cap = 0;
 };
 
 namespace {
@@ -137,6 +140,7 @@ void agnes_ctx_destroy(agnes_ctx* c) {
     (void)hipSetDevice(c->device);
     free_power(c);
     if (c->d_err) (void)hipFree(c->d_err);
+    if (c->d_list) (void)hipFree(c->d_list);
     delete c;
 }
 
@@ -152,6 +156,7 @@ int agnes_upload_power(agnes_ctx* c, const int64_t* power, uint32_t n_sets, uint
     const uint64_t n = (uint64_t)n_sets * n_vals;
     std::vector<agnes_set_info> sets(n_sets);
     std::vector<uint32_t> p32(n);
+    bool all_fast = true;
     for (uint32_t s = 0; s < n_sets; ++s) {
         const int64_t* row = power + (uint64_t)s * n_vals;
         int64_t t = 0;
@@ -159,6 +164,7 @@ int agnes_upload_power(agnes_ctx* c, const int64_t* power, uint32_t n_sets, uint
         else
             for (uint32_t v = 0; v < n_vals; ++v) t = wadd(t, row[v]);
         sets[s] = set_info(row, n_vals, t);
+        all_fast = all_fast && sets[s].fast;
         for (uint32_t v = 0; v < n_vals; ++v) p32[(uint64_t)s * n_vals + v] = (uint32_t)row[v];
     }
     const size_t pb = (size_t)(n ? n : 1);
@@ -173,6 +179,7 @@ int agnes_upload_power(agnes_ctx* c, const int64_t* power, uint32_t n_sets, uint
                         hipMemcpyHostToDevice));
     c->n_sets = n_sets;
     c->n_vals = n_vals;
+    c->all_fast = all_fast;
     return AGNES_OK;
 }
 
@@ -184,15 +191,27 @@ int64_t agnes_lds_bytes_per_wave(const agnes_config* cfg, uint32_t n_vals) {
 
 static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b,
                       uint8_t* codes, agnes_state* states, agnes_carry_rec* carry,
-                      const agnes_set_info* sets, uint32_t n_sets, hipStream_t st) {
+                      const agnes_set_info* sets, uint32_t n_sets, bool sets_fast,
+                      hipStream_t st) {
     if (!c || !cfg_ok(cfg) || !b || !b->offsets) return AGNES_E_INVALID;
     if (b->n_votes && (!codes || !b->instance || !b->round || !b->type || !b->value ||
                        !b->validator))
         return AGNES_E_INVALID;
     if ((cfg->flags & AGNES_FLAG_STATE_MACHINE) && !states) return AGNES_E_INVALID;
+    /* u32 columns naturally aligned */
+    if (((uintptr_t)b->instance | (uintptr_t)b->value | (uintptr_t)b->validator) & 3u) return AGNES_E_INVALID;
     const int64_t lpw = agnes_lds_bytes_per_wave(cfg, c->n_vals);
     if (lpw < 0) return (int)lpw;
     AGNES_TRY(hipSetDevice(c->device));
+    const bool wide_all = b->weight != nullptr || carry != nullptr || !sets_fast;
+    if (!wide_all && c->list_cap < b->n_instances + 1u) { /* deferred-instance list */
+        AGNES_TRY(hipStreamSynchronize(st));
+        if (c->d_list) (void)hipFree(c->d_list);
+        c->d_list = nullptr;
+        c->list_cap = 0;
+        AGNES_TRY(hipMalloc(&c->d_list, ((size_t)b->n_instances + 1u) * sizeof(uint32_t)));
+        c->list_cap = b->n_instances + 1u;
+    }
     AGNES_TRY(hipMemsetAsync(c->d_err, 0, sizeof(unsigned long long), st));
     agnes_tally_args a;
     std::memset(&a, 0, sizeof(a));
@@ -208,6 +227,8 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     a.states = (cfg->flags & AGNES_FLAG_STATE_MACHINE) ? states : nullptr;
     a.carry = carry;
     a.n_invalid = c->d_err;
+    a.list = c->d_list;
+    a.list_count = c->d_list ? c->d_list + (c->list_cap - 1u) : nullptr;
     /* DEDUP / RoundSkip tables tag entries with (instance epoch, local vote index):
      * the local index of any vote is < n_votes, so it needs bit_length(n_votes - 1) bits */
     if (cfg->mode == AGNES_MODE_DEDUP || (cfg->flags & AGNES_FLAG_ROUND_SKIP)) {
@@ -223,14 +244,15 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     } else {
         a.epoch_shift = 31;
     }
+    if (const char* d = std::getenv("AGNES_DEBUG_SKIP")) a.dbg = (uint32_t)std::atoi(d);
     c->last_stream = st;
-    return status_of(agnes_launch_tally(&a, cfg->mode, c->num_cus, st));
+    return status_of(agnes_launch_tally(&a, cfg->mode, c->num_cus, wide_all, st));
 }
 
 int agnes_tally(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint8_t* codes,
                 agnes_state* states, void* stream) {
     if (!c) return AGNES_E_INVALID;
-    return tally_impl(c, cfg, b, codes, states, nullptr, c->d_sets, c->n_sets,
+    return tally_impl(c, cfg, b, codes, states, nullptr, c->d_sets, c->n_sets, c->all_fast,
                       (hipStream_t)stream);
 }
 
@@ -282,11 +304,12 @@ int agnes_gen_votes_device(agnes_ctx* c, const agnes_gen_params* p, const uint64
 /* ---------------- scalar mirror ---------------- */
 
 /* One GPU-resident executor pair (prevotes, precommits) + a 1-vote batch.
- * device block: [set_info 24][carry 3x24][offsets 16][weight 8][instance 4]
- *               [value 4][validator 4][round 1][type 1][code 1][pad] */
+ * device block: [set_info 24][carry 3x24][offsets 16][weight 8][pad][instance 16]
+ *               [value 16][validator 16][round 4][type 4][code 4]
+ * (vote columns 16-byte aligned: the kernel reads 4 votes per lane) */
 namespace {
-constexpr size_t SX_SET = 0, SX_CARRY = 24, SX_OFF = 96, SX_W = 112, SX_INST = 120, SX_VAL = 124,
-                 SX_VIDX = 128, SX_ROUND = 132, SX_TYPE = 133, SX_CODE = 134, SX_BYTES = 144;
+constexpr size_t SX_SET = 0, SX_CARRY = 24, SX_OFF = 96, SX_W = 112, SX_INST = 128, SX_VAL = 144,
+                 SX_VIDX = 160, SX_ROUND = 176, SX_TYPE = 180, SX_CODE = 184, SX_BYTES = 192;
 
 struct ScalarExec {
     unsigned char* dev = nullptr;
@@ -343,7 +366,7 @@ int sx_add(ScalarExec* x, uint32_t slot, uint32_t as_type, uint32_t value, int64
     c->n_vals = 0; /* no power table: the validator index is unused */
     agnes_carry_rec* carry = (agnes_carry_rec*)(x->dev + SX_CARRY) + slot;
     rc = tally_impl(c, &cfg, &b, x->dev + SX_CODE, nullptr, carry,
-                    (const agnes_set_info*)(x->dev + SX_SET), 1u, nullptr);
+                    (const agnes_set_info*)(x->dev + SX_SET), 1u, false, nullptr);
     c->n_vals = saved_nv;
     if (rc != AGNES_OK) return rc;
     unsigned char back[SX_BYTES];

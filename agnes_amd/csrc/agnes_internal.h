@@ -44,15 +44,20 @@ typedef struct agnes_tally_args {
     agnes_state* states;
     agnes_carry_rec* carry; /* optional [n_instances][2*max_rounds], in/out */
     unsigned long long* n_invalid;
+    uint32_t* list;       /* deferred instances (fast kernel -> wide kernel), n_instances */
+    uint32_t* list_count;
     uint32_t epoch_shift; /* bits of a vote's index inside its instance (DEDUP/SKIP tables) */
-    uint32_t pad_;
+    uint32_t dbg;         /* development knob (AGNES_DEBUG_SKIP): phases to skip; 0 in production */
 } agnes_tally_args;
 
 /* bytes of dynamic LDS one wave uses */
 int64_t agnes_lds_per_wave(uint32_t mode, uint32_t flags, uint32_t max_rounds, uint32_t n_vals);
 
 /* launchers (agnes_kernels.hip) — enqueue only */
-hipError_t agnes_launch_tally(const agnes_tally_args* a, uint32_t mode, int num_cus,
+/* wide_all: every instance on the i64 path (caller weights, carried executors or
+ * a power set outside the fast domain); else the u32 kernel runs first and
+ * defers the instances it cannot prove to the i64 list kernel */
+hipError_t agnes_launch_tally(const agnes_tally_args* a, uint32_t mode, int num_cus, bool wide_all,
                               hipStream_t stream);
 hipError_t agnes_launch_apply_events(agnes_state* states, uint32_t n, const uint64_t* off,
                                      const agnes_event* ev, agnes_message* msgs, uint32_t flags,

@@ -1,8 +1,9 @@
 /*
  * agnes_kernels.hip — gfx950 kernels of the Agnes vote-tally engine.
  *
- * K1-K4 fused (tally_kernel): one wave64 per instance (grid-stride over
- * instances), 64 consecutive votes of the instance per step, one vote per lane:
+ * K1-K4 fused (tally_kernel): each wave64 owns a contiguous range of instances
+ * and tallies them one at a time in 256-vote chunks = 4 rows of 64 (every load
+ * a coalesced 64-lane row; the next chunk's loads in flight while one computes):
  *
  *   K1 ingest   coalesced SoA loads (instance, round, type, value, validator)
  *               + gather w = power[set][validator]          (consensus_executor.rs:62-63
@@ -325,44 +326,32 @@ __device__ __forceinline__ uint32_t vmsg_of(bool h1, bool h2, const MsgOut& m2) 
     return b;
 }
 
-/* ------------------------------------------------------------------ */
-/* LDS of one wave                                                     */
-
-/* Two carry buffers (ping-pong): the executors of the instance left open at a
- * chunk end live in buffer `pp`; a chunk that opens a new instance writes that
- * instance's carries into the other buffer.  Per buffer: RoundVotes of every
- * round = value/nil weights + last value label per (round, type) slot, and the
- * RoundSkip weight per round. */
-struct CarryBuf {
-    uint64_t* vw;  /* [2R] */
-    uint64_t* vn;  /* [2R] */
-    uint64_t* skw; /* [R]  */
-    uint32_t* lv;  /* [2R] */
-};
-
-struct WaveLds {
-    unsigned char* cbase; /* carry buffer 0; buffer 1 at cbase + cbytes */
-    uint32_t cbytes;
-    uint32_t R;
-    uint32_t* first_v; /* DEDUP [2R][nv]: epoch<<LB | (LMASK - local) of the first vote */
-    uint32_t* first_s; /* SKIP  [R][nv]:  same, per (round, validator)                  */
-};
-
-__device__ __forceinline__ CarryBuf carry_buf(const WaveLds& L, uint32_t b) {
-    CarryBuf cb;
-    cb.vw = reinterpret_cast<uint64_t*>(L.cbase + b * L.cbytes);
-    cb.vn = cb.vw + 2u * L.R;
-    cb.skw = cb.vn + 2u * L.R;
-    cb.lv = reinterpret_cast<uint32_t*>(cb.skw + L.R);
-    return cb;
+template <typename T>
+__device__ __forceinline__ T pick4(const T (&x)[4], uint32_t e) { /* e wave-uniform */
+    return e == 0 ? x[0] : (e == 1 ? x[1] : (e == 2 ? x[2] : x[3]));
 }
+
+/* ------------------------------------------------------------------ */
+/* LDS of one wave: the executors of the instance being tallied        */
+
+/* RoundVotes of every round of the current instance (round_votes.rs:74-80):
+ * value / nil weight and last value label per (round, type) slot, plus the
+ * RoundSkip weight per round; and the first-vote tables. */
+struct WaveLds {
+    uint64_t* vw;      /* [2R] */
+    uint64_t* vn;      /* [2R] */
+    uint64_t* skw;     /* [R]  */
+    uint32_t* lv;      /* [2R] */
+    uint32_t* first_v; /* DEDUP [2R][nv]: epoch << lb | (LMASK - local) of the first vote */
+    uint32_t* first_s; /* SKIP  [R][nv]:  same per (round, validator)                    */
+};
 
 __host__ __device__ inline uint64_t align16(uint64_t x) { return (x + 15u) & ~15ull; }
 
 __host__ __device__ inline void lds_layout(uint32_t mode, uint32_t flags, uint32_t R, uint32_t nv,
                                            uint64_t* o_first_v, uint64_t* o_first_s,
                                            uint64_t* total) {
-    uint64_t o = 2ull * align16(48ull * R); /* 2 x (vw 16R + vn 16R + skw 8R + lv 8R) */
+    uint64_t o = align16(48ull * R); /* vw 16R + vn 16R + skw 8R + lv 8R */
     *o_first_v = o;
     if (mode == AGNES_MODE_DEDUP) o = align16(o + 2ull * R * nv * 4u);
     *o_first_s = o;
@@ -378,65 +367,61 @@ __device__ inline void fill_u32(uint32_t* p, uint64_t n, uint32_t v, uint32_t la
     for (uint64_t k = (n4 << 2) + lane; k < n; k += 64) p[k] = v;
 }
 
-__device__ inline void zero_carry(const CarryBuf& b, uint32_t R, uint32_t lane) {
-    for (uint32_t k = lane; k < 2u * R; k += 64) {
-        b.vw[k] = 0;
-        b.vn[k] = 0;
-        b.lv[k] = 0;
-    }
-    for (uint32_t k = lane; k < R; k += 64) b.skw[k] = 0;
-}
-
 /* ------------------------------------------------------------------ */
 /* fused tally kernel                                                  */
 
-/* Per-lane view of the instances vbase + lane of the wave's range (a 64-wide
- * window, reloaded as the stream advances; read back with v_readlane). */
-struct Window {
-    uint64_t end;  /* offsets[k+1] (clamped to n_votes)          */
-    int64_t tot;   /* total_weight of the instance's set          */
-    uint32_t q2;   /* fast-path quorum threshold floor(2t/3)     */
-    uint32_t q1;   /* fast-path RoundSkip threshold floor(t/3)   */
-    uint32_t pb;   /* set * n_vals: row of the power table       */
-    uint32_t fl;   /* bit0: set exists; bit1: fast path provable */
+constexpr uint32_t SUBS = 4;             /* 64-vote rows per chunk         */
+constexpr uint32_t CHUNK = 64u * SUBS;   /* votes per chunk (one instance) */
+
+/* one chunk of the canonical SoA: row s, lane l = vote c + 64 s + l (every
+ * load a fully coalesced 64-lane row) */
+struct Raw {
+    uint32_t inst[SUBS], value[SUBS], val[SUBS], r[SUBS], t[SUBS];
 };
 
-struct Fields {
-    uint32_t inst, value, val, r, t;
-};
-
-__device__ __forceinline__ Fields load_fields(const agnes_vote_batch& vb, uint64_t j, bool in) {
-    Fields f = {0u, 0u, 0u, 0u, 0u};
-    if (in) {
-        f.inst = vb.instance[j];
-        f.r = vb.round[j];
-        f.t = vb.type[j];
-        f.value = vb.value[j];
-        f.val = vb.validator[j];
+__device__ __forceinline__ void load_raw(const agnes_vote_batch& vb, uint64_t c, uint64_t lim,
+                                         Raw& x) {
+    const uint32_t lane = lane_id();
+    if (c + CHUNK <= lim) { /* wave-uniform: whole chunk readable */
+#pragma unroll
+        for (uint32_t s = 0; s < SUBS; ++s) {
+            const uint64_t j = c + 64u * s + lane;
+            x.inst[s] = vb.instance[j];
+            x.value[s] = vb.value[j];
+            x.val[s] = vb.validator[j];
+            x.r[s] = vb.round[j];
+            x.t[s] = vb.type[j];
+        }
+    } else {
+#pragma unroll
+        for (uint32_t s = 0; s < SUBS; ++s) {
+            const uint64_t j = c + 64u * s + lane;
+            const bool in = j < lim;
+            x.inst[s] = in ? vb.instance[j] : 0u;
+            x.value[s] = in ? vb.value[j] : 0u;
+            x.val[s] = in ? vb.validator[j] : 0u;
+            x.r[s] = in ? (uint32_t)vb.round[j] : 0u;
+            x.t[s] = in ? (uint32_t)vb.type[j] : 0u;
+        }
     }
-    return f;
 }
 
-/* Everything a chunk needs besides its fields. */
-struct Chunk {
-    uint64_t c;        /* first vote of the chunk            */
-    uint32_t nvalid;   /* votes in the chunk (cl - c)         */
-    uint32_t cur;      /* instance of lane 0                  */
-    uint32_t last;     /* instance of the last valid lane     */
-    uint32_t m;        /* instance boundaries inside          */
-    uint32_t hl;       /* first lane of `last` (m > 0)        */
-    uint64_t cur_start;
-    uint32_t ebase;
-    bool last_continues;
+/* uniform facts of the instance being tallied */
+struct Inst {
+    uint64_t beg, end; /* its votes                        */
+    uint32_t i;        /* its index                        */
+    uint32_t pbase;    /* set * n_vals                     */
+    uint32_t q2, q1;   /* fast-path thresholds             */
+    int64_t total;     /* total_weight (wide path)         */
+    uint32_t ep;       /* epoch tag of its first-vote rows */
+    bool set_ok;
 };
 
 template <bool WIDE, uint32_t MODE, bool SKIP, bool SM>
 __device__ __forceinline__ void process_chunk(const agnes_tally_args& a, const WaveLds& L,
-                                              uint32_t pp, const Chunk& ch, const Fields& f,
-                                              uint32_t myi, uint32_t head, uint32_t q2l,
-                                              uint32_t q1l, int64_t totl, uint32_t pbl,
-                                              bool setok, Sm& st, const Sm& st_next,
-                                              uint32_t lb, uint64_t& n_bad) {
+                                              const Inst& in_, uint64_t c, uint64_t cl,
+                                              const Raw& x, Sm& st, uint32_t lb,
+                                              uint32_t& bad_lane) {
     using W = typename std::conditional<WIDE, uint64_t, uint32_t>::type;
     const uint32_t lane = lane_id();
     const uint32_t R = a.max_rounds;
@@ -444,199 +429,244 @@ __device__ __forceinline__ void process_chunk(const agnes_tally_args& a, const W
     const agnes_vote_batch& vb = a.vb;
     const bool has_w = vb.weight != nullptr;
     const bool need_val = !has_w || MODE == AGNES_MODE_DEDUP || SKIP;
-    const bool track = SM || a.carry != nullptr; /* carried executors keep their label */
-    const CarryBuf P = carry_buf(L, pp);
-    const CarryBuf Q = carry_buf(L, pp ^ 1u);
-    const uint64_t j = ch.c + lane;
-    const bool valid = lane < ch.nvalid;
+    const bool track = SM || a.carry != nullptr; /* labels: state machine / carried executors */
+    const uint32_t nvalid = (uint32_t)(cl - c);
 
-    const bool ok = valid && f.inst == myi && f.r < R && f.t <= 1u &&
-                    (!need_val || (setok && f.val < nv)) && (has_w || setok);
-    n_bad += __builtin_popcountll(ballot(valid && !ok));
-    W w = 0;
-    if (ok) {
-        if (has_w) w = (W)vb.weight[j];
-        else if (WIDE) w = (W)a.power[(uint64_t)pbl + f.val];
-        else w = (W)a.power32[(uint64_t)pbl + f.val];
+    bool valid[SUBS], ok[SUBS], acc[SUBS], isnil[SUBS];
+    W w[SUBS];
+#pragma unroll
+    for (uint32_t s = 0; s < SUBS; ++s) {
+        valid[s] = 64u * s + lane < nvalid;
+        ok[s] = valid[s] && x.inst[s] == in_.i && x.r[s] < R && x.t[s] <= 1u &&
+                (!need_val || (in_.set_ok && x.val[s] < nv)) && (has_w || in_.set_ok);
+        bad_lane += (valid[s] && !ok[s]) ? 1u : 0u;
+        isnil[s] = x.value[s] == AGNES_NIL;
+        acc[s] = ok[s];
+        /* K1 weight gather (consensus_executor.rs:62-63 -> validators.rs:7), branch-free */
+        if (has_w) {
+            w[s] = ok[s] ? (W)vb.weight[c + 64u * s + lane] : (W)0;
+        } else {
+            const uint32_t idx = ok[s] ? in_.pbase + x.val[s] : 0u;
+            const W g = WIDE ? (W)a.power[idx] : (W)a.power32[idx];
+            w[s] = ok[s] ? g : (W)0;
+        }
     }
 
-    /* first-vote-wins tables (DEDUP) and distinct-validator tables (RoundSkip):
-     * atomic max of (epoch << lb | LMASK - local); instances of one chunk in
-     * stream order, so a later instance never overwrites an earlier one's
-     * entry before that one has read it back. */
-    bool acc = ok, sfirst = false;
+    /* first-vote-wins (DEDUP) / distinct-validator (RoundSkip) tables: atomic max of
+     * (epoch << lb | LMASK - local index): the earliest vote of the instance wins,
+     * entries of earlier instances (smaller epochs) are simply overwritten */
+    bool sfirst[SUBS];
+#pragma unroll
+    for (uint32_t s = 0; s < SUBS; ++s) sfirst[s] = false;
     if (MODE == AGNES_MODE_DEDUP || SKIP) {
-        const uint32_t lmask = (lb >= 32u) ? 0xFFFFFFFFu : ((1u << lb) - 1u);
-        const uint64_t start = (myi == ch.cur) ? ch.cur_start : ch.c + head;
-        const uint32_t loc = (uint32_t)(j - start);
-        for (uint32_t k = ch.cur; k <= ch.last; ++k) {
-            const bool inseg = ok && myi == k;
-            if (!ballot(inseg)) continue;
-            const uint32_t enc = ((k - ch.ebase + 1u) << lb) | (lmask - loc);
-            uint32_t* ev = nullptr;
-            uint32_t* es = nullptr;
-            if (MODE == AGNES_MODE_DEDUP) ev = &L.first_v[(f.r * 2u + f.t) * nv + f.val];
-            if (SKIP) es = &L.first_s[f.r * nv + f.val];
-            if (inseg) {
-                if (MODE == AGNES_MODE_DEDUP) atomicMax(ev, enc);
-                if (SKIP) atomicMax(es, enc);
-            }
-            __builtin_amdgcn_wave_barrier();
-            if (inseg) {
-                if (MODE == AGNES_MODE_DEDUP) acc = *(volatile uint32_t*)ev == enc;
-                if (SKIP) sfirst = *(volatile uint32_t*)es == enc;
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-    }
-
-    /* K2: per (round,type) slot present: unsegmented inclusive scans; a lane's
-     * prefix = scan - scan[just before its instance's first lane], or + the
-     * carried executor for the instance open since an earlier chunk. */
-    const bool isnil = f.value == AGNES_NIL;
-    const uint32_t slot = f.r * 2u + f.t;
-    const uint32_t hidx = head ? head - 1u : 0u;
-    const uint64_t ge_head = ~((1ull << head) - 1ull);
-    const bool multi = ch.m != 0u;
-    /* carries are needed after the chunk when the last instance continues, or
-     * when they are persisted (carry mode: one instance per chunk) */
-    const bool upd = ch.last_continues || a.carry != nullptr;
-    W pv = 0, pn = 0;
-    uint32_t lab = 0;
-    uint64_t rem = ballot(acc);
-    while (rem) {
-        const uint32_t k = rdl(slot, (uint32_t)__builtin_ctzll(rem));
-        const bool in = acc && slot == k;
-        rem &= ~ballot(in);
-        const W sv = scan((W)((in && !isnil) ? w : (W)0));
-        const W sn = scan((W)((in && isnil) ? w : (W)0));
-        const W cv = (W)P.vw[k], cn = (W)P.vn[k];
-        W bv = cv, bn = cn;
-        if (multi) {
-            const W gv = shfl(sv, hidx), gn = shfl(sn, hidx);
-            bv = head ? (W)(0 - gv) : cv;
-            bn = head ? (W)(0 - gn) : cn;
-        }
-        if (in) {
-            pv = sv + bv;
-            pn = sn + bn;
-        }
-        if (upd) {
-            const W tv = rdl(sv, 63u), tn = rdl(sn, 63u);
-            if (!multi) {
-                P.vw[k] = (uint64_t)(W)(cv + tv);
-                P.vn[k] = (uint64_t)(W)(cn + tn);
-            } else {
-                Q.vw[k] = (uint64_t)(W)(tv - rdl(sv, ch.hl - 1u));
-                Q.vn[k] = (uint64_t)(W)(tn - rdl(sn, ch.hl - 1u));
+        const uint32_t lmask = (1u << lb) - 1u;
+        const uint32_t loc0 = (uint32_t)(c - in_.beg) + lane;
+        uint32_t enc[SUBS];
+#pragma unroll
+        for (uint32_t s = 0; s < SUBS; ++s) {
+            enc[s] = (in_.ep << lb) | (lmask - (loc0 + 64u * s));
+            if (ok[s]) {
+                if (MODE == AGNES_MODE_DEDUP)
+                    atomicMax(&L.first_v[(x.r[s] * 2u + x.t[s]) * nv + x.val[s]], enc[s]);
+                if (SKIP) atomicMax(&L.first_s[x.r[s] * nv + x.val[s]], enc[s]);
             }
         }
-        if (track) { /* Thresh::Value payload: last value written (round_votes.rs:53) */
-            const uint64_t mv = ballot(in && !isnil);
-            const uint64_t le = mv & lanemask_le(lane) & ge_head;
-            const uint32_t src = le ? 63u - (uint32_t)__builtin_clzll(le) : 0u;
-            const uint32_t got = shfl(f.value, src);
-            const uint32_t cl = (head == 0u) ? P.lv[k] : 0u;
-            if (in) lab = isnil ? (le ? got : cl) : f.value;
-            if (upd) {
-                const uint64_t mvl = multi ? (mv & ~((1ull << ch.hl) - 1ull)) : mv;
-                if (mvl) (multi ? Q : P).lv[k] = rdl(f.value, 63u - (uint32_t)__builtin_clzll(mvl));
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (uint32_t s = 0; s < SUBS; ++s) {
+            if (ok[s]) {
+                if (MODE == AGNES_MODE_DEDUP)
+                    acc[s] = *(volatile uint32_t*)&L.first_v[(x.r[s] * 2u + x.t[s]) * nv + x.val[s]] == enc[s];
+                if (SKIP) sfirst[s] = *(volatile uint32_t*)&L.first_s[x.r[s] * nv + x.val[s]] == enc[s];
             }
         }
         __builtin_amdgcn_wave_barrier();
     }
-    W ps = 0;
-    if (SKIP) { /* RoundSkip weight of distinct validators per round, same scheme */
-        rem = ballot(acc);
-        while (rem) {
-            const uint32_t kr = rdl(f.r, (uint32_t)__builtin_ctzll(rem));
-            const bool in = acc && f.r == kr;
-            rem &= ~ballot(in);
-            const W ss = scan((W)((in && sfirst) ? w : (W)0));
-            const W cs = (W)P.skw[kr];
-            W bs = cs;
-            if (multi) { /* bpermute with every lane active: inactive sources read as 0 */
-                const W gs = shfl(ss, hidx);
-                bs = head ? (W)(0 - gs) : cs;
+
+    /* K2: per (round,type) slot present: row by row, a wave64 inclusive scan of the
+     * value and nil buckets plus the running executor — VoteCount::add_vote's sums in
+     * stream order (round_votes.rs:48-56) */
+    uint32_t slot[SUBS];
+    uint64_t rem[SUBS];
+#pragma unroll
+    for (uint32_t s = 0; s < SUBS; ++s) {
+        slot[s] = x.r[s] * 2u + x.t[s];
+        rem[s] = ballot(acc[s]);
+    }
+    W pv[SUBS], pn[SUBS];
+    uint32_t lab[SUBS];
+#pragma unroll
+    for (uint32_t s = 0; s < SUBS; ++s) {
+        pv[s] = 0;
+        pn[s] = 0;
+        lab[s] = 0;
+    }
+    for (;;) {
+        uint32_t key = 0xFFFFFFFFu;
+#pragma unroll
+        for (uint32_t s = 0; s < SUBS; ++s)
+            if (key == 0xFFFFFFFFu && rem[s]) key = rdl(slot[s], (uint32_t)__builtin_ctzll(rem[s]));
+        if (key == 0xFFFFFFFFu) break;
+        W cv = (W)L.vw[key], cn = (W)L.vn[key];
+        uint32_t lbl = track ? L.lv[key] : 0u;
+#pragma unroll
+        for (uint32_t s = 0; s < SUBS; ++s) {
+            const bool in = acc[s] && slot[s] == key;
+            const uint64_t min_ = ballot(in);
+            rem[s] &= ~min_;
+            if (!min_) continue; /* wave-uniform */
+            const W sv = scan((W)((in && !isnil[s]) ? w[s] : (W)0));
+            const W sn = scan((W)((in && isnil[s]) ? w[s] : (W)0));
+            if (in) {
+                pv[s] = cv + sv;
+                pn[s] = cn + sn;
             }
-            if (in) ps = ss + bs;
-            if (upd) {
-                const W ts = rdl(ss, 63u);
-                if (!multi) P.skw[kr] = (uint64_t)(W)(cs + ts);
-                else Q.skw[kr] = (uint64_t)(W)(ts - rdl(ss, ch.hl - 1u));
+            cv += rdl(sv, 63u);
+            cn += rdl(sn, 63u);
+            if (track) { /* Thresh::Value payload: the last value written (round_votes.rs:53) */
+                const uint64_t mv = ballot(in && !isnil[s]);
+                bool qv;
+                if (WIDE) qv = (int64_t)(3ull * (uint64_t)pv[s]) > (int64_t)(2ull * (uint64_t)in_.total);
+                else qv = (uint32_t)pv[s] > in_.q2;
+                /* a nil vote needs a propagated label only when its value bucket is at quorum */
+                if (ballot(in && isnil[s] && qv)) {
+                    const uint64_t le = mv & lanemask_le(lane);
+                    const uint32_t got = shfl(x.value[s], le ? 63u - (uint32_t)__builtin_clzll(le) : 0u);
+                    if (in) lab[s] = isnil[s] ? (le ? got : lbl) : x.value[s];
+                } else if (in && !isnil[s]) {
+                    lab[s] = x.value[s];
+                }
+                if (mv) lbl = rdl(x.value[s], 63u - (uint32_t)__builtin_clzll(mv));
             }
+        }
+        L.vw[key] = (uint64_t)cv;
+        L.vn[key] = (uint64_t)cn;
+        if (track) L.lv[key] = lbl;
+        __builtin_amdgcn_wave_barrier();
+    }
+
+    /* RoundSkip (+1/3 of distinct validators of the vote's round, extension):
+     * the same scheme keyed by round over each validator's first vote */
+    W ps[SUBS];
+#pragma unroll
+    for (uint32_t s = 0; s < SUBS; ++s) ps[s] = 0;
+    if (SKIP) {
+#pragma unroll
+        for (uint32_t s = 0; s < SUBS; ++s) rem[s] = ballot(acc[s]);
+        for (;;) {
+            uint32_t kr = 0xFFFFFFFFu;
+#pragma unroll
+            for (uint32_t s = 0; s < SUBS; ++s)
+                if (kr == 0xFFFFFFFFu && rem[s]) kr = rdl(x.r[s], (uint32_t)__builtin_ctzll(rem[s]));
+            if (kr == 0xFFFFFFFFu) break;
+            W cs = (W)L.skw[kr];
+#pragma unroll
+            for (uint32_t s = 0; s < SUBS; ++s) {
+                const bool in = acc[s] && x.r[s] == kr;
+                const uint64_t min_ = ballot(in);
+                rem[s] &= ~min_;
+                if (!min_) continue;
+                const W ss = scan((W)((in && sfirst[s]) ? w[s] : (W)0));
+                if (in) ps[s] = cs + ss;
+                cs += rdl(ss, 63u);
+            }
+            L.skw[kr] = (uint64_t)cs;
             __builtin_amdgcn_wave_barrier();
         }
     }
 
-    /* K3: is_quorum precedence (round_votes.rs:58-66) and to_event (vote_executor.rs:26-36) */
-    uint32_t code;
-    if (!ok) {
-        code = AGNES_CODE_INVALID;
-    } else if (!acc) {
-        code = AGNES_CODE_REJECTED;
-    } else {
-        bool qv, qn, qa, q3;
-        if (WIDE) {
-            const int64_t t2 = (int64_t)(2ull * (uint64_t)totl);
-            qv = (int64_t)(3ull * (uint64_t)pv) > t2;
-            qn = (int64_t)(3ull * (uint64_t)pn) > t2;
-            qa = (int64_t)(3ull * ((uint64_t)pv + (uint64_t)pn)) > t2;
-            q3 = (int64_t)(3ull * (uint64_t)ps) > totl;
+    /* K3: is_quorum precedence Value > Nil > Any > Init (round_votes.rs:58-66) and
+     * to_event (vote_executor.rs:26-36) */
+    uint32_t code[SUBS];
+#pragma unroll
+    for (uint32_t s = 0; s < SUBS; ++s) {
+        if (!ok[s]) {
+            code[s] = AGNES_CODE_INVALID;
+        } else if (!acc[s]) {
+            code[s] = AGNES_CODE_REJECTED;
         } else {
-            qv = (uint32_t)pv > q2l;
-            qn = (uint32_t)pn > q2l;
-            qa = (uint32_t)pv + (uint32_t)pn > q2l;
-            q3 = (uint32_t)ps > q1l;
+            bool qv, qn, qa, q3;
+            if (WIDE) { /* literal i64 wrapping: round_votes.rs:32 */
+                const int64_t t2 = (int64_t)(2ull * (uint64_t)in_.total);
+                qv = (int64_t)(3ull * (uint64_t)pv[s]) > t2;
+                qn = (int64_t)(3ull * (uint64_t)pn[s]) > t2;
+                qa = (int64_t)(3ull * ((uint64_t)pv[s] + (uint64_t)pn[s])) > t2;
+                q3 = (int64_t)(3ull * (uint64_t)ps[s]) > in_.total;
+            } else {
+                qv = (uint32_t)pv[s] > in_.q2;
+                qn = (uint32_t)pn[s] > in_.q2;
+                qa = (uint32_t)pv[s] + (uint32_t)pn[s] > in_.q2;
+                q3 = (uint32_t)ps[s] > in_.q1;
+            }
+            const uint32_t t = x.t[s];
+            const uint32_t ev = qv ? (t ? AGNES_CODE_PRECOMMIT_VALUE : AGNES_CODE_POLKA_VALUE)
+                              : qn ? (t ? AGNES_CODE_NONE : AGNES_CODE_POLKA_NIL)
+                              : qa ? (t ? AGNES_CODE_PRECOMMIT_ANY : AGNES_CODE_POLKA_ANY)
+                                   : AGNES_CODE_NONE;
+            code[s] = ev | ((SKIP && q3) ? AGNES_CODE_SKIP : 0u);
         }
-        const uint32_t ev = qv ? (f.t ? AGNES_CODE_PRECOMMIT_VALUE : AGNES_CODE_POLKA_VALUE)
-                          : qn ? (f.t ? AGNES_CODE_NONE : AGNES_CODE_POLKA_NIL)
-                          : qa ? (f.t ? AGNES_CODE_PRECOMMIT_ANY : AGNES_CODE_POLKA_ANY)
-                               : AGNES_CODE_NONE;
-        code = ev | ((SKIP && q3) ? AGNES_CODE_SKIP : 0u);
     }
 
-    /* K4: State::apply(v.round, event) per instance in stream order
-     * (consensus_executor.rs:64-68) */
+    /* K4: State::apply(v.round, event) in stream order (consensus_executor.rs:64-68):
+     * each pass classifies every pending vote of the chunk against the current
+     * (wave-uniform) state; votes before the first state change get their message,
+     * the changing vote is applied on the scalar path, repeat */
     if (SM) {
-        const uint32_t evc = code & AGNES_CODE_EVENT_MASK;
-        const bool skp = (code & AGNES_CODE_SKIP) != 0u;
-        const bool pend_any = acc && (code & 0x0Fu) != 0u;
-        uint32_t msg = 0;
-        for (uint32_t k = ch.cur; k <= ch.last; ++k) {
-            Sm s = (k == ch.cur) ? st : (k == ch.cur + 1u ? st_next : sm_load(&a.states[k]));
-            uint64_t P2 = ballot(pend_any && myi == k);
-            while (P2 && s.step != AGNES_STEP_COMMIT) {
-                const SmTab tb = sm_tab(s);
-                bool change;
-                uint32_t cm;
-                sm_classify(tb, f.r, evc, lab, skp, change, cm);
-                const bool inP = (P2 >> lane) & 1ull;
-                const uint64_t Cm = ballot(inP && change);
-                const uint32_t first = Cm ? (uint32_t)__builtin_ctzll(Cm) : 64u;
-                if (inP && lane < first) msg = cm;
-                if (!Cm) break;
-                const int64_t fr = (int64_t)rdl(f.r, first);
-                const uint32_t fev = rdl(evc, first);
-                const uint32_t flab = rdl(lab, first);
-                const bool fsk = rdl((uint32_t)skp, first) != 0u;
-                MsgOut m1, m2;
-                bool h1 = false, h2 = false;
-                if (fsk) h1 = sm_apply(s, fr, AGNES_EV_ROUND_SKIP, 0u, 0, a.flags, m1);
-                if (fev) h2 = sm_apply(s, fr, fev + 3u, flab, 0, a.flags, m2);
-                const uint32_t vm = vmsg_of(h1, h2, m2);
-                if (lane == first) msg = vm;
-                P2 = first >= 63u ? 0ull : (P2 & (~0ull << (first + 1u)));
-            }
-            if (k == ch.last && ch.last_continues) st = s;
-            else if (lane == 0) sm_store(&a.states[k], s);
+        uint32_t msg[SUBS];
+        uint64_t pend[SUBS];
+#pragma unroll
+        for (uint32_t s = 0; s < SUBS; ++s) {
+            msg[s] = 0;
+            pend[s] = ballot(acc[s] && (code[s] & 0x0Fu) != 0u);
         }
-        code |= msg << AGNES_CODE_MSG_SHIFT;
+        while (st.step != AGNES_STEP_COMMIT && (pend[0] | pend[1] | pend[2] | pend[3])) {
+            const SmTab tb = sm_tab(st);
+            uint32_t first = 0xFFFFFFFFu; /* chunk position s*64+lane of the first change */
+            uint32_t cm[SUBS];
+#pragma unroll
+            for (uint32_t s = 0; s < SUBS; ++s) {
+                bool chg;
+                sm_classify(tb, x.r[s], code[s] & AGNES_CODE_EVENT_MASK, lab[s],
+                            (code[s] & AGNES_CODE_SKIP) != 0u, chg, cm[s]);
+                const uint64_t bk = ballot(chg && ((pend[s] >> lane) & 1ull));
+                if (first == 0xFFFFFFFFu && bk) first = 64u * s + (uint32_t)__builtin_ctzll(bk);
+            }
+#pragma unroll
+            for (uint32_t s = 0; s < SUBS; ++s)
+                if (((pend[s] >> lane) & 1ull) && 64u * s + lane < first) msg[s] = cm[s];
+            if (first == 0xFFFFFFFFu) break;
+            const uint32_t fs = first >> 6, fl = first & 63u;
+            const int64_t fr = (int64_t)rdl(pick4(x.r, fs), fl);
+            const uint32_t fcode = rdl(pick4(code, fs), fl);
+            const uint32_t flab = rdl(pick4(lab, fs), fl);
+            const uint32_t fev = fcode & AGNES_CODE_EVENT_MASK;
+            MsgOut m1, m2;
+            bool h1 = false, h2 = false;
+            if (fcode & AGNES_CODE_SKIP) h1 = sm_apply(st, fr, AGNES_EV_ROUND_SKIP, 0u, 0, a.flags, m1);
+            if (fev) h2 = sm_apply(st, fr, fev + 3u, flab, 0, a.flags, m2);
+            const uint32_t vm = vmsg_of(h1, h2, m2);
+#pragma unroll
+            for (uint32_t s = 0; s < SUBS; ++s) {
+                if (64u * s + lane == first) msg[s] = vm;
+                /* drop every vote up to and including the change */
+                if (64u * s + 63u <= first) pend[s] = 0;
+                else if (64u * s <= first) pend[s] &= ~0ull << (first - 64u * s + 1u);
+            }
+        }
+#pragma unroll
+        for (uint32_t s = 0; s < SUBS; ++s) code[s] |= msg[s] << AGNES_CODE_MSG_SHIFT;
     }
-    if (valid) a.codes[j] = (uint8_t)code;
+
+#pragma unroll
+    for (uint32_t s = 0; s < SUBS; ++s)
+        if (valid[s]) a.codes[c + 64u * s + lane] = (uint8_t)code[s];
 }
 
-template <uint32_t MODE, bool SKIP, bool SM>
+/* Per wave: a contiguous range of instances (or, LIST, the deferred instances
+ * grid-strided), one instance at a time, 256-vote chunks, the next chunk's loads
+ * in flight while this one computes.  FAST kernels defer instances whose sums
+ * could reach 2^31 (or whose set is not fast) to the WIDE LIST kernel. */
+template <bool WIDE, uint32_t MODE, bool SKIP, bool SM, bool LIST>
 __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t lds_per_wave) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t lane = lane_id();
@@ -646,217 +676,135 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
     const agnes_vote_batch& vb = a.vb;
     const uint32_t n = vb.n_instances;
     const uint64_t NV = vb.n_votes;
-
-    /* contiguous instance range of this wave: one vote stream */
     const uint32_t Wn = gridDim.x * AGNES_WAVES_PER_BLOCK;
     const uint32_t gw = blockIdx.x * AGNES_WAVES_PER_BLOCK + wave;
-    const uint32_t ia = (uint32_t)(((uint64_t)n * gw) / Wn);
-    const uint32_t ib = (uint32_t)(((uint64_t)n * (gw + 1u)) / Wn);
-    if (ia >= ib) return;
+
+    uint32_t q0, qend, qstep;
+    if (LIST) {
+        q0 = gw;
+        qend = rfl(*(volatile uint32_t*)a.list_count);
+        qstep = Wn;
+    } else {
+        q0 = (uint32_t)(((uint64_t)n * gw) / Wn);
+        qend = (uint32_t)(((uint64_t)n * (gw + 1u)) / Wn);
+        qstep = 1;
+    }
+    if (q0 >= qend) return;
 
     uint64_t o_fv, o_fs, o_tot;
     lds_layout(MODE, SKIP ? AGNES_FLAG_ROUND_SKIP : 0u, R, nv, &o_fv, &o_fs, &o_tot);
     unsigned char* base = smem + (uint64_t)wave * lds_per_wave;
     WaveLds L;
-    L.cbase = base;
-    L.cbytes = (uint32_t)align16(48ull * R);
-    L.R = R;
+    L.vw = reinterpret_cast<uint64_t*>(base);
+    L.vn = L.vw + 2u * R;
+    L.skw = L.vn + 2u * R;
+    L.lv = reinterpret_cast<uint32_t*>(L.skw + R);
     L.first_v = reinterpret_cast<uint32_t*>(base + o_fv);
     L.first_s = reinterpret_cast<uint32_t*>(base + o_fs);
+    const bool tables = MODE == AGNES_MODE_DEDUP || SKIP;
     if (MODE == AGNES_MODE_DEDUP) fill_u32(L.first_v, 2ull * R * nv, 0u, lane);
     if (SKIP) fill_u32(L.first_s, (uint64_t)R * nv, 0u, lane);
-
-    const uint32_t lb = a.epoch_shift;               /* bits of the local vote index */
-    const uint32_t emax = lb >= 31u ? 1u : ((1u << (32u - lb)) - 1u); /* epochs per table fill */
-    const bool tables = MODE == AGNES_MODE_DEDUP || SKIP;
+    const uint32_t lb = a.epoch_shift;                                /* bits of a local vote index */
+    const uint32_t emax = lb >= 31u ? 1u : ((1u << (32u - lb)) - 1u); /* epochs per table fill      */
+    uint32_t ep = 0;
 
     auto off_at = [&](uint32_t k) -> uint64_t {
         const uint64_t o = vb.offsets[k];
         return o < NV ? o : NV;
     };
-    const uint64_t v0 = rfl64(off_at(ia));
-    uint64_t vend = rfl64(off_at(ib));
-    vend = vend > v0 ? vend : v0;
+    /* contiguous mode: the wave's votes end at vend; the next chunk is prefetched */
+    const uint64_t vend = LIST ? NV : rfl64(off_at(qend));
+    uint64_t pf_at = ~0ull;
+    Raw pf;
+    uint32_t bad_lane = 0;
 
-    Window win;
-    uint32_t vbase = ia;
-    auto load_window = [&](uint32_t b) {
-        vbase = b;
-        const uint32_t k = b + lane;
-        const bool in = k < ib;
-        const uint64_t st = in ? off_at(k) : vend;
-        const uint64_t en = in ? off_at(k + 1u) : vend;
-        uint32_t set = 0;
-        if (in) set = vb.instance_set ? vb.instance_set[k] : (a.n_sets ? k % a.n_sets : 0u);
-        const bool sok = in && set < a.n_sets;
+    for (uint32_t q = q0; q < qend; q += qstep) {
+        Inst I;
+        I.i = LIST ? rfl(a.list[q]) : q;
+        I.beg = rfl64(off_at(I.i));
+        uint64_t e = rfl64(off_at(I.i + 1u));
+        I.end = e > I.beg ? e : I.beg;
+        uint32_t set = vb.instance_set ? vb.instance_set[I.i] : (a.n_sets ? I.i % a.n_sets : 0u);
+        set = rfl(set);
+        I.set_ok = set < a.n_sets;
         agnes_set_info si;
-        if (sok) {
+        if (I.set_ok) {
             si = a.sets[set];
         } else {
             si.total = 0;
             si.q2 = si.q1 = si.maxpow = si.fast = 0;
         }
-        const uint64_t len = en > st ? en - st : 0ull;
-        const bool fast = sok && si.fast && vb.weight == nullptr && a.carry == nullptr &&
-                          len < (1ull << 32) && len * (uint64_t)si.maxpow < (1ull << 31);
-        win.end = en;
-        win.tot = si.total;
-        win.q2 = si.q2;
-        win.q1 = si.q1;
-        win.pb = set * nv;
-        win.fl = (sok ? 1u : 0u) | (fast ? 2u : 0u);
-    };
-    auto endof = [&](uint32_t k) -> uint64_t { return rdl(win.end, k - vbase); };
-    load_window(ia);
-
-    uint64_t n_bad = 0;
-    uint64_t c = v0;
-    uint32_t cur = ia;
-    bool open = false;
-    uint64_t cur_start = v0;
-    uint32_t ebase = ia;
-    uint32_t pp = 0;
-    Sm st, st_next;
-    Fields f = load_fields(vb, c + lane, c + lane < vend);
-
-    while (c < vend) {
-        /* instance containing vote c */
-        for (;;) {
-            if (cur >= ib) break;
-            if (cur - vbase >= 64u) load_window(cur);
-            if (endof(cur) > c) break;
-            ++cur;
-            open = false;
+        I.pbase = set * nv;
+        I.q2 = si.q2;
+        I.q1 = si.q1;
+        I.total = si.total;
+        if (!WIDE) { /* sums provably < 2^31: u32 arithmetic; otherwise defer to WIDE */
+            const uint64_t len = I.end - I.beg;
+            const bool fast = !I.set_ok || (si.fast && len < (1ull << 32) &&
+                                            len * (uint64_t)si.maxpow < (1ull << 31));
+            if (!fast) {
+                if (lane == 0) a.list[atomicAdd(a.list_count, 1u)] = I.i;
+                continue;
+            }
         }
-        if (cur >= ib) break; /* malformed offsets */
-        if (cur - vbase >= 32u && vbase + 64u < ib) load_window(cur);
+        if (I.beg == I.end) continue; /* no votes: executors and State untouched */
 
-        if (!open) { /* RoundVotes::new for every round (round_votes.rs:83-90) + State */
-            cur_start = c;
-            if (tables && cur - ebase + 1u > emax) { /* epoch space used up: clear tables */
+        /* RoundVotes::new for every round (round_votes.rs:83-90) */
+        if (tables) {
+            if (++ep > emax) { /* epoch space used up: recycle the tables */
                 if (MODE == AGNES_MODE_DEDUP) fill_u32(L.first_v, 2ull * R * nv, 0u, lane);
                 if (SKIP) fill_u32(L.first_s, (uint64_t)R * nv, 0u, lane);
-                ebase = cur;
+                ep = 1;
             }
+        }
+        I.ep = ep;
+        for (uint32_t k = lane; k < 2u * R; k += 64) {
             if (a.carry) {
-                const CarryBuf cb = carry_buf(L, pp);
-                for (uint32_t k = lane; k < 2u * R; k += 64) {
-                    const agnes_carry_rec cr = a.carry[(uint64_t)cur * 2u * R + k];
-                    cb.vw[k] = (uint64_t)cr.value_w;
-                    cb.vn[k] = (uint64_t)cr.nil_w;
-                    cb.lv[k] = cr.value;
-                }
-                for (uint32_t k = lane; k < R; k += 64) cb.skw[k] = 0;
+                const agnes_carry_rec cr = a.carry[(uint64_t)I.i * 2u * R + k];
+                L.vw[k] = (uint64_t)cr.value_w;
+                L.vn[k] = (uint64_t)cr.nil_w;
+                L.lv[k] = cr.value;
             } else {
-                zero_carry(carry_buf(L, pp), R, lane);
+                L.vw[k] = 0;
+                L.vn[k] = 0;
+                L.lv[k] = 0;
             }
-            if (SM) st = sm_load(&a.states[cur]);
-            open = true;
+        }
+        for (uint32_t k = lane; k < R; k += 64) L.skw[k] = 0;
+        Sm st;
+        if (SM) st = sm_load(&a.states[I.i]);
+        __builtin_amdgcn_wave_barrier();
+
+        for (uint64_t c = I.beg; c < I.end; c += CHUNK) {
+            const uint64_t cl = c + CHUNK < I.end ? c + CHUNK : I.end;
+            Raw x;
+            if (pf_at == c) {
+                x = pf;
+            } else {
+                load_raw(vb, c, cl, x);
+            }
+            if (!LIST && cl < vend) { /* next chunk (this instance or the next one) */
+                load_raw(vb, cl, vend, pf);
+                pf_at = cl;
+            }
+            process_chunk<WIDE, MODE, SKIP, SM>(a, L, I, c, cl, x, st, lb, bad_lane);
             __builtin_amdgcn_wave_barrier();
         }
-
-        /* chunk [c, cl): <= 64 votes, never past the window or the epoch budget */
-        uint64_t cl = c + 64u < vend ? c + 64u : vend;
-        if (vbase + 63u < ib) {
-            const uint64_t e = endof(vbase + 63u);
-            cl = e < cl ? e : cl;
-        }
-        if (tables) {
-            const uint64_t kcut = (uint64_t)ebase + emax - 1u;
-            if (kcut < ib && kcut <= (uint64_t)vbase + 63u) {
-                const uint64_t e = endof((uint32_t)kcut);
-                cl = e < cl ? e : cl;
+        if (SM && lane == 0) sm_store(&a.states[I.i], st);
+        if (a.carry) { /* persist the executors */
+            for (uint32_t k = lane; k < 2u * R; k += 64) {
+                agnes_carry_rec cr;
+                cr.value_w = (int64_t)L.vw[k];
+                cr.nil_w = (int64_t)L.vn[k];
+                cr.value = L.lv[k];
+                cr.pad = 0;
+                a.carry[(uint64_t)I.i * 2u * R + k] = cr;
             }
         }
-        if (a.carry) {
-            const uint64_t e = endof(cur);
-            cl = e < cl ? e : cl;
-        }
-
-        /* next chunk's fields in flight while this one computes */
-        const Fields fn = load_fields(vb, cl + lane, cl + lane < vend);
-
-        /* lane -> instance map: walk the boundaries inside the chunk */
-        const uint64_t j = c + lane;
-        const uint32_t wl = cur - vbase;
-        uint32_t myi = cur, head = 0;
-        uint32_t q2l = rdl(win.q2, wl), q1l = rdl(win.q1, wl), pbl = rdl(win.pb, wl);
-        int64_t totl = (int64_t)rdl((uint64_t)win.tot, wl);
-        uint32_t fll = rdl(win.fl, wl);
-        uint32_t fast_all = fll;
-        uint32_t k = cur, m = 0, hl = 0;
-        for (;;) {
-            const uint64_t ek = endof(k);
-            if (ek >= cl || k + 1u >= ib) break;
-            ++k;
-            ++m;
-            const uint32_t h = (uint32_t)(ek > c ? ek - c : 0u);
-            const uint32_t wk = k - vbase;
-            const uint32_t kq2 = rdl(win.q2, wk), kq1 = rdl(win.q1, wk), kpb = rdl(win.pb, wk);
-            const int64_t ktot = (int64_t)rdl((uint64_t)win.tot, wk);
-            const uint32_t kfl = rdl(win.fl, wk);
-            fast_all &= kfl;
-            if (j >= ek) {
-                myi = k;
-                head = h;
-                q2l = kq2;
-                q1l = kq1;
-                pbl = kpb;
-                totl = ktot;
-                fll = kfl;
-            }
-            hl = h;
-        }
-        Chunk chk;
-        chk.c = c;
-        chk.nvalid = (uint32_t)(cl - c);
-        chk.cur = cur;
-        chk.last = k;
-        chk.m = m;
-        chk.hl = hl;
-        chk.cur_start = cur_start;
-        chk.ebase = ebase;
-        chk.last_continues = endof(k) > cl;
-        if (SM && m != 0u) st_next = sm_load(&a.states[cur + 1u]);
-        if (chk.last_continues && m != 0u) zero_carry(carry_buf(L, pp ^ 1u), R, lane);
         __builtin_amdgcn_wave_barrier();
-
-        const bool setok = (fll & 1u) != 0u;
-        if (fast_all & 2u)
-            process_chunk<false, MODE, SKIP, SM>(a, L, pp, chk, f, myi, head, q2l, q1l, totl, pbl,
-                                                 setok, st, st_next, lb, n_bad);
-        else
-            process_chunk<true, MODE, SKIP, SM>(a, L, pp, chk, f, myi, head, q2l, q1l, totl, pbl,
-                                                setok, st, st_next, lb, n_bad);
-        __builtin_amdgcn_wave_barrier();
-
-        /* the instance open after this chunk */
-        if (chk.last_continues) {
-            if (m != 0u) {
-                pp ^= 1u;
-                cur_start = c + hl;
-            }
-            cur = k;
-            open = true;
-        } else {
-            if (a.carry) { /* persist the finished executors */
-                const CarryBuf cb = carry_buf(L, pp);
-                for (uint32_t q = lane; q < 2u * R; q += 64) {
-                    agnes_carry_rec cr;
-                    cr.value_w = (int64_t)cb.vw[q];
-                    cr.nil_w = (int64_t)cb.vn[q];
-                    cr.value = cb.lv[q];
-                    cr.pad = 0;
-                    a.carry[(uint64_t)cur * 2u * R + q] = cr;
-                }
-            }
-            cur = k + 1u;
-            open = false;
-        }
-        c = cl;
-        f = fn;
     }
-    if (lane == 0 && n_bad) atomicAdd(a.n_invalid, (unsigned long long)n_bad);
+    const uint32_t nb = rdl(scan(bad_lane), 63u);
+    if (lane == 0 && nb) atomicAdd(a.n_invalid, (unsigned long long)nb);
 }
 
 /* ------------------------------------------------------------------ */
@@ -923,51 +871,62 @@ int64_t agnes_lds_per_wave(uint32_t mode, uint32_t flags, uint32_t max_rounds, u
     return (int64_t)tot;
 }
 
-template <uint32_t MODE, bool SKIP, bool SM>
-static hipError_t launch_t(const agnes_tally_args* a, uint32_t lpw, int num_cus, hipStream_t st) {
+template <bool WIDE, uint32_t MODE, bool SKIP, bool SM, bool LIST>
+static hipError_t launch_k(const agnes_tally_args* a, uint32_t lpw, int num_cus, hipStream_t st) {
     const uint32_t n = a->vb.n_instances;
     if (n == 0) return hipSuccess;
-    uint64_t blocks = (n + AGNES_WAVES_PER_BLOCK - 1) / AGNES_WAVES_PER_BLOCK;
     const uint64_t lds = (uint64_t)lpw * AGNES_WAVES_PER_BLOCK;
-    const void* fn = reinterpret_cast<const void*>(&agnes::tally_kernel<MODE, SKIP, SM>);
+    const void* fn = reinterpret_cast<const void*>(&agnes::tally_kernel<WIDE, MODE, SKIP, SM, LIST>);
     if (lds > 48u * 1024u) {
         hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    /* every wave owns an equal slice of the instances: launch exactly the
-     * resident grid (blocks per CU from the occupancy query, cached per LDS size) */
+    /* every wave owns an equal slice of the instances: launch the resident grid
+     * (blocks per CU from the occupancy query, cached per LDS size) */
     static thread_local uint64_t cached_lds = ~0ull;
     static thread_local int cached_per_cu = 0;
     if (cached_lds != lds) {
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, (size_t)lds) !=
-                hipSuccess || per_cu < 1)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, (size_t)lds) != hipSuccess ||
+            per_cu < 1)
             per_cu = 1;
         cached_lds = lds;
         cached_per_cu = per_cu;
     }
     const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256) * (uint64_t)cached_per_cu;
+    uint64_t blocks = (n + AGNES_WAVES_PER_BLOCK - 1) / AGNES_WAVES_PER_BLOCK;
     if (blocks > cap) blocks = cap;
-    hipLaunchKernelGGL((agnes::tally_kernel<MODE, SKIP, SM>), dim3((uint32_t)blocks), dim3(256),
+    if (LIST && blocks > (uint64_t)(num_cus > 0 ? num_cus : 256)) blocks = (uint64_t)(num_cus > 0 ? num_cus : 256);
+    hipLaunchKernelGGL((agnes::tally_kernel<WIDE, MODE, SKIP, SM, LIST>), dim3((uint32_t)blocks), dim3(256),
                        (size_t)lds, st, *a, lpw);
     return hipGetLastError();
 }
 
-hipError_t agnes_launch_tally(const agnes_tally_args* a, uint32_t mode, int num_cus,
+template <uint32_t MODE, bool SKIP, bool SM>
+static hipError_t launch_mode(const agnes_tally_args* a, uint32_t lpw, int num_cus, bool wide_all,
+                              hipStream_t st) {
+    if (wide_all) return launch_k<true, MODE, SKIP, SM, false>(a, lpw, num_cus, st);
+    hipError_t e = hipMemsetAsync(a->list_count, 0, sizeof(uint32_t), st);
+    if (e == hipSuccess) e = launch_k<false, MODE, SKIP, SM, false>(a, lpw, num_cus, st);
+    if (e == hipSuccess) e = launch_k<true, MODE, SKIP, SM, true>(a, lpw, num_cus, st);
+    return e;
+}
+
+hipError_t agnes_launch_tally(const agnes_tally_args* a, uint32_t mode, int num_cus, bool wide_all,
                               hipStream_t st) {
     const bool skip = (a->flags & AGNES_FLAG_ROUND_SKIP) != 0;
     const bool sm = (a->flags & AGNES_FLAG_STATE_MACHINE) != 0 && a->states != nullptr;
     const uint32_t lpw = (uint32_t)agnes_lds_per_wave(mode, a->flags, a->max_rounds, a->n_vals);
     if (mode == AGNES_MODE_DEDUP) {
-        if (skip) return sm ? launch_t<1, true, true>(a, lpw, num_cus, st)
-                            : launch_t<1, true, false>(a, lpw, num_cus, st);
-        return sm ? launch_t<1, false, true>(a, lpw, num_cus, st)
-                  : launch_t<1, false, false>(a, lpw, num_cus, st);
+        if (skip) return sm ? launch_mode<1, true, true>(a, lpw, num_cus, wide_all, st)
+                            : launch_mode<1, true, false>(a, lpw, num_cus, wide_all, st);
+        return sm ? launch_mode<1, false, true>(a, lpw, num_cus, wide_all, st)
+                  : launch_mode<1, false, false>(a, lpw, num_cus, wide_all, st);
     }
-    if (skip) return sm ? launch_t<0, true, true>(a, lpw, num_cus, st)
-                        : launch_t<0, true, false>(a, lpw, num_cus, st);
-    return sm ? launch_t<0, false, true>(a, lpw, num_cus, st)
-              : launch_t<0, false, false>(a, lpw, num_cus, st);
+    if (skip) return sm ? launch_mode<0, true, true>(a, lpw, num_cus, wide_all, st)
+                        : launch_mode<0, true, false>(a, lpw, num_cus, wide_all, st);
+    return sm ? launch_mode<0, false, true>(a, lpw, num_cus, wide_all, st)
+              : launch_mode<0, false, false>(a, lpw, num_cus, wide_all, st);
 }
 
 hipError_t agnes_launch_apply_events(agnes_state* states, uint32_t n, const uint64_t* off,

@@ -355,6 +355,19 @@ def test_ragged_tiny_and_empty_instances(eng, mode, flags):
     assert_same(g, o)
 
 
+@pytest.mark.parametrize("mode,flags", [
+    (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE),
+    (abi.MODE_DEDUP, abi.FLAG_STATE_MACHINE | abi.FLAG_ROUND_SKIP)])
+def test_early_quorum_labels(eng, mode, flags):
+    """Two equal validators: every second vote crosses a threshold, so nil votes
+    carry Value events whose label comes from another lane / tile / instance."""
+    hb = _ragged_batch(8, 30000, 2, 2, [1, 2, 3, 4, 5, 7, 9, 17, 33, 80])
+    power = np.ones((1, 2), np.int64)
+    cfg = abi.config(mode, flags, 2)
+    g, o = run_both(eng, cfg, hb, power, None, _start_states(hb.n_instances))
+    assert_same(g, o)
+
+
 def test_epoch_table_recycling(eng, monkeypatch):
     """DEDUP/RoundSkip tables tag entries with per-instance epochs; with few
     epoch bits the tables are cleared every 3 instances (chunks cut there)."""

@@ -20,6 +20,9 @@ VARIANTS = {
                  (abi.POWER_UNIFORM, 1, 1000, 1), abi.MODE_REFERENCE, 0, 1),
     "c2_sm": (dict(n_instances=1_000_000, n_vals=100, nil_permille=200),
               (abi.POWER_UNIFORM, 1, 1000, 1), abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 1),
+    "c2_sm_commit": (dict(n_instances=1_000_000, n_vals=100, nil_permille=200),
+                     (abi.POWER_UNIFORM, 1, 1000, 1), abi.MODE_REFERENCE,
+                     abi.FLAG_STATE_MACHINE, 1),
     "c2_sm_phased": (dict(n_instances=1_000_000, n_vals=100, nil_permille=200,
                           order=abi.ORDER_PHASED),
                      (abi.POWER_UNIFORM, 1, 1000, 1), abi.MODE_REFERENCE,
@@ -42,7 +45,8 @@ def run(eng, name, iters):
     eng.upload_power(eng.gen_power(0xA6E5, n_sets, p.n_vals, kind, lo, hi))
     b = eng.gen_batch(p)
     cfg = abi.config(mode, flags, R)
-    st0 = states_to_device(abi.new_states(p.n_instances, 1, abi.STEP_PREVOTE), eng.device)
+    step0 = abi.STEP_COMMIT if name.endswith("_commit") else abi.STEP_PREVOTE
+    st0 = states_to_device(abi.new_states(p.n_instances, 1, step0), eng.device)
     st = torch.empty_like(st0)
     codes = torch.empty(b.n_votes, dtype=torch.uint8, device=eng.device)
     stream = torch.cuda.current_stream()
@@ -73,10 +77,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("variants", nargs="*", default=list(VARIANTS))
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--dbg", default="", help="comma list of AGNES_DEBUG_SKIP values to sweep")
     args = ap.parse_args()
     eng = Engine(0)
-    for v in args.variants:
-        run(eng, v, args.iters)
+    for d in (args.dbg.split(",") if args.dbg else [None]):
+        if d is not None:
+            os.environ["AGNES_DEBUG_SKIP"] = d
+            print(json.dumps({"AGNES_DEBUG_SKIP": d}), flush=True)
+        for v in args.variants:
+            run(eng, v, args.iters)
 
 
 if __name__ == "__main__":
