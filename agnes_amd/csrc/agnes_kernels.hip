@@ -331,6 +331,64 @@ __device__ __forceinline__ T pick4(const T (&x)[4], uint32_t e) { /* e wave-unif
     return e == 0 ? x[0] : (e == 1 ? x[1] : (e == 2 ? x[2] : x[3]));
 }
 
+/* State::apply for the events a vote can produce (RoundSkip, then the tally
+ * event at the vote's round), state_machine.rs:196-211 restricted to those arms;
+ * returns the message nibble.  Equivalent to sm_apply + vmsg_of for these events. */
+__device__ __forceinline__ uint32_t sm_vote(Sm& s, int64_t r, uint32_t code, uint32_t lab) {
+    if (s.step == AGNES_STEP_COMMIT) return AGNES_VMSG_NONE; /* :205 */
+    bool nr = false;
+    if ((code & AGNES_CODE_SKIP) && s.round < r) { /* :210 round_skip */
+        s.round = r;
+        s.step = AGNES_STEP_NEW_ROUND;
+        nr = true;
+    }
+    uint32_t b = AGNES_VMSG_NONE;
+    const bool eqr = s.round == r;
+    switch (code & AGNES_CODE_EVENT_MASK) {
+    case AGNES_CODE_POLKA_ANY: /* :196 */
+        if (eqr && s.step == AGNES_STEP_PREVOTE) b = AGNES_VMSG_TIMEOUT_PREVOTE;
+        break;
+    case AGNES_CODE_POLKA_NIL: /* :197 precommit_nil */
+        if (eqr && s.step == AGNES_STEP_PREVOTE) {
+            s.step = AGNES_STEP_PRECOMMIT;
+            b = AGNES_VMSG_PRECOMMIT_NIL;
+        }
+        break;
+    case AGNES_CODE_POLKA_VALUE:
+        if (eqr && s.step == AGNES_STEP_PREVOTE) { /* :198 precommit */
+            s.locked = 1;
+            s.locked_round = s.round;
+            s.locked_value = lab;
+            s.valid = 1;
+            s.valid_round = s.round;
+            s.valid_value = lab;
+            s.step = AGNES_STEP_PRECOMMIT;
+            b = AGNES_VMSG_PRECOMMIT_VALUE;
+        } else if (eqr && s.step == AGNES_STEP_PRECOMMIT) { /* :202 set_valid_value */
+            s.valid = 1;
+            s.valid_round = s.round;
+            s.valid_value = lab;
+        }
+        break;
+    case AGNES_CODE_PRECOMMIT_ANY: /* :208 */
+        if (eqr) b = AGNES_VMSG_TIMEOUT_PRECOMMIT;
+        break;
+    case AGNES_CODE_PRECOMMIT_VALUE: /* :211 commit */
+        s.step = AGNES_STEP_COMMIT;
+        s.decided = 1;
+        s.decision_round = r;
+        s.decision_value = lab;
+        b = AGNES_VMSG_DECISION;
+        break;
+    default:
+        break;
+    }
+    if (nr) return b == AGNES_VMSG_TIMEOUT_PRECOMMIT ? AGNES_VMSG_NEW_ROUND_TIMEOUT_PRECOMMIT
+                 : b == AGNES_VMSG_DECISION           ? AGNES_VMSG_NEW_ROUND_DECISION
+                                                      : AGNES_VMSG_NEW_ROUND;
+    return b;
+}
+
 /* ------------------------------------------------------------------ */
 /* LDS of one wave: the executors of the instance being tallied        */
 
@@ -421,7 +479,7 @@ template <bool WIDE, uint32_t MODE, bool SKIP, bool SM>
 __device__ __forceinline__ void process_chunk(const agnes_tally_args& a, const WaveLds& L,
                                               const Inst& in_, uint64_t c, uint64_t cl,
                                               const Raw& x, Sm& st, uint32_t lb,
-                                              uint32_t& bad_lane) {
+                                              uint32_t& bad_lane, bool ld_carry, bool st_carry) {
     using W = typename std::conditional<WIDE, uint64_t, uint32_t>::type;
     const uint32_t lane = lane_id();
     const uint32_t R = a.max_rounds;
@@ -507,8 +565,13 @@ __device__ __forceinline__ void process_chunk(const agnes_tally_args& a, const W
         for (uint32_t s = 0; s < SUBS; ++s)
             if (key == 0xFFFFFFFFu && rem[s]) key = rdl(slot[s], (uint32_t)__builtin_ctzll(rem[s]));
         if (key == 0xFFFFFFFFu) break;
-        W cv = (W)L.vw[key], cn = (W)L.vn[key];
-        uint32_t lbl = track ? L.lv[key] : 0u;
+        W cv = 0, cn = 0;
+        uint32_t lbl = 0;
+        if (ld_carry) {
+            cv = (W)L.vw[key];
+            cn = (W)L.vn[key];
+            if (track) lbl = L.lv[key];
+        }
 #pragma unroll
         for (uint32_t s = 0; s < SUBS; ++s) {
             const bool in = acc[s] && slot[s] == key;
@@ -539,9 +602,11 @@ __device__ __forceinline__ void process_chunk(const agnes_tally_args& a, const W
                 if (mv) lbl = rdl(x.value[s], 63u - (uint32_t)__builtin_clzll(mv));
             }
         }
-        L.vw[key] = (uint64_t)cv;
-        L.vn[key] = (uint64_t)cn;
-        if (track) L.lv[key] = lbl;
+        if (st_carry) {
+            L.vw[key] = (uint64_t)cv;
+            L.vn[key] = (uint64_t)cn;
+            if (track) L.lv[key] = lbl;
+        }
         __builtin_amdgcn_wave_barrier();
     }
 
@@ -559,7 +624,7 @@ __device__ __forceinline__ void process_chunk(const agnes_tally_args& a, const W
             for (uint32_t s = 0; s < SUBS; ++s)
                 if (kr == 0xFFFFFFFFu && rem[s]) kr = rdl(x.r[s], (uint32_t)__builtin_ctzll(rem[s]));
             if (kr == 0xFFFFFFFFu) break;
-            W cs = (W)L.skw[kr];
+            W cs = ld_carry ? (W)L.skw[kr] : (W)0;
 #pragma unroll
             for (uint32_t s = 0; s < SUBS; ++s) {
                 const bool in = acc[s] && x.r[s] == kr;
@@ -570,7 +635,7 @@ __device__ __forceinline__ void process_chunk(const agnes_tally_args& a, const W
                 if (in) ps[s] = cs + ss;
                 cs += rdl(ss, 63u);
             }
-            L.skw[kr] = (uint64_t)cs;
+            if (st_carry) L.skw[kr] = (uint64_t)cs;
             __builtin_amdgcn_wave_barrier();
         }
     }
@@ -639,12 +704,7 @@ __device__ __forceinline__ void process_chunk(const agnes_tally_args& a, const W
             const int64_t fr = (int64_t)rdl(pick4(x.r, fs), fl);
             const uint32_t fcode = rdl(pick4(code, fs), fl);
             const uint32_t flab = rdl(pick4(lab, fs), fl);
-            const uint32_t fev = fcode & AGNES_CODE_EVENT_MASK;
-            MsgOut m1, m2;
-            bool h1 = false, h2 = false;
-            if (fcode & AGNES_CODE_SKIP) h1 = sm_apply(st, fr, AGNES_EV_ROUND_SKIP, 0u, 0, a.flags, m1);
-            if (fev) h2 = sm_apply(st, fr, fev + 3u, flab, 0, a.flags, m2);
-            const uint32_t vm = vmsg_of(h1, h2, m2);
+            const uint32_t vm = sm_vote(st, fr, fcode, flab);
 #pragma unroll
             for (uint32_t s = 0; s < SUBS; ++s) {
                 if (64u * s + lane == first) msg[s] = vm;
@@ -662,10 +722,17 @@ __device__ __forceinline__ void process_chunk(const agnes_tally_args& a, const W
         if (valid[s]) a.codes[c + 64u * s + lane] = (uint8_t)code[s];
 }
 
+/* set constants cached in LDS (block-shared) when the table is small */
+constexpr uint32_t SET_CACHE_MAX = 1024u;
+__host__ __device__ inline uint32_t set_cache_bytes(uint32_t n_sets) {
+    return n_sets <= SET_CACHE_MAX ? (uint32_t)align16(20ull * n_sets) : 0u;
+}
+
 /* Per wave: a contiguous range of instances (or, LIST, the deferred instances
- * grid-strided), one instance at a time, 256-vote chunks, the next chunk's loads
- * in flight while this one computes.  FAST kernels defer instances whose sums
- * could reach 2^31 (or whose set is not fast) to the WIDE LIST kernel. */
+ * grid-strided), one instance at a time, 256-vote chunks; the next chunk's votes
+ * and the next instance's header and State are in flight while one computes.
+ * FAST kernels defer instances whose sums could reach 2^31 (or whose set is not
+ * fast) to the WIDE LIST kernel. */
 template <bool WIDE, uint32_t MODE, bool SKIP, bool SM, bool LIST>
 __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t lds_per_wave) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -678,6 +745,25 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
     const uint64_t NV = vb.n_votes;
     const uint32_t Wn = gridDim.x * AGNES_WAVES_PER_BLOCK;
     const uint32_t gw = blockIdx.x * AGNES_WAVES_PER_BLOCK + wave;
+
+    /* block-shared set cache: q2[ns] q1[ns] mp[ns] (maxpow | fast<<31) tot[ns] (u64) */
+    const uint32_t ns = a.n_sets;
+    const uint32_t scb = set_cache_bytes(ns);
+    uint32_t* sc_q2 = reinterpret_cast<uint32_t*>(smem);
+    uint32_t* sc_q1 = sc_q2 + ns;
+    uint32_t* sc_mp = sc_q1 + ns;
+    uint32_t* sc_tot = sc_mp + ns; /* lo, hi pairs */
+    if (scb) {
+        for (uint32_t k = threadIdx.x; k < ns; k += blockDim.x) {
+            const agnes_set_info si = a.sets[k];
+            sc_q2[k] = si.q2;
+            sc_q1[k] = si.q1;
+            sc_mp[k] = si.maxpow | (si.fast ? 0x80000000u : 0u);
+            sc_tot[2 * k] = (uint32_t)si.total;
+            sc_tot[2 * k + 1] = (uint32_t)((uint64_t)si.total >> 32);
+        }
+        __syncthreads();
+    }
 
     uint32_t q0, qend, qstep;
     if (LIST) {
@@ -693,7 +779,7 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
 
     uint64_t o_fv, o_fs, o_tot;
     lds_layout(MODE, SKIP ? AGNES_FLAG_ROUND_SKIP : 0u, R, nv, &o_fv, &o_fs, &o_tot);
-    unsigned char* base = smem + (uint64_t)wave * lds_per_wave;
+    unsigned char* base = smem + scb + (uint64_t)wave * lds_per_wave;
     WaveLds L;
     L.vw = reinterpret_cast<uint64_t*>(base);
     L.vn = L.vw + 2u * R;
@@ -708,48 +794,71 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
     const uint32_t emax = lb >= 31u ? 1u : ((1u << (32u - lb)) - 1u); /* epochs per table fill      */
     uint32_t ep = 0;
 
-    auto off_at = [&](uint32_t k) -> uint64_t {
-        const uint64_t o = vb.offsets[k];
-        return o < NV ? o : NV;
-    };
-    /* contiguous mode: the wave's votes end at vend; the next chunk is prefetched */
-    const uint64_t vend = LIST ? NV : rfl64(off_at(qend));
+    /* the wave's votes end at vend (contiguous mode): the next chunk is prefetched */
+    const uint64_t vend = LIST ? NV : (vb.offsets[qend] < NV ? rfl64(vb.offsets[qend]) : NV);
     uint64_t pf_at = ~0ull;
     Raw pf;
     uint32_t bad_lane = 0;
 
+    /* header of instance k, spread over lanes: 0,1 = offsets[k]; 2,3 = offsets[k+1];
+     * 4 = its set; 16..29 = its State (dwords 0..13) */
+    auto load_hdr = [&](uint32_t k) -> uint32_t {
+        uint32_t h = 0;
+        if (lane < 4u) h = reinterpret_cast<const uint32_t*>(vb.offsets + k)[lane];
+        else if (lane == 4u) h = vb.instance_set ? vb.instance_set[k] : (ns ? k % ns : 0u);
+        else if (SM && lane >= 16u && lane < 30u) h = reinterpret_cast<const uint32_t*>(&a.states[k])[lane - 16u];
+        return h;
+    };
+    uint32_t qi = LIST ? rfl(a.list[q0]) : q0;
+    uint32_t hdr = load_hdr(qi);
+
     for (uint32_t q = q0; q < qend; q += qstep) {
         Inst I;
-        I.i = LIST ? rfl(a.list[q]) : q;
-        I.beg = rfl64(off_at(I.i));
-        uint64_t e = rfl64(off_at(I.i + 1u));
-        I.end = e > I.beg ? e : I.beg;
-        uint32_t set = vb.instance_set ? vb.instance_set[I.i] : (a.n_sets ? I.i % a.n_sets : 0u);
-        set = rfl(set);
-        I.set_ok = set < a.n_sets;
-        agnes_set_info si;
-        if (I.set_ok) {
-            si = a.sets[set];
+        I.i = qi;
+        const uint32_t h = hdr;
+        /* next instance's header in flight while this one is tallied */
+        if (q + qstep < qend) {
+            qi = LIST ? rfl(a.list[q + qstep]) : q + qstep;
+            hdr = load_hdr(qi);
+        }
+        uint64_t b = ((uint64_t)rdl(h, 1u) << 32) | rdl(h, 0u);
+        uint64_t e = ((uint64_t)rdl(h, 3u) << 32) | rdl(h, 2u);
+        b = b < NV ? b : NV;
+        e = e < NV ? e : NV;
+        I.beg = b;
+        I.end = e > b ? e : b;
+        const uint32_t set = rdl(h, 4u);
+        I.set_ok = set < ns;
+        uint32_t mp = 0;
+        if (!I.set_ok) {
+            I.q2 = I.q1 = 0;
+            I.total = 0;
+        } else if (scb) {
+            I.q2 = sc_q2[set];
+            I.q1 = sc_q1[set];
+            mp = sc_mp[set];
+            I.total = (int64_t)(((uint64_t)sc_tot[2 * set + 1] << 32) | sc_tot[2 * set]);
         } else {
-            si.total = 0;
-            si.q2 = si.q1 = si.maxpow = si.fast = 0;
+            const agnes_set_info si = a.sets[set];
+            I.q2 = si.q2;
+            I.q1 = si.q1;
+            mp = si.maxpow | (si.fast ? 0x80000000u : 0u);
+            I.total = si.total;
         }
         I.pbase = set * nv;
-        I.q2 = si.q2;
-        I.q1 = si.q1;
-        I.total = si.total;
+        const uint64_t len = I.end - I.beg;
         if (!WIDE) { /* sums provably < 2^31: u32 arithmetic; otherwise defer to WIDE */
-            const uint64_t len = I.end - I.beg;
-            const bool fast = !I.set_ok || (si.fast && len < (1ull << 32) &&
-                                            len * (uint64_t)si.maxpow < (1ull << 31));
+            const bool fast = !I.set_ok || ((mp >> 31) && len < (1ull << 32) &&
+                                            len * (uint64_t)(mp & 0x7FFFFFFFu) < (1ull << 31));
             if (!fast) {
                 if (lane == 0) a.list[atomicAdd(a.list_count, 1u)] = I.i;
                 continue;
             }
         }
-        if (I.beg == I.end) continue; /* no votes: executors and State untouched */
+        if (len == 0) continue; /* no votes: executors and State untouched */
 
-        /* RoundVotes::new for every round (round_votes.rs:83-90) */
+        /* RoundVotes::new for every round (round_votes.rs:83-90): zero carries are
+         * implicit in an instance's first chunk; LDS holds them only across chunks */
         if (tables) {
             if (++ep > emax) { /* epoch space used up: recycle the tables */
                 if (MODE == AGNES_MODE_DEDUP) fill_u32(L.first_v, 2ull * R * nv, 0u, lane);
@@ -758,21 +867,38 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
             }
         }
         I.ep = ep;
-        for (uint32_t k = lane; k < 2u * R; k += 64) {
-            if (a.carry) {
-                const agnes_carry_rec cr = a.carry[(uint64_t)I.i * 2u * R + k];
-                L.vw[k] = (uint64_t)cr.value_w;
-                L.vn[k] = (uint64_t)cr.nil_w;
-                L.lv[k] = cr.value;
-            } else {
-                L.vw[k] = 0;
-                L.vn[k] = 0;
-                L.lv[k] = 0;
+        const bool multi = len > CHUNK || a.carry != nullptr;
+        if (multi) {
+            for (uint32_t k = lane; k < 2u * R; k += 64) {
+                if (a.carry) {
+                    const agnes_carry_rec cr = a.carry[(uint64_t)I.i * 2u * R + k];
+                    L.vw[k] = (uint64_t)cr.value_w;
+                    L.vn[k] = (uint64_t)cr.nil_w;
+                    L.lv[k] = cr.value;
+                } else {
+                    L.vw[k] = 0;
+                    L.vn[k] = 0;
+                    L.lv[k] = 0;
+                }
             }
+            for (uint32_t k = lane; k < R; k += 64) L.skw[k] = 0;
         }
-        for (uint32_t k = lane; k < R; k += 64) L.skw[k] = 0;
         Sm st;
-        if (SM) st = sm_load(&a.states[I.i]);
+        if (SM) { /* State from the header lanes 16..29 */
+            st.height = (int64_t)(((uint64_t)rdl(h, 17u) << 32) | rdl(h, 16u));
+            st.round = (int64_t)(((uint64_t)rdl(h, 19u) << 32) | rdl(h, 18u));
+            st.locked_round = (int64_t)(((uint64_t)rdl(h, 21u) << 32) | rdl(h, 20u));
+            st.valid_round = (int64_t)(((uint64_t)rdl(h, 23u) << 32) | rdl(h, 22u));
+            st.decision_round = (int64_t)(((uint64_t)rdl(h, 25u) << 32) | rdl(h, 24u));
+            st.locked_value = rdl(h, 26u);
+            st.valid_value = rdl(h, 27u);
+            st.decision_value = rdl(h, 28u);
+            const uint32_t f = rdl(h, 29u);
+            st.step = f & 0xFFu;
+            st.locked = (f >> 8) & 0xFFu;
+            st.valid = (f >> 16) & 0xFFu;
+            st.decided = f >> 24;
+        }
         __builtin_amdgcn_wave_barrier();
 
         for (uint64_t c = I.beg; c < I.end; c += CHUNK) {
@@ -787,10 +913,34 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
                 load_raw(vb, cl, vend, pf);
                 pf_at = cl;
             }
-            process_chunk<WIDE, MODE, SKIP, SM>(a, L, I, c, cl, x, st, lb, bad_lane);
+            process_chunk<WIDE, MODE, SKIP, SM>(a, L, I, c, cl, x, st, lb, bad_lane,
+                                                /*ld_carry=*/c != I.beg || a.carry != nullptr,
+                                                /*st_carry=*/cl != I.end || a.carry != nullptr);
             __builtin_amdgcn_wave_barrier();
         }
-        if (SM && lane == 0) sm_store(&a.states[I.i], st);
+        if (SM) { /* State back: one dword per lane, lanes 0..13 */
+            const uint32_t f = (st.step & 0xFFu) | ((st.locked & 0xFFu) << 8) |
+                               ((st.valid & 0xFFu) << 16) | (st.decided << 24);
+            uint32_t d = 0;
+            switch (lane) {
+            case 0: d = (uint32_t)st.height; break;
+            case 1: d = (uint32_t)((uint64_t)st.height >> 32); break;
+            case 2: d = (uint32_t)st.round; break;
+            case 3: d = (uint32_t)((uint64_t)st.round >> 32); break;
+            case 4: d = (uint32_t)st.locked_round; break;
+            case 5: d = (uint32_t)((uint64_t)st.locked_round >> 32); break;
+            case 6: d = (uint32_t)st.valid_round; break;
+            case 7: d = (uint32_t)((uint64_t)st.valid_round >> 32); break;
+            case 8: d = (uint32_t)st.decision_round; break;
+            case 9: d = (uint32_t)((uint64_t)st.decision_round >> 32); break;
+            case 10: d = st.locked_value; break;
+            case 11: d = st.valid_value; break;
+            case 12: d = st.decision_value; break;
+            case 13: d = f; break;
+            default: break;
+            }
+            if (lane < 14u) reinterpret_cast<uint32_t*>(&a.states[I.i])[lane] = d;
+        }
         if (a.carry) { /* persist the executors */
             for (uint32_t k = lane; k < 2u * R; k += 64) {
                 agnes_carry_rec cr;
@@ -875,7 +1025,7 @@ template <bool WIDE, uint32_t MODE, bool SKIP, bool SM, bool LIST>
 static hipError_t launch_k(const agnes_tally_args* a, uint32_t lpw, int num_cus, hipStream_t st) {
     const uint32_t n = a->vb.n_instances;
     if (n == 0) return hipSuccess;
-    const uint64_t lds = (uint64_t)lpw * AGNES_WAVES_PER_BLOCK;
+    const uint64_t lds = (uint64_t)lpw * AGNES_WAVES_PER_BLOCK + agnes::set_cache_bytes(a->n_sets);
     const void* fn = reinterpret_cast<const void*>(&agnes::tally_kernel<WIDE, MODE, SKIP, SM, LIST>);
     if (lds > 48u * 1024u) {
         hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

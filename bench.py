@@ -27,6 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from agnes_amd import abi  # noqa: E402
+from agnes_amd import dist as adist  # noqa: E402
 from agnes_amd.engine import Engine, states_to_device  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
@@ -56,27 +57,9 @@ WORKLOADS = {
 }
 
 
-def dist_env():
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    return rank, world, local
-
-
 def start_states(n: int) -> np.ndarray:
     """Every instance past NewRoundProposer + Proposal of round 0 (Prevote step)."""
     return abi.new_states(n, height=1, step=abi.STEP_PREVOTE, round_=0)
-
-
-def make_shard(w: dict, rank: int, world: int):
-    g = dict(w["gen"])
-    if w["scaling"] == "strong":
-        n = g["n_instances"]
-        lo, hi = n * rank // world, n * (rank + 1) // world
-        g["n_instances"], base = hi - lo, lo
-    else:
-        base = rank * g["n_instances"]
-    return abi.gen_params(seed=0xA6E5, instance_base=base, **g), base
 
 
 def cpu_baseline(eng, cfg, batch, power, states0, set_of_instance):
@@ -114,7 +97,7 @@ def main():
     ap.add_argument("--check", action="store_true", help="compare the CPU sample with the GPU codes")
     args = ap.parse_args()
 
-    rank, world, local = dist_env()
+    rank, world, local = adist.env()
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
     torch.cuda.set_device(local)
@@ -124,14 +107,14 @@ def main():
 
     w = WORKLOADS[args.config]
     eng = Engine(local)
-    p, base = make_shard(w, rank, world)
+    shard = adist.make_shard(w["gen"], rank, world, strong=w["scaling"] == "strong")
+    p = shard.params
     kind, lo, hi, n_sets = w["power"]
     power = eng.gen_power(0xA6E5, n_sets, p.n_vals, kind, lo, hi)
     eng.upload_power(power)
     stream = torch.cuda.current_stream()
     batch = eng.gen_batch(p)
-    # global instance -> power set (instance mod n_sets, with the shard's global ids)
-    set_of = ((np.arange(p.n_instances, dtype=np.int64) + base) % n_sets).astype(np.uint32)
+    set_of = adist.set_of_instances(shard, n_sets)   # global instance id mod n_sets
     batch.instance_set = torch.from_numpy(set_of.view(np.int32)).to(eng.device)
     cfg = abi.config(w["mode"], w["flags"], w["max_rounds"])
     st0_host = start_states(p.n_instances)
@@ -164,16 +147,10 @@ def main():
         step(pairs[k])
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    elapsed = adist.max_over_ranks(elapsed)
+    total_votes_step = adist.sum_over_ranks(batch.n_votes)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=eng.device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        nv = torch.tensor([batch.n_votes], dtype=torch.int64, device=eng.device)
-        dist.all_reduce(nv)
-        total_votes_step = int(nv.item())
         dist.barrier()
-    else:
-        total_votes_step = batch.n_votes
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in pairs]))
 
     if rank == 0:

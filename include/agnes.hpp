@@ -263,8 +263,8 @@ struct Message {
         case AGNES_MSG_NEW_ROUND: return new_round(r.round);
         case AGNES_MSG_PROPOSAL: return proposal_(r.round, agnes::Value{r.value}, r.pol_round);
         case AGNES_MSG_VOTE:
-            return r.vote_type == AGNES_PREVOTE ? prevote(r.round, from_raw(r.value))
-                                                : precommit(r.round, from_raw(r.value));
+            return r.vote_type == AGNES_PREVOTE ? prevote(r.round, agnes::from_raw(r.value))
+                                                : precommit(r.round, agnes::from_raw(r.value));
         case AGNES_MSG_TIMEOUT: return timeout_(r.round, (TimeoutStep)r.timeout_step);
         default: return decision_(r.round, agnes::Value{r.value});
         }
