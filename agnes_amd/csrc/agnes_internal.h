@@ -48,6 +48,8 @@ typedef struct agnes_tally_args {
     uint32_t* list_count;
     uint32_t epoch_shift; /* bits of a vote's index inside its instance (DEDUP/SKIP tables) */
     uint32_t dbg;         /* development knob (AGNES_DEBUG_SKIP): phases to skip; 0 in production */
+    uint32_t set_cache;   /* bytes of block LDS caching the set constants (0: read them from HBM);
+                             set by the launcher only when it costs no occupancy */
 } agnes_tally_args;
 
 /* bytes of dynamic LDS one wave uses */

@@ -748,7 +748,7 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
 
     /* block-shared set cache: q2[ns] q1[ns] mp[ns] (maxpow | fast<<31) tot[ns] (u64) */
     const uint32_t ns = a.n_sets;
-    const uint32_t scb = set_cache_bytes(ns);
+    const uint32_t scb = a.set_cache;
     uint32_t* sc_q2 = reinterpret_cast<uint32_t*>(smem);
     uint32_t* sc_q1 = sc_q2 + ns;
     uint32_t* sc_mp = sc_q1 + ns;
@@ -1025,30 +1025,53 @@ template <bool WIDE, uint32_t MODE, bool SKIP, bool SM, bool LIST>
 static hipError_t launch_k(const agnes_tally_args* a, uint32_t lpw, int num_cus, hipStream_t st) {
     const uint32_t n = a->vb.n_instances;
     if (n == 0) return hipSuccess;
-    const uint64_t lds = (uint64_t)lpw * AGNES_WAVES_PER_BLOCK + agnes::set_cache_bytes(a->n_sets);
     const void* fn = reinterpret_cast<const void*>(&agnes::tally_kernel<WIDE, MODE, SKIP, SM, LIST>);
+    const uint64_t wave_lds = (uint64_t)lpw * AGNES_WAVES_PER_BLOCK;
+    const uint32_t scb = agnes::set_cache_bytes(a->n_sets);
+    /* every wave owns an equal slice of the instances: launch the resident grid
+     * (blocks per CU from the occupancy query).  The set cache is used only when
+     * it does not lower the blocks per CU.  Cached per (kernel, LDS shape). */
+    struct Occ { const void* fn; uint64_t wave_lds; uint32_t scb; int per_cu; uint32_t use; };
+    static thread_local Occ occ[8];
+    static thread_local unsigned occ_next = 0;
+    Occ* o = nullptr;
+    for (auto& c : occ)
+        if (c.fn == fn && c.wave_lds == wave_lds && c.scb == scb) o = &c;
+    if (!o) {
+        auto blocks_per_cu = [&](uint64_t lds) -> int {
+            if (lds > 48u * 1024u &&
+                hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+                return 0;
+            int per_cu = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, (size_t)lds) != hipSuccess)
+                per_cu = 0;
+            return per_cu;
+        };
+        const int without = blocks_per_cu(wave_lds);
+        const int with = scb ? blocks_per_cu(wave_lds + scb) : 0;
+        o = &occ[occ_next++ % 8];
+        *o = Occ{fn, wave_lds, scb, 0, 0};
+        if (scb && with >= without && with > 0) {
+            o->per_cu = with;
+            o->use = scb;
+        } else {
+            o->per_cu = without > 0 ? without : 1;
+        }
+    }
+    agnes_tally_args b = *a;
+    b.set_cache = o->use;
+    const uint64_t lds = wave_lds + o->use;
     if (lds > 48u * 1024u) {
         hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    /* every wave owns an equal slice of the instances: launch the resident grid
-     * (blocks per CU from the occupancy query, cached per LDS size) */
-    static thread_local uint64_t cached_lds = ~0ull;
-    static thread_local int cached_per_cu = 0;
-    if (cached_lds != lds) {
-        int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, (size_t)lds) != hipSuccess ||
-            per_cu < 1)
-            per_cu = 1;
-        cached_lds = lds;
-        cached_per_cu = per_cu;
-    }
-    const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256) * (uint64_t)cached_per_cu;
+    const uint64_t ncu = (uint64_t)(num_cus > 0 ? num_cus : 256);
+    const uint64_t cap = ncu * (uint64_t)o->per_cu;
     uint64_t blocks = (n + AGNES_WAVES_PER_BLOCK - 1) / AGNES_WAVES_PER_BLOCK;
     if (blocks > cap) blocks = cap;
-    if (LIST && blocks > (uint64_t)(num_cus > 0 ? num_cus : 256)) blocks = (uint64_t)(num_cus > 0 ? num_cus : 256);
+    if (LIST && blocks > ncu) blocks = ncu;
     hipLaunchKernelGGL((agnes::tally_kernel<WIDE, MODE, SKIP, SM, LIST>), dim3((uint32_t)blocks), dim3(256),
-                       (size_t)lds, st, *a, lpw);
+                       (size_t)lds, st, b, lpw);
     return hipGetLastError();
 }
 
