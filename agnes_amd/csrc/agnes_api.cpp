@@ -198,8 +198,11 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
                        !b->validator))
         return AGNES_E_INVALID;
     if ((cfg->flags & AGNES_FLAG_STATE_MACHINE) && !states) return AGNES_E_INVALID;
-    /* u32 columns naturally aligned */
-    if (((uintptr_t)b->instance | (uintptr_t)b->value | (uintptr_t)b->validator) & 3u) return AGNES_E_INVALID;
+    /* the kernel reads 4 consecutive votes per lane: u32 columns 16-B aligned,
+     * u8 columns and the codes 4-B aligned, weights naturally aligned */
+    if (((uintptr_t)b->instance | (uintptr_t)b->value | (uintptr_t)b->validator) & 15u) return AGNES_E_INVALID;
+    if (((uintptr_t)b->round | (uintptr_t)b->type | (uintptr_t)codes) & 3u) return AGNES_E_INVALID;
+    if ((uintptr_t)b->weight & 7u) return AGNES_E_INVALID;
     const int64_t lpw = agnes_lds_bytes_per_wave(cfg, c->n_vals);
     if (lpw < 0) return (int)lpw;
     AGNES_TRY(hipSetDevice(c->device));

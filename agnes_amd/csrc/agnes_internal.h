@@ -50,6 +50,7 @@ typedef struct agnes_tally_args {
     uint32_t dbg;         /* development knob (AGNES_DEBUG_SKIP): phases to skip; 0 in production */
     uint32_t set_cache;   /* bytes of block LDS caching the set constants (0: read them from HBM);
                              set by the launcher only when it costs no occupancy */
+    uint32_t power_cache; /* bytes of block LDS holding the u32 power table (0: gather from HBM) */
 } agnes_tally_args;
 
 /* bytes of dynamic LDS one wave uses */

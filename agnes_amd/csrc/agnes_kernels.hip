@@ -327,7 +327,7 @@ __device__ __forceinline__ uint32_t vmsg_of(bool h1, bool h2, const MsgOut& m2) 
 }
 
 template <typename T>
-__device__ __forceinline__ T pick4(const T (&x)[4], uint32_t e) { /* e wave-uniform */
+__device__ __forceinline__ T pick4(const T (&x)[4], uint32_t e) {
     return e == 0 ? x[0] : (e == 1 ? x[1] : (e == 2 ? x[2] : x[3]));
 }
 
@@ -428,41 +428,58 @@ __device__ inline void fill_u32(uint32_t* p, uint64_t n, uint32_t v, uint32_t la
 /* ------------------------------------------------------------------ */
 /* fused tally kernel                                                  */
 
-constexpr uint32_t SUBS = 4;             /* 64-vote rows per chunk         */
-constexpr uint32_t CHUNK = 64u * SUBS;   /* votes per chunk (one instance) */
+constexpr uint32_t VPL = 4;             /* consecutive votes per lane          */
+constexpr uint32_t CHUNK = 64u * VPL;   /* votes per chunk (one instance pass) */
 
-/* one chunk of the canonical SoA: row s, lane l = vote c + 64 s + l (every
- * load a fully coalesced 64-lane row) */
+/* One chunk of the canonical SoA, lane-major: lane l holds votes c + 4l .. c + 4l + 3
+ * (c 4-aligned), so the u32 columns arrive as one 16-B load per lane and the u8
+ * columns as one 4-B load per lane (vote s in byte s). */
 struct Raw {
-    uint32_t inst[SUBS], value[SUBS], val[SUBS], r[SUBS], t[SUBS];
+    uint32_t inst[VPL], value[VPL], val[VPL];
+    uint32_t r4, t4;
 };
 
 __device__ __forceinline__ void load_raw(const agnes_vote_batch& vb, uint64_t c, uint64_t lim,
                                          Raw& x) {
-    const uint32_t lane = lane_id();
-    if (c + CHUNK <= lim) { /* wave-uniform: whole chunk readable */
-#pragma unroll
-        for (uint32_t s = 0; s < SUBS; ++s) {
-            const uint64_t j = c + 64u * s + lane;
-            x.inst[s] = vb.instance[j];
-            x.value[s] = vb.value[j];
-            x.val[s] = vb.validator[j];
-            x.r[s] = vb.round[j];
-            x.t[s] = vb.type[j];
-        }
+    const uint64_t j = c + 4u * lane_id();
+    if (j + VPL <= lim) {
+        const uint4 a = *reinterpret_cast<const uint4*>(vb.instance + j);
+        const uint4 v = *reinterpret_cast<const uint4*>(vb.value + j);
+        const uint4 d = *reinterpret_cast<const uint4*>(vb.validator + j);
+        x.inst[0] = a.x; x.inst[1] = a.y; x.inst[2] = a.z; x.inst[3] = a.w;
+        x.value[0] = v.x; x.value[1] = v.y; x.value[2] = v.z; x.value[3] = v.w;
+        x.val[0] = d.x; x.val[1] = d.y; x.val[2] = d.z; x.val[3] = d.w;
+        x.r4 = *reinterpret_cast<const uint32_t*>(vb.round + j);
+        x.t4 = *reinterpret_cast<const uint32_t*>(vb.type + j);
     } else {
+        x.r4 = x.t4 = 0;
 #pragma unroll
-        for (uint32_t s = 0; s < SUBS; ++s) {
-            const uint64_t j = c + 64u * s + lane;
-            const bool in = j < lim;
-            x.inst[s] = in ? vb.instance[j] : 0u;
-            x.value[s] = in ? vb.value[j] : 0u;
-            x.val[s] = in ? vb.validator[j] : 0u;
-            x.r[s] = in ? (uint32_t)vb.round[j] : 0u;
-            x.t[s] = in ? (uint32_t)vb.type[j] : 0u;
+        for (uint32_t s = 0; s < VPL; ++s) {
+            const bool in = j + s < lim;
+            x.inst[s] = in ? vb.instance[j + s] : 0u;
+            x.value[s] = in ? vb.value[j + s] : 0u;
+            x.val[s] = in ? vb.validator[j + s] : 0u;
+            x.r4 |= (in ? (uint32_t)vb.round[j + s] : 0u) << (8u * s);
+            x.t4 |= (in ? (uint32_t)vb.type[j + s] : 0u) << (8u * s);
         }
     }
 }
+
+/* inclusive stream-order prefix of a[0..3] over the wave (vote 4l+s); returns the
+ * chunk total.  Lane-local serial sums + one wave scan of the lane totals. */
+template <typename W>
+__device__ __forceinline__ W scan4(const W (&a)[VPL], W (&o)[VPL]) {
+    const W l0 = a[0], l1 = l0 + a[1], l2 = l1 + a[2], l3 = l2 + a[3];
+    const W inc = scan(l3);
+    const W ex = inc - l3;
+    o[0] = ex + l0;
+    o[1] = ex + l1;
+    o[2] = ex + l2;
+    o[3] = ex + l3;
+    return rdl(inc, 63u);
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt(uint32_t l) { return (1ull << l) - 1ull; }
 
 /* uniform facts of the instance being tallied */
 struct Inst {
@@ -475,96 +492,133 @@ struct Inst {
     bool set_ok;
 };
 
-template <bool WIDE, uint32_t MODE, bool SKIP, bool SM>
-__device__ __forceinline__ void process_chunk(const agnes_tally_args& a, const WaveLds& L,
-                                              const Inst& in_, uint64_t c, uint64_t cl,
-                                              const Raw& x, Sm& st, uint32_t lb,
-                                              uint32_t& bad_lane, bool ld_carry, bool st_carry) {
+/* per-vote facts of one chunk pass, computed before anything else so that the
+ * weight gather is the first memory operation issued for the chunk */
+template <typename W>
+struct Pre {
+    uint32_t rr[VPL], tt[VPL];
+    uint32_t f_valid, f_ok, f_nil; /* bit s = vote s of the lane */
+    W w[VPL];
+};
+
+/* validation (the vote belongs to the instance, round < max_rounds, type in
+ * {0,1}, validator in the set) and the K1 weight gather
+ * (consensus_executor.rs:62-63 -> validators.rs:7), branch-free; the gather reads
+ * the block's LDS copy of the power table when the launcher staged one */
+template <bool WIDE, uint32_t MODE, bool SKIP>
+__device__ __forceinline__ void prep_chunk(const agnes_tally_args& a, const Inst& in_, uint64_t c,
+                                           const Raw& x, const uint32_t* pcache, Pre<
+                                           typename std::conditional<WIDE, uint64_t, uint32_t>::type>& P,
+                                           uint32_t& bad_lane) {
     using W = typename std::conditional<WIDE, uint64_t, uint32_t>::type;
-    const uint32_t lane = lane_id();
     const uint32_t R = a.max_rounds;
     const uint32_t nv = a.n_vals;
     const agnes_vote_batch& vb = a.vb;
     const bool has_w = vb.weight != nullptr;
     const bool need_val = !has_w || MODE == AGNES_MODE_DEDUP || SKIP;
-    const bool track = SM || a.carry != nullptr; /* labels: state machine / carried executors */
-    const uint32_t nvalid = (uint32_t)(cl - c);
-
-    bool valid[SUBS], ok[SUBS], acc[SUBS], isnil[SUBS];
-    W w[SUBS];
+    /* the instance's votes in this chunk: positions [lo, hi) */
+    const uint32_t lo = c < in_.beg ? (uint32_t)(in_.beg - c) : 0u;
+    const uint32_t hi = in_.end - c < CHUNK ? (uint32_t)(in_.end - c) : CHUNK;
+    const uint32_t p0 = 4u * lane_id();
+    P.f_valid = P.f_ok = P.f_nil = 0;
 #pragma unroll
-    for (uint32_t s = 0; s < SUBS; ++s) {
-        valid[s] = 64u * s + lane < nvalid;
-        ok[s] = valid[s] && x.inst[s] == in_.i && x.r[s] < R && x.t[s] <= 1u &&
-                (!need_val || (in_.set_ok && x.val[s] < nv)) && (has_w || in_.set_ok);
-        bad_lane += (valid[s] && !ok[s]) ? 1u : 0u;
-        isnil[s] = x.value[s] == AGNES_NIL;
-        acc[s] = ok[s];
-        /* K1 weight gather (consensus_executor.rs:62-63 -> validators.rs:7), branch-free */
+    for (uint32_t s = 0; s < VPL; ++s) {
+        P.rr[s] = (x.r4 >> (8u * s)) & 0xFFu;
+        P.tt[s] = (x.t4 >> (8u * s)) & 0xFFu;
+        const bool valid = p0 + s >= lo && p0 + s < hi;
+        const bool ok = valid && x.inst[s] == in_.i && P.rr[s] < R && P.tt[s] <= 1u &&
+                        (!need_val || (in_.set_ok && x.val[s] < nv)) && (has_w || in_.set_ok);
+        bad_lane += (valid && !ok) ? 1u : 0u;
+        P.f_valid |= (valid ? 1u : 0u) << s;
+        P.f_ok |= (ok ? 1u : 0u) << s;
+        P.f_nil |= (x.value[s] == AGNES_NIL ? 1u : 0u) << s;
         if (has_w) {
-            w[s] = ok[s] ? (W)vb.weight[c + 64u * s + lane] : (W)0;
+            P.w[s] = ok ? (W)vb.weight[c + p0 + s] : (W)0;
         } else {
-            const uint32_t idx = ok[s] ? in_.pbase + x.val[s] : 0u;
-            const W g = WIDE ? (W)a.power[idx] : (W)a.power32[idx];
-            w[s] = ok[s] ? g : (W)0;
+            const uint32_t idx = ok ? in_.pbase + x.val[s] : 0u;
+            W g;
+            if (WIDE) g = (W)a.power[idx];
+            else g = pcache ? (W)pcache[idx] : (W)a.power32[idx];
+            P.w[s] = ok ? g : (W)0;
         }
     }
+}
+
+/* One pass over chunk [c, c + CHUNK) for instance in_ (votes outside
+ * [in_.beg, in_.end) untouched); returns the lane's 4 code bytes, packed. */
+template <bool WIDE, uint32_t MODE, bool SKIP, bool SM>
+__device__ __forceinline__ uint32_t process_chunk(const agnes_tally_args& a, const WaveLds& L,
+                                                  const Inst& in_, uint64_t c, const Raw& x,
+                                                  const Pre<typename std::conditional<WIDE, uint64_t, uint32_t>::type>& P,
+                                                  Sm& st, uint32_t lb, bool ld_carry, bool st_carry) {
+    using W = typename std::conditional<WIDE, uint64_t, uint32_t>::type;
+    const uint32_t lane = lane_id();
+    const uint32_t nv = a.n_vals;
+    const bool track = SM || a.carry != nullptr; /* labels: state machine / carried executors */
+    const uint32_t p0 = 4u * lane;
+    const uint32_t(&rr)[VPL] = P.rr;
+    const uint32_t(&tt)[VPL] = P.tt;
+    const W(&w)[VPL] = P.w;
+    const uint32_t f_ok = P.f_ok, f_nil = P.f_nil;
+    uint32_t f_acc = f_ok;
 
     /* first-vote-wins (DEDUP) / distinct-validator (RoundSkip) tables: atomic max of
      * (epoch << lb | LMASK - local index): the earliest vote of the instance wins,
      * entries of earlier instances (smaller epochs) are simply overwritten */
-    bool sfirst[SUBS];
-#pragma unroll
-    for (uint32_t s = 0; s < SUBS; ++s) sfirst[s] = false;
+    uint32_t f_sfirst = 0;
     if (MODE == AGNES_MODE_DEDUP || SKIP) {
         const uint32_t lmask = (1u << lb) - 1u;
-        const uint32_t loc0 = (uint32_t)(c - in_.beg) + lane;
-        uint32_t enc[SUBS];
+        const uint32_t loc0 = (uint32_t)(c - in_.beg) + p0; /* wraps only for votes before beg */
+        uint32_t enc[VPL];
 #pragma unroll
-        for (uint32_t s = 0; s < SUBS; ++s) {
-            enc[s] = (in_.ep << lb) | (lmask - (loc0 + 64u * s));
-            if (ok[s]) {
+        for (uint32_t s = 0; s < VPL; ++s) {
+            enc[s] = (in_.ep << lb) | (lmask - (loc0 + s));
+            if ((f_ok >> s) & 1u) {
                 if (MODE == AGNES_MODE_DEDUP)
-                    atomicMax(&L.first_v[(x.r[s] * 2u + x.t[s]) * nv + x.val[s]], enc[s]);
-                if (SKIP) atomicMax(&L.first_s[x.r[s] * nv + x.val[s]], enc[s]);
+                    atomicMax(&L.first_v[(rr[s] * 2u + tt[s]) * nv + x.val[s]], enc[s]);
+                if (SKIP) atomicMax(&L.first_s[rr[s] * nv + x.val[s]], enc[s]);
             }
         }
         __builtin_amdgcn_wave_barrier();
+        if (MODE == AGNES_MODE_DEDUP) f_acc = 0;
 #pragma unroll
-        for (uint32_t s = 0; s < SUBS; ++s) {
-            if (ok[s]) {
+        for (uint32_t s = 0; s < VPL; ++s) {
+            if ((f_ok >> s) & 1u) {
                 if (MODE == AGNES_MODE_DEDUP)
-                    acc[s] = *(volatile uint32_t*)&L.first_v[(x.r[s] * 2u + x.t[s]) * nv + x.val[s]] == enc[s];
-                if (SKIP) sfirst[s] = *(volatile uint32_t*)&L.first_s[x.r[s] * nv + x.val[s]] == enc[s];
+                    f_acc |= (*(volatile uint32_t*)&L.first_v[(rr[s] * 2u + tt[s]) * nv + x.val[s]] == enc[s]
+                                  ? 1u : 0u) << s;
+                if (SKIP)
+                    f_sfirst |= (*(volatile uint32_t*)&L.first_s[rr[s] * nv + x.val[s]] == enc[s] ? 1u : 0u)
+                                << s;
             }
         }
         __builtin_amdgcn_wave_barrier();
     }
 
-    /* K2: per (round,type) slot present: row by row, a wave64 inclusive scan of the
-     * value and nil buckets plus the running executor — VoteCount::add_vote's sums in
-     * stream order (round_votes.rs:48-56) */
-    uint32_t slot[SUBS];
-    uint64_t rem[SUBS];
+    /* K2: per (round,type) slot present, one stream-order scan of the value and nil
+     * buckets over the chunk plus the running executor — VoteCount::add_vote's sums
+     * (round_votes.rs:48-56) */
+    uint32_t slot[VPL];
+    W pv[VPL], pn[VPL];
+    uint32_t lab[VPL];
 #pragma unroll
-    for (uint32_t s = 0; s < SUBS; ++s) {
-        slot[s] = x.r[s] * 2u + x.t[s];
-        rem[s] = ballot(acc[s]);
-    }
-    W pv[SUBS], pn[SUBS];
-    uint32_t lab[SUBS];
-#pragma unroll
-    for (uint32_t s = 0; s < SUBS; ++s) {
+    for (uint32_t s = 0; s < VPL; ++s) {
+        slot[s] = rr[s] * 2u + tt[s];
         pv[s] = 0;
         pn[s] = 0;
         lab[s] = 0;
     }
+    uint32_t rem = f_acc;
     for (;;) {
-        uint32_t key = 0xFFFFFFFFu;
+        const uint64_t lm = ballot(rem != 0u);
+        if (!lm) break;
+        const uint32_t kl = (uint32_t)__builtin_ctzll(lm);
+        const uint32_t ks = (uint32_t)__builtin_ctz(rdl(rem, kl));
+        const uint32_t key = rdl(pick4(slot, ks), kl);
+        uint32_t inb = 0;
 #pragma unroll
-        for (uint32_t s = 0; s < SUBS; ++s)
-            if (key == 0xFFFFFFFFu && rem[s]) key = rdl(slot[s], (uint32_t)__builtin_ctzll(rem[s]));
-        if (key == 0xFFFFFFFFu) break;
+        for (uint32_t s = 0; s < VPL; ++s) inb |= (((rem >> s) & 1u) && slot[s] == key ? 1u : 0u) << s;
+        rem &= ~inb;
         W cv = 0, cn = 0;
         uint32_t lbl = 0;
         if (ld_carry) {
@@ -572,39 +626,54 @@ __device__ __forceinline__ void process_chunk(const agnes_tally_args& a, const W
             cn = (W)L.vn[key];
             if (track) lbl = L.lv[key];
         }
+        W av[VPL], an[VPL], ov[VPL], on[VPL];
 #pragma unroll
-        for (uint32_t s = 0; s < SUBS; ++s) {
-            const bool in = acc[s] && slot[s] == key;
-            const uint64_t min_ = ballot(in);
-            rem[s] &= ~min_;
-            if (!min_) continue; /* wave-uniform */
-            const W sv = scan((W)((in && !isnil[s]) ? w[s] : (W)0));
-            const W sn = scan((W)((in && isnil[s]) ? w[s] : (W)0));
-            if (in) {
-                pv[s] = cv + sv;
-                pn[s] = cn + sn;
+        for (uint32_t s = 0; s < VPL; ++s) {
+            const bool in = (inb >> s) & 1u, nil = (f_nil >> s) & 1u;
+            av[s] = (in && !nil) ? w[s] : (W)0;
+            an[s] = (in && nil) ? w[s] : (W)0;
+        }
+        const W tv = scan4(av, ov);
+        const W tn = scan4(an, on);
+#pragma unroll
+        for (uint32_t s = 0; s < VPL; ++s) {
+            if ((inb >> s) & 1u) {
+                pv[s] = cv + ov[s];
+                pn[s] = cn + on[s];
             }
-            cv += rdl(sv, 63u);
-            cn += rdl(sn, 63u);
-            if (track) { /* Thresh::Value payload: the last value written (round_votes.rs:53) */
-                const uint64_t mv = ballot(in && !isnil[s]);
+        }
+        if (track) { /* Thresh::Value payload: the last value written (round_votes.rs:53) */
+            const uint32_t nnb = inb & ~f_nil; /* this key's value votes in the lane */
+            const uint32_t lastv = nnb ? pick4(x.value, 31u - (uint32_t)__builtin_clz(nnb)) : 0u;
+            const uint64_t lanes_nn = ballot(nnb != 0u);
+            /* a nil vote needs a propagated label only when its value bucket is at quorum */
+            bool need = false;
+#pragma unroll
+            for (uint32_t s = 0; s < VPL; ++s) {
                 bool qv;
                 if (WIDE) qv = (int64_t)(3ull * (uint64_t)pv[s]) > (int64_t)(2ull * (uint64_t)in_.total);
                 else qv = (uint32_t)pv[s] > in_.q2;
-                /* a nil vote needs a propagated label only when its value bucket is at quorum */
-                if (ballot(in && isnil[s] && qv)) {
-                    const uint64_t le = mv & lanemask_le(lane);
-                    const uint32_t got = shfl(x.value[s], le ? 63u - (uint32_t)__builtin_clzll(le) : 0u);
-                    if (in) lab[s] = isnil[s] ? (le ? got : lbl) : x.value[s];
-                } else if (in && !isnil[s]) {
-                    lab[s] = x.value[s];
-                }
-                if (mv) lbl = rdl(x.value[s], 63u - (uint32_t)__builtin_clzll(mv));
+                need |= ((inb & f_nil) >> s) & 1u && qv;
             }
+            if (ballot(need)) {
+                const uint64_t le = lanes_nn & lanemask_lt(lane);
+                const uint32_t got = shfl(lastv, le ? 63u - (uint32_t)__builtin_clzll(le) : 0u);
+                uint32_t run = le ? got : lbl;
+#pragma unroll
+                for (uint32_t s = 0; s < VPL; ++s) {
+                    if ((nnb >> s) & 1u) run = x.value[s];
+                    if ((inb >> s) & 1u) lab[s] = run;
+                }
+            } else {
+#pragma unroll
+                for (uint32_t s = 0; s < VPL; ++s)
+                    if ((nnb >> s) & 1u) lab[s] = x.value[s];
+            }
+            if (lanes_nn) lbl = rdl(lastv, 63u - (uint32_t)__builtin_clzll(lanes_nn));
         }
         if (st_carry) {
-            L.vw[key] = (uint64_t)cv;
-            L.vn[key] = (uint64_t)cn;
+            L.vw[key] = (uint64_t)(cv + tv);
+            L.vn[key] = (uint64_t)(cn + tn);
             if (track) L.lv[key] = lbl;
         }
         __builtin_amdgcn_wave_barrier();
@@ -612,42 +681,42 @@ __device__ __forceinline__ void process_chunk(const agnes_tally_args& a, const W
 
     /* RoundSkip (+1/3 of distinct validators of the vote's round, extension):
      * the same scheme keyed by round over each validator's first vote */
-    W ps[SUBS];
+    W ps[VPL];
 #pragma unroll
-    for (uint32_t s = 0; s < SUBS; ++s) ps[s] = 0;
+    for (uint32_t s = 0; s < VPL; ++s) ps[s] = 0;
     if (SKIP) {
-#pragma unroll
-        for (uint32_t s = 0; s < SUBS; ++s) rem[s] = ballot(acc[s]);
+        uint32_t rs = f_acc;
         for (;;) {
-            uint32_t kr = 0xFFFFFFFFu;
+            const uint64_t lm = ballot(rs != 0u);
+            if (!lm) break;
+            const uint32_t kl = (uint32_t)__builtin_ctzll(lm);
+            const uint32_t ks = (uint32_t)__builtin_ctz(rdl(rs, kl));
+            const uint32_t kr = rdl(pick4(rr, ks), kl);
+            uint32_t inb = 0;
 #pragma unroll
-            for (uint32_t s = 0; s < SUBS; ++s)
-                if (kr == 0xFFFFFFFFu && rem[s]) kr = rdl(x.r[s], (uint32_t)__builtin_ctzll(rem[s]));
-            if (kr == 0xFFFFFFFFu) break;
-            W cs = ld_carry ? (W)L.skw[kr] : (W)0;
+            for (uint32_t s = 0; s < VPL; ++s) inb |= (((rs >> s) & 1u) && rr[s] == kr ? 1u : 0u) << s;
+            rs &= ~inb;
+            const W cs = ld_carry ? (W)L.skw[kr] : (W)0;
+            W as[VPL], os[VPL];
 #pragma unroll
-            for (uint32_t s = 0; s < SUBS; ++s) {
-                const bool in = acc[s] && x.r[s] == kr;
-                const uint64_t min_ = ballot(in);
-                rem[s] &= ~min_;
-                if (!min_) continue;
-                const W ss = scan((W)((in && sfirst[s]) ? w[s] : (W)0));
-                if (in) ps[s] = cs + ss;
-                cs += rdl(ss, 63u);
-            }
-            if (st_carry) L.skw[kr] = (uint64_t)cs;
+            for (uint32_t s = 0; s < VPL; ++s) as[s] = ((inb & f_sfirst) >> s) & 1u ? w[s] : (W)0;
+            const W ts = scan4(as, os);
+#pragma unroll
+            for (uint32_t s = 0; s < VPL; ++s)
+                if ((inb >> s) & 1u) ps[s] = cs + os[s];
+            if (st_carry) L.skw[kr] = (uint64_t)(cs + ts);
             __builtin_amdgcn_wave_barrier();
         }
     }
 
     /* K3: is_quorum precedence Value > Nil > Any > Init (round_votes.rs:58-66) and
      * to_event (vote_executor.rs:26-36) */
-    uint32_t code[SUBS];
+    uint32_t code[VPL];
 #pragma unroll
-    for (uint32_t s = 0; s < SUBS; ++s) {
-        if (!ok[s]) {
+    for (uint32_t s = 0; s < VPL; ++s) {
+        if (!((f_ok >> s) & 1u)) {
             code[s] = AGNES_CODE_INVALID;
-        } else if (!acc[s]) {
+        } else if (!((f_acc >> s) & 1u)) {
             code[s] = AGNES_CODE_REJECTED;
         } else {
             bool qv, qn, qa, q3;
@@ -663,7 +732,7 @@ __device__ __forceinline__ void process_chunk(const agnes_tally_args& a, const W
                 qa = (uint32_t)pv[s] + (uint32_t)pn[s] > in_.q2;
                 q3 = (uint32_t)ps[s] > in_.q1;
             }
-            const uint32_t t = x.t[s];
+            const uint32_t t = tt[s];
             const uint32_t ev = qv ? (t ? AGNES_CODE_PRECOMMIT_VALUE : AGNES_CODE_POLKA_VALUE)
                               : qn ? (t ? AGNES_CODE_NONE : AGNES_CODE_POLKA_NIL)
                               : qa ? (t ? AGNES_CODE_PRECOMMIT_ANY : AGNES_CODE_POLKA_ANY)
@@ -677,55 +746,75 @@ __device__ __forceinline__ void process_chunk(const agnes_tally_args& a, const W
      * (wave-uniform) state; votes before the first state change get their message,
      * the changing vote is applied on the scalar path, repeat */
     if (SM) {
-        uint32_t msg[SUBS];
-        uint64_t pend[SUBS];
+        uint32_t msg[VPL];
+        uint32_t pend = 0;
 #pragma unroll
-        for (uint32_t s = 0; s < SUBS; ++s) {
+        for (uint32_t s = 0; s < VPL; ++s) {
             msg[s] = 0;
-            pend[s] = ballot(acc[s] && (code[s] & 0x0Fu) != 0u);
+            pend |= (((f_acc >> s) & 1u) && (code[s] & 0x0Fu) != 0u ? 1u : 0u) << s;
         }
-        while (st.step != AGNES_STEP_COMMIT && (pend[0] | pend[1] | pend[2] | pend[3])) {
+        while (st.step != AGNES_STEP_COMMIT && ballot(pend != 0u)) {
             const SmTab tb = sm_tab(st);
-            uint32_t first = 0xFFFFFFFFu; /* chunk position s*64+lane of the first change */
-            uint32_t cm[SUBS];
+            uint32_t chb = 0, cm[VPL];
 #pragma unroll
-            for (uint32_t s = 0; s < SUBS; ++s) {
+            for (uint32_t s = 0; s < VPL; ++s) {
                 bool chg;
-                sm_classify(tb, x.r[s], code[s] & AGNES_CODE_EVENT_MASK, lab[s],
+                sm_classify(tb, rr[s], code[s] & AGNES_CODE_EVENT_MASK, lab[s],
                             (code[s] & AGNES_CODE_SKIP) != 0u, chg, cm[s]);
-                const uint64_t bk = ballot(chg && ((pend[s] >> lane) & 1ull));
-                if (first == 0xFFFFFFFFu && bk) first = 64u * s + (uint32_t)__builtin_ctzll(bk);
+                chb |= (chg ? 1u : 0u) << s;
+            }
+            chb &= pend;
+            const uint64_t bk = ballot(chb != 0u);
+            uint32_t first = 0xFFFFFFFFu; /* chunk position 4*lane+s of the first change */
+            uint32_t fl = 0, fs = 0;
+            if (bk) {
+                fl = (uint32_t)__builtin_ctzll(bk);
+                fs = (uint32_t)__builtin_ctz(rdl(chb, fl));
+                first = 4u * fl + fs;
             }
 #pragma unroll
-            for (uint32_t s = 0; s < SUBS; ++s)
-                if (((pend[s] >> lane) & 1ull) && 64u * s + lane < first) msg[s] = cm[s];
-            if (first == 0xFFFFFFFFu) break;
-            const uint32_t fs = first >> 6, fl = first & 63u;
-            const int64_t fr = (int64_t)rdl(pick4(x.r, fs), fl);
+            for (uint32_t s = 0; s < VPL; ++s)
+                if (((pend >> s) & 1u) && p0 + s < first) msg[s] = cm[s];
+            if (!bk) break;
+            const int64_t fr = (int64_t)rdl(pick4(rr, fs), fl);
             const uint32_t fcode = rdl(pick4(code, fs), fl);
             const uint32_t flab = rdl(pick4(lab, fs), fl);
             const uint32_t vm = sm_vote(st, fr, fcode, flab);
 #pragma unroll
-            for (uint32_t s = 0; s < SUBS; ++s) {
-                if (64u * s + lane == first) msg[s] = vm;
-                /* drop every vote up to and including the change */
-                if (64u * s + 63u <= first) pend[s] = 0;
-                else if (64u * s <= first) pend[s] &= ~0ull << (first - 64u * s + 1u);
+            for (uint32_t s = 0; s < VPL; ++s) {
+                if (p0 + s == first) msg[s] = vm;
+                if (p0 + s <= first) pend &= ~(1u << s); /* drop every vote up to the change */
             }
         }
 #pragma unroll
-        for (uint32_t s = 0; s < SUBS; ++s) code[s] |= msg[s] << AGNES_CODE_MSG_SHIFT;
+        for (uint32_t s = 0; s < VPL; ++s) code[s] |= msg[s] << AGNES_CODE_MSG_SHIFT;
     }
 
+    return code[0] | (code[1] << 8) | (code[2] << 16) | (code[3] << 24);
+}
+
+/* the lane's 4 code bytes of chunk c: one 4-B store when all 4 belong to the pass */
+__device__ __forceinline__ void store_codes(uint8_t* codes, uint64_t c, uint32_t packed, uint32_t f_valid) {
+    const uint64_t j = c + 4u * lane_id();
+    if (f_valid == 0xFu) {
+        *reinterpret_cast<uint32_t*>(codes + j) = packed;
+    } else {
 #pragma unroll
-    for (uint32_t s = 0; s < SUBS; ++s)
-        if (valid[s]) a.codes[c + 64u * s + lane] = (uint8_t)code[s];
+        for (uint32_t s = 0; s < VPL; ++s)
+            if ((f_valid >> s) & 1u) codes[j + s] = (uint8_t)(packed >> (8u * s));
+    }
 }
 
 /* set constants cached in LDS (block-shared) when the table is small */
 constexpr uint32_t SET_CACHE_MAX = 1024u;
 __host__ __device__ inline uint32_t set_cache_bytes(uint32_t n_sets) {
     return n_sets <= SET_CACHE_MAX ? (uint32_t)align16(20ull * n_sets) : 0u;
+}
+/* the u32 power table cached in LDS when it is at most 32 KB */
+constexpr uint64_t POWER_CACHE_MAX = 32u * 1024u;
+__host__ __device__ inline uint32_t power_cache_bytes(uint32_t n_sets, uint32_t n_vals) {
+    const uint64_t b = align16(4ull * n_sets * n_vals);
+    return b <= POWER_CACHE_MAX ? (uint32_t)b : 0u;
 }
 
 /* Per wave: a contiguous range of instances (or, LIST, the deferred instances
@@ -762,8 +851,18 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
             sc_tot[2 * k] = (uint32_t)si.total;
             sc_tot[2 * k + 1] = (uint32_t)((uint64_t)si.total >> 32);
         }
-        __syncthreads();
     }
+    /* block-shared power table (u32, fast kernels) when the launcher staged one: the
+     * gather is then an LDS read, waited on by lgkmcnt, not behind the vector
+     * memory queue of prefetches and stores */
+    const uint32_t* pcache = nullptr;
+    if (!WIDE && a.power_cache) {
+        uint32_t* pc = reinterpret_cast<uint32_t*>(smem + scb);
+        const uint32_t np = ns * nv;
+        for (uint32_t k = threadIdx.x; k < np; k += blockDim.x) pc[k] = a.power32[k];
+        pcache = pc;
+    }
+    if (scb || a.power_cache) __syncthreads();
 
     uint32_t q0, qend, qstep;
     if (LIST) {
@@ -779,7 +878,7 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
 
     uint64_t o_fv, o_fs, o_tot;
     lds_layout(MODE, SKIP ? AGNES_FLAG_ROUND_SKIP : 0u, R, nv, &o_fv, &o_fs, &o_tot);
-    unsigned char* base = smem + scb + (uint64_t)wave * lds_per_wave;
+    unsigned char* base = smem + scb + a.power_cache + (uint64_t)wave * lds_per_wave;
     WaveLds L;
     L.vw = reinterpret_cast<uint64_t*>(base);
     L.vn = L.vw + 2u * R;
@@ -799,6 +898,18 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
     uint64_t pf_at = ~0ull;
     Raw pf;
     uint32_t bad_lane = 0;
+    /* stores deferred until the next chunk's gather is issued (gfx9 vmcnt retires
+     * in issue order: a store ahead of a load delays every wait on that load) */
+    uint64_t dc_at = ~0ull;      /* chunk whose codes are pending                  */
+    uint32_t dc_code = 0, dc_valid = 0;
+    uint32_t ds_i = 0xFFFFFFFFu; /* instance whose State (lanes 0..13) is pending */
+    uint32_t ds_word = 0;
+    auto flush = [&]() {
+        if (dc_at != ~0ull) store_codes(a.codes, dc_at, dc_code, dc_valid);
+        dc_at = ~0ull;
+        if (SM && ds_i != 0xFFFFFFFFu && lane < 14u) reinterpret_cast<uint32_t*>(&a.states[ds_i])[lane] = ds_word;
+        ds_i = 0xFFFFFFFFu;
+    };
 
     /* header of instance k, spread over lanes: 0,1 = offsets[k]; 2,3 = offsets[k+1];
      * 4 = its set; 16..29 = its State (dwords 0..13) */
@@ -867,7 +978,8 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
             }
         }
         I.ep = ep;
-        const bool multi = len > CHUNK || a.carry != nullptr;
+        const uint64_t c0 = I.beg & ~3ull; /* chunks are 4-aligned in the stream */
+        const bool multi = I.end - c0 > CHUNK || a.carry != nullptr;
         if (multi) {
             for (uint32_t k = lane; k < 2u * R; k += 64) {
                 if (a.carry) {
@@ -901,24 +1013,31 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
         }
         __builtin_amdgcn_wave_barrier();
 
-        for (uint64_t c = I.beg; c < I.end; c += CHUNK) {
-            const uint64_t cl = c + CHUNK < I.end ? c + CHUNK : I.end;
+        for (uint64_t c = c0; c < I.end; c += CHUNK) {
             Raw x;
             if (pf_at == c) {
                 x = pf;
             } else {
-                load_raw(vb, c, cl, x);
+                load_raw(vb, c, LIST ? NV : vend, x);
             }
-            if (!LIST && cl < vend) { /* next chunk (this instance or the next one) */
-                load_raw(vb, cl, vend, pf);
-                pf_at = cl;
+            /* issue order: gather of this chunk, the previous chunk's stores, then the
+             * next chunk (this instance's, or the next instance's first) */
+            Pre<typename std::conditional<WIDE, uint64_t, uint32_t>::type> P;
+            prep_chunk<WIDE, MODE, SKIP>(a, I, c, x, pcache, P, bad_lane);
+            flush();
+            const uint64_t nc = c + CHUNK < I.end ? c + CHUNK : (I.end & ~3ull);
+            if (!LIST && nc < vend) {
+                load_raw(vb, nc, vend, pf);
+                pf_at = nc;
             }
-            process_chunk<WIDE, MODE, SKIP, SM>(a, L, I, c, cl, x, st, lb, bad_lane,
-                                                /*ld_carry=*/c != I.beg || a.carry != nullptr,
-                                                /*st_carry=*/cl != I.end || a.carry != nullptr);
+            dc_code = process_chunk<WIDE, MODE, SKIP, SM>(a, L, I, c, x, P, st, lb,
+                                                          /*ld_carry=*/c != c0 || a.carry != nullptr,
+                                                          /*st_carry=*/c + CHUNK < I.end || a.carry != nullptr);
+            dc_valid = P.f_valid;
+            dc_at = c;
             __builtin_amdgcn_wave_barrier();
         }
-        if (SM) { /* State back: one dword per lane, lanes 0..13 */
+        if (SM) { /* State back (deferred): one dword per lane, lanes 0..13 */
             const uint32_t f = (st.step & 0xFFu) | ((st.locked & 0xFFu) << 8) |
                                ((st.valid & 0xFFu) << 16) | (st.decided << 24);
             uint32_t d = 0;
@@ -939,7 +1058,8 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
             case 13: d = f; break;
             default: break;
             }
-            if (lane < 14u) reinterpret_cast<uint32_t*>(&a.states[I.i])[lane] = d;
+            ds_word = d;
+            ds_i = I.i;
         }
         if (a.carry) { /* persist the executors */
             for (uint32_t k = lane; k < 2u * R; k += 64) {
@@ -953,6 +1073,7 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
         }
         __builtin_amdgcn_wave_barrier();
     }
+    flush();
     const uint32_t nb = rdl(scan(bad_lane), 63u);
     if (lane == 0 && nb) atomicAdd(a.n_invalid, (unsigned long long)nb);
 }
@@ -1028,17 +1149,20 @@ static hipError_t launch_k(const agnes_tally_args* a, uint32_t lpw, int num_cus,
     const void* fn = reinterpret_cast<const void*>(&agnes::tally_kernel<WIDE, MODE, SKIP, SM, LIST>);
     const uint64_t wave_lds = (uint64_t)lpw * AGNES_WAVES_PER_BLOCK;
     const uint32_t scb = agnes::set_cache_bytes(a->n_sets);
+    const uint32_t pcb = WIDE ? 0u : agnes::power_cache_bytes(a->n_sets, a->n_vals);
     /* every wave owns an equal slice of the instances: launch the resident grid
-     * (blocks per CU from the occupancy query).  The set cache is used only when
-     * it does not lower the blocks per CU.  Cached per (kernel, LDS shape). */
-    struct Occ { const void* fn; uint64_t wave_lds; uint32_t scb; int per_cu; uint32_t use; };
+     * (blocks per CU from the occupancy query).  The set and power caches are
+     * used only where they do not lower the blocks per CU.  Cached per (kernel,
+     * LDS shape). */
+    struct Occ { const void* fn; uint64_t wave_lds; uint32_t scb, pcb; int per_cu; uint32_t use_s, use_p; };
     static thread_local Occ occ[8];
     static thread_local unsigned occ_next = 0;
     Occ* o = nullptr;
     for (auto& c : occ)
-        if (c.fn == fn && c.wave_lds == wave_lds && c.scb == scb) o = &c;
+        if (c.fn == fn && c.wave_lds == wave_lds && c.scb == scb && c.pcb == pcb) o = &c;
     if (!o) {
         auto blocks_per_cu = [&](uint64_t lds) -> int {
+            if (lds > 160u * 1024u) return 0;
             if (lds > 48u * 1024u &&
                 hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
                 return 0;
@@ -1047,20 +1171,27 @@ static hipError_t launch_k(const agnes_tally_args* a, uint32_t lpw, int num_cus,
                 per_cu = 0;
             return per_cu;
         };
-        const int without = blocks_per_cu(wave_lds);
-        const int with = scb ? blocks_per_cu(wave_lds + scb) : 0;
+        const int base = blocks_per_cu(wave_lds);
         o = &occ[occ_next++ % 8];
-        *o = Occ{fn, wave_lds, scb, 0, 0};
-        if (scb && with >= without && with > 0) {
-            o->per_cu = with;
-            o->use = scb;
-        } else {
-            o->per_cu = without > 0 ? without : 1;
+        *o = Occ{fn, wave_lds, scb, pcb, base > 0 ? base : 1, 0u, 0u};
+        /* preference: both caches, power only, set only, none */
+        const uint32_t cand[3][2] = {{scb, pcb}, {0u, pcb}, {scb, 0u}};
+        for (const auto& cd : cand) {
+            if (!cd[0] && !cd[1]) continue;
+            if ((cd[0] && !scb) || (cd[1] && !pcb)) continue;
+            const int pc = blocks_per_cu(wave_lds + cd[0] + cd[1]);
+            if (pc > 0 && pc >= base) {
+                o->per_cu = pc;
+                o->use_s = cd[0];
+                o->use_p = cd[1];
+                break;
+            }
         }
     }
     agnes_tally_args b = *a;
-    b.set_cache = o->use;
-    const uint64_t lds = wave_lds + o->use;
+    b.set_cache = o->use_s;
+    b.power_cache = o->use_p;
+    const uint64_t lds = wave_lds + o->use_s + o->use_p;
     if (lds > 48u * 1024u) {
         hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;

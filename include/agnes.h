@@ -198,7 +198,10 @@ typedef struct agnes_config {
  * Votes of one instance are CONTIGUOUS and in arrival order:
  *   instance i owns votes [offsets[i], offsets[i+1]).
  * Each instance is the reference's per-height executor pair (VoteExecutor +
- * State), one independent VoteExecutor per (instance, round). */
+ * State), one independent VoteExecutor per (instance, round).
+ * Alignment (device columns): instance/value/validator 16 B, round/type and the
+ * codes output 4 B, weight 8 B — any hipMalloc / torch allocation qualifies;
+ * otherwise agnes_tally returns AGNES_E_INVALID. */
 typedef struct agnes_vote_batch {
     const uint32_t* instance;  /* n_votes — must equal the owning segment's index  */
     const uint8_t* round;      /* n_votes — Vote.round                             */
