@@ -37,6 +37,9 @@
 
 namespace agnes {
 
+/* the kernels' dynamic LDS (block caches, then the per-wave executor areas) */
+extern __shared__ __attribute__((aligned(16))) unsigned char agnes_smem[];
+
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ uint32_t rdl(uint32_t x, uint32_t l) {
@@ -439,10 +442,10 @@ struct Raw {
     uint32_t r4, t4;
 };
 
-__device__ __forceinline__ void load_raw(const agnes_vote_batch& vb, uint64_t c, uint64_t lim,
-                                         Raw& x) {
+__device__ __forceinline__ void load_raw(const agnes_vote_batch& vb, uint64_t c, Raw& x) {
     const uint64_t j = c + 4u * lane_id();
-    if (j + VPL <= lim) {
+    const uint64_t NV = vb.n_votes;
+    if (c + CHUNK <= NV) { /* wave-uniform: the whole chunk lies inside the columns */
         const uint4 a = *reinterpret_cast<const uint4*>(vb.instance + j);
         const uint4 v = *reinterpret_cast<const uint4*>(vb.value + j);
         const uint4 d = *reinterpret_cast<const uint4*>(vb.validator + j);
@@ -451,11 +454,11 @@ __device__ __forceinline__ void load_raw(const agnes_vote_batch& vb, uint64_t c,
         x.val[0] = d.x; x.val[1] = d.y; x.val[2] = d.z; x.val[3] = d.w;
         x.r4 = *reinterpret_cast<const uint32_t*>(vb.round + j);
         x.t4 = *reinterpret_cast<const uint32_t*>(vb.type + j);
-    } else {
+    } else { /* the batch's last chunk */
         x.r4 = x.t4 = 0;
 #pragma unroll
         for (uint32_t s = 0; s < VPL; ++s) {
-            const bool in = j + s < lim;
+            const bool in = j + s < NV;
             x.inst[s] = in ? vb.instance[j + s] : 0u;
             x.value[s] = in ? vb.value[j + s] : 0u;
             x.val[s] = in ? vb.validator[j + s] : 0u;
@@ -498,24 +501,29 @@ template <typename W>
 struct Pre {
     uint32_t rr[VPL], tt[VPL];
     uint32_t f_valid, f_ok, f_nil; /* bit s = vote s of the lane */
-    W w[VPL];
+    W w[VPL]; /* meaningful only where f_ok */
 };
 
 /* validation (the vote belongs to the instance, round < max_rounds, type in
  * {0,1}, validator in the set) and the K1 weight gather
  * (consensus_executor.rs:62-63 -> validators.rs:7), branch-free; the gather reads
  * the block's LDS copy of the power table when the launcher staged one */
-template <bool WIDE, uint32_t MODE, bool SKIP>
+template <bool WIDE, uint32_t MODE, bool SKIP, bool PC>
 __device__ __forceinline__ void prep_chunk(const agnes_tally_args& a, const Inst& in_, uint64_t c,
-                                           const Raw& x, const uint32_t* pcache, Pre<
+                                           const Raw& x, uint32_t pc_off, Pre<
                                            typename std::conditional<WIDE, uint64_t, uint32_t>::type>& P,
                                            uint32_t& bad_lane) {
     using W = typename std::conditional<WIDE, uint64_t, uint32_t>::type;
     const uint32_t R = a.max_rounds;
     const uint32_t nv = a.n_vals;
     const agnes_vote_batch& vb = a.vb;
-    const bool has_w = vb.weight != nullptr;
+    const bool has_w = WIDE && vb.weight != nullptr; /* caller weights run on the i64 kernels */
     const bool need_val = !has_w || MODE == AGNES_MODE_DEDUP || SKIP;
+    /* uniform part of the checks: the validator must index the set's row when the
+     * vote needs it; the weight needs a valid set unless the caller supplied it */
+    const bool set_ok = in_.set_ok;
+    const bool vote_ok_u = has_w || set_ok;
+    const bool table = !has_w && (uint64_t)a.n_sets * nv > 0u;
     /* the instance's votes in this chunk: positions [lo, hi) */
     const uint32_t lo = c < in_.beg ? (uint32_t)(in_.beg - c) : 0u;
     const uint32_t hi = in_.end - c < CHUNK ? (uint32_t)(in_.end - c) : CHUNK;
@@ -525,21 +533,36 @@ __device__ __forceinline__ void prep_chunk(const agnes_tally_args& a, const Inst
     for (uint32_t s = 0; s < VPL; ++s) {
         P.rr[s] = (x.r4 >> (8u * s)) & 0xFFu;
         P.tt[s] = (x.t4 >> (8u * s)) & 0xFFu;
-        const bool valid = p0 + s >= lo && p0 + s < hi;
-        const bool ok = valid && x.inst[s] == in_.i && P.rr[s] < R && P.tt[s] <= 1u &&
-                        (!need_val || (in_.set_ok && x.val[s] < nv)) && (has_w || in_.set_ok);
-        bad_lane += (valid && !ok) ? 1u : 0u;
-        P.f_valid |= (valid ? 1u : 0u) << s;
-        P.f_ok |= (ok ? 1u : 0u) << s;
-        P.f_nil |= (x.value[s] == AGNES_NIL ? 1u : 0u) << s;
-        if (has_w) {
-            P.w[s] = ok ? (W)vb.weight[c + p0 + s] : (W)0;
-        } else {
+        /* bitwise, not short-circuit: no divergent branches */
+        const uint32_t valid = (uint32_t)(p0 + s >= lo) & (uint32_t)(p0 + s < hi);
+        const uint32_t vidx_ok = need_val ? ((uint32_t)set_ok & (uint32_t)(x.val[s] < nv)) : 1u;
+        const uint32_t ok = valid & (uint32_t)(x.inst[s] == in_.i) & (uint32_t)(P.rr[s] < R) &
+                            (uint32_t)(P.tt[s] <= 1u) & vidx_ok & (uint32_t)vote_ok_u;
+        bad_lane += valid & (ok ^ 1u);
+        P.f_valid |= valid << s;
+        P.f_ok |= ok << s;
+        P.f_nil |= (uint32_t)(x.value[s] == AGNES_NIL) << s;
+    }
+    if (has_w) {
+#pragma unroll
+        for (uint32_t s = 0; s < VPL; ++s)
+            P.w[s] = ((P.f_ok >> s) & 1u) ? (W)vb.weight[c + p0 + s] : (W)0;
+    } else if (!table) {
+#pragma unroll
+        for (uint32_t s = 0; s < VPL; ++s) P.w[s] = 0;
+    } else if (!WIDE && PC) { /* LDS copy of the table (lgkmcnt) */
+        const uint32_t* pc = reinterpret_cast<const uint32_t*>(agnes_smem + pc_off);
+#pragma unroll
+        for (uint32_t s = 0; s < VPL; ++s) {
+            const bool ok = (P.f_ok >> s) & 1u;
+            P.w[s] = (W)pc[ok ? in_.pbase + x.val[s] : 0u]; /* used only under f_acc <= f_ok */
+        }
+    } else { /* HBM table; entry 0 exists, so every lane loads (no divergence) */
+#pragma unroll
+        for (uint32_t s = 0; s < VPL; ++s) {
+            const bool ok = (P.f_ok >> s) & 1u;
             const uint32_t idx = ok ? in_.pbase + x.val[s] : 0u;
-            W g;
-            if (WIDE) g = (W)a.power[idx];
-            else g = pcache ? (W)pcache[idx] : (W)a.power32[idx];
-            P.w[s] = ok ? g : (W)0;
+            P.w[s] = WIDE ? (W)a.power[idx] : (W)a.power32[idx]; /* used only under f_acc */
         }
     }
 }
@@ -822,9 +845,9 @@ __host__ __device__ inline uint32_t power_cache_bytes(uint32_t n_sets, uint32_t 
  * and the next instance's header and State are in flight while one computes.
  * FAST kernels defer instances whose sums could reach 2^31 (or whose set is not
  * fast) to the WIDE LIST kernel. */
-template <bool WIDE, uint32_t MODE, bool SKIP, bool SM, bool LIST>
+template <bool WIDE, uint32_t MODE, bool SKIP, bool SM, bool LIST, bool PC>
 __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t lds_per_wave) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char* const smem = agnes_smem;
     const uint32_t lane = lane_id();
     const uint32_t wave = rfl(threadIdx.x >> 6);
     const uint32_t R = a.max_rounds;
@@ -855,14 +878,14 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
     /* block-shared power table (u32, fast kernels) when the launcher staged one: the
      * gather is then an LDS read, waited on by lgkmcnt, not behind the vector
      * memory queue of prefetches and stores */
-    const uint32_t* pcache = nullptr;
-    if (!WIDE && a.power_cache) {
+    uint32_t pc_off = 0xFFFFFFFFu;
+    if (!WIDE && PC) {
         uint32_t* pc = reinterpret_cast<uint32_t*>(smem + scb);
         const uint32_t np = ns * nv;
         for (uint32_t k = threadIdx.x; k < np; k += blockDim.x) pc[k] = a.power32[k];
-        pcache = pc;
+        pc_off = scb;
     }
-    if (scb || a.power_cache) __syncthreads();
+    if (scb || (!WIDE && PC)) __syncthreads();
 
     uint32_t q0, qend, qstep;
     if (LIST) {
@@ -1018,16 +1041,16 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
             if (pf_at == c) {
                 x = pf;
             } else {
-                load_raw(vb, c, LIST ? NV : vend, x);
+                load_raw(vb, c, x);
             }
             /* issue order: gather of this chunk, the previous chunk's stores, then the
              * next chunk (this instance's, or the next instance's first) */
             Pre<typename std::conditional<WIDE, uint64_t, uint32_t>::type> P;
-            prep_chunk<WIDE, MODE, SKIP>(a, I, c, x, pcache, P, bad_lane);
+            prep_chunk<WIDE, MODE, SKIP, PC>(a, I, c, x, pc_off, P, bad_lane);
             flush();
             const uint64_t nc = c + CHUNK < I.end ? c + CHUNK : (I.end & ~3ull);
             if (!LIST && nc < vend) {
-                load_raw(vb, nc, vend, pf);
+                load_raw(vb, nc, pf);
                 pf_at = nc;
             }
             dc_code = process_chunk<WIDE, MODE, SKIP, SM>(a, L, I, c, x, P, st, lb,
@@ -1146,7 +1169,7 @@ template <bool WIDE, uint32_t MODE, bool SKIP, bool SM, bool LIST>
 static hipError_t launch_k(const agnes_tally_args* a, uint32_t lpw, int num_cus, hipStream_t st) {
     const uint32_t n = a->vb.n_instances;
     if (n == 0) return hipSuccess;
-    const void* fn = reinterpret_cast<const void*>(&agnes::tally_kernel<WIDE, MODE, SKIP, SM, LIST>);
+    const void* fn = reinterpret_cast<const void*>(&agnes::tally_kernel<WIDE, MODE, SKIP, SM, LIST, false>);
     const uint64_t wave_lds = (uint64_t)lpw * AGNES_WAVES_PER_BLOCK;
     const uint32_t scb = agnes::set_cache_bytes(a->n_sets);
     const uint32_t pcb = WIDE ? 0u : agnes::power_cache_bytes(a->n_sets, a->n_vals);
@@ -1201,8 +1224,22 @@ static hipError_t launch_k(const agnes_tally_args* a, uint32_t lpw, int num_cus,
     uint64_t blocks = (n + AGNES_WAVES_PER_BLOCK - 1) / AGNES_WAVES_PER_BLOCK;
     if (blocks > cap) blocks = cap;
     if (LIST && blocks > ncu) blocks = ncu;
-    hipLaunchKernelGGL((agnes::tally_kernel<WIDE, MODE, SKIP, SM, LIST>), dim3((uint32_t)blocks), dim3(256),
-                       (size_t)lds, st, b, lpw);
+    bool launched = false;
+    if constexpr (!WIDE) {
+      if (o->use_p) {
+        const void* fp = reinterpret_cast<const void*>(&agnes::tally_kernel<WIDE, MODE, SKIP, SM, LIST, true>);
+        if (lds > 48u * 1024u) {
+            hipError_t e = hipFuncSetAttribute(fp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL((agnes::tally_kernel<WIDE, MODE, SKIP, SM, LIST, true>), dim3((uint32_t)blocks),
+                           dim3(256), (size_t)lds, st, b, lpw);
+        launched = true;
+      }
+    }
+    if (!launched)
+        hipLaunchKernelGGL((agnes::tally_kernel<WIDE, MODE, SKIP, SM, LIST, false>), dim3((uint32_t)blocks),
+                           dim3(256), (size_t)lds, st, b, lpw);
     return hipGetLastError();
 }
 
