@@ -276,25 +276,21 @@ __device__ bool sm_apply(Sm& s, int64_t round, uint32_t k, uint32_t v, int64_t p
  * chg bit idx: the event changes the state (applied on the scalar path);
  * msg nibble idx: the message a NON-changing event produces. */
 struct SmTab {
-    uint64_t msg;
-    uint32_t chg;
-    uint32_t pv_pc;      /* PolkaValue at eqr in Precommit: change iff valid differs (:202) */
-    uint32_t vsame;      /* valid == Some{round: s.round, ..}                           */
-    uint32_t vval;       /* valid value                                                 */
-    uint32_t r8;         /* s.round when in [0,255], else 0x100 (never a u8 round)      */
-    int32_t rlt;         /* clamp(s.round, -1, 256): u8 round r > rlt <=> s.round < r   */
+    uint32_t chg;   /* bit idx: the event changes the state (applied on the scalar path) */
+    uint32_t pv;    /* step == Prevote                                               */
+    uint32_t pc;    /* step == Precommit: PolkaValue at eqr changes iff valid differs (:202) */
+    uint32_t vsame; /* valid == Some{round: s.round, ..}                             */
+    uint32_t vval;  /* valid value                                                   */
+    uint32_t r8;    /* s.round when in [0,255], else 0x100 (never a u8 round)        */
+    int32_t rlt;    /* clamp(s.round, -1, 256): u8 round r > rlt <=> s.round < r      */
 };
 
 __device__ __forceinline__ SmTab sm_tab(const Sm& s) {
     SmTab t;
-    const bool pv = s.step == AGNES_STEP_PREVOTE;
-    t.msg = (uint64_t)AGNES_VMSG_TIMEOUT_PRECOMMIT << ((AGNES_CODE_PRECOMMIT_ANY * 2 + 1) * 4); /* :208 */
+    t.pv = s.step == AGNES_STEP_PREVOTE;
+    t.pc = s.step == AGNES_STEP_PRECOMMIT;
     t.chg = (1u << (AGNES_CODE_PRECOMMIT_VALUE * 2)) | (1u << (AGNES_CODE_PRECOMMIT_VALUE * 2 + 1)); /* :211 */
-    if (pv) {
-        t.msg |= (uint64_t)AGNES_VMSG_TIMEOUT_PREVOTE << ((AGNES_CODE_POLKA_ANY * 2 + 1) * 4); /* :196 */
-        t.chg |= (1u << (AGNES_CODE_POLKA_NIL * 2 + 1)) | (1u << (AGNES_CODE_POLKA_VALUE * 2 + 1));
-    }
-    t.pv_pc = s.step == AGNES_STEP_PRECOMMIT;
+    if (t.pv) t.chg |= (1u << (AGNES_CODE_POLKA_NIL * 2 + 1)) | (1u << (AGNES_CODE_POLKA_VALUE * 2 + 1));
     t.vsame = s.valid && s.valid_round == s.round;
     t.vval = s.valid_value;
     t.r8 = (s.round >= 0 && s.round <= 255) ? (uint32_t)s.round : 0x100u;
@@ -302,12 +298,20 @@ __device__ __forceinline__ SmTab sm_tab(const Sm& s) {
     return t;
 }
 
+/* Vote events against a wave-uniform state, branch-free.  idx = code*2 + eqr
+ * (code 1..5 = PolkaAny..PrecommitValue, eqr = s.round == r).  change: the event
+ * changes the state; msg: the message of a NON-changing event — TimeoutPrevote for
+ * PolkaAny at eqr in Prevote (:196), TimeoutPrecommit for PrecommitAny at eqr (:208). */
 __device__ __forceinline__ void sm_classify(const SmTab& t, uint32_t r, uint32_t code, uint32_t lab,
-                                            bool skip, bool& change, uint32_t& msg) {
-    const uint32_t idx = code * 2u + (r == t.r8 ? 1u : 0u);
-    const bool pvpc = t.pv_pc && idx == AGNES_CODE_POLKA_VALUE * 2u + 1u && !(t.vsame && t.vval == lab);
-    change = ((t.chg >> idx) & 1u) || (skip && (int32_t)r > t.rlt) || pvpc;
-    msg = change ? 0u : (uint32_t)(t.msg >> (idx * 4u)) & 0xFu;
+                                            uint32_t skip, uint32_t& change, uint32_t& msg) {
+    const uint32_t idx = code * 2u + (uint32_t)(r == t.r8);
+    const uint32_t pvpc = t.pc & (uint32_t)(idx == AGNES_CODE_POLKA_VALUE * 2u + 1u) &
+                          ((t.vsame & (uint32_t)(t.vval == lab)) ^ 1u);
+    change = ((t.chg >> idx) & 1u) | (skip & (uint32_t)((int32_t)r > t.rlt)) | pvpc;
+    const uint32_t m = (idx == AGNES_CODE_POLKA_ANY * 2u + 1u) ? (t.pv ? AGNES_VMSG_TIMEOUT_PREVOTE : 0u)
+                     : (idx == AGNES_CODE_PRECOMMIT_ANY * 2u + 1u) ? AGNES_VMSG_TIMEOUT_PRECOMMIT
+                                                                    : 0u;
+    msg = change ? 0u : m;
 }
 
 __device__ __forceinline__ uint32_t vmsg_of(bool h1, bool h2, const MsgOut& m2) {
@@ -390,6 +394,49 @@ __device__ __forceinline__ uint32_t sm_vote(Sm& s, int64_t r, uint32_t code, uin
                  : b == AGNES_VMSG_DECISION           ? AGNES_VMSG_NEW_ROUND_DECISION
                                                       : AGNES_VMSG_NEW_ROUND;
     return b;
+}
+
+/* The State of the instance being tallied lives lane-distributed in one VGPR
+ * (lane 16 + k = dword k of agnes_state, k < 14), so it costs no scalar registers
+ * outside the state-machine loop; unpacked to scalars only while events apply. */
+constexpr uint32_t SM_LANE = 16u;
+__device__ __forceinline__ Sm sm_unpack(uint32_t v) {
+    Sm s;
+    s.height = (int64_t)(((uint64_t)rdl(v, SM_LANE + 1u) << 32) | rdl(v, SM_LANE + 0u));
+    s.round = (int64_t)(((uint64_t)rdl(v, SM_LANE + 3u) << 32) | rdl(v, SM_LANE + 2u));
+    s.locked_round = (int64_t)(((uint64_t)rdl(v, SM_LANE + 5u) << 32) | rdl(v, SM_LANE + 4u));
+    s.valid_round = (int64_t)(((uint64_t)rdl(v, SM_LANE + 7u) << 32) | rdl(v, SM_LANE + 6u));
+    s.decision_round = (int64_t)(((uint64_t)rdl(v, SM_LANE + 9u) << 32) | rdl(v, SM_LANE + 8u));
+    s.locked_value = rdl(v, SM_LANE + 10u);
+    s.valid_value = rdl(v, SM_LANE + 11u);
+    s.decision_value = rdl(v, SM_LANE + 12u);
+    const uint32_t f = rdl(v, SM_LANE + 13u);
+    s.step = f & 0xFFu;
+    s.locked = (f >> 8) & 0xFFu;
+    s.valid = (f >> 16) & 0xFFu;
+    s.decided = f >> 24;
+    return s;
+}
+__device__ __forceinline__ uint32_t wrl(uint32_t v, uint32_t l, uint32_t x) {
+    return lane_id() == l ? x : v;
+}
+__device__ __forceinline__ uint32_t sm_pack(const Sm& s, uint32_t v) {
+    v = wrl(v, SM_LANE + 0u, (uint32_t)s.height);
+    v = wrl(v, SM_LANE + 1u, (uint32_t)((uint64_t)s.height >> 32));
+    v = wrl(v, SM_LANE + 2u, (uint32_t)s.round);
+    v = wrl(v, SM_LANE + 3u, (uint32_t)((uint64_t)s.round >> 32));
+    v = wrl(v, SM_LANE + 4u, (uint32_t)s.locked_round);
+    v = wrl(v, SM_LANE + 5u, (uint32_t)((uint64_t)s.locked_round >> 32));
+    v = wrl(v, SM_LANE + 6u, (uint32_t)s.valid_round);
+    v = wrl(v, SM_LANE + 7u, (uint32_t)((uint64_t)s.valid_round >> 32));
+    v = wrl(v, SM_LANE + 8u, (uint32_t)s.decision_round);
+    v = wrl(v, SM_LANE + 9u, (uint32_t)((uint64_t)s.decision_round >> 32));
+    v = wrl(v, SM_LANE + 10u, s.locked_value);
+    v = wrl(v, SM_LANE + 11u, s.valid_value);
+    v = wrl(v, SM_LANE + 12u, s.decision_value);
+    v = wrl(v, SM_LANE + 13u, (s.step & 0xFFu) | ((s.locked & 0xFFu) << 8) | ((s.valid & 0xFFu) << 16) |
+                                  (s.decided << 24));
+    return v;
 }
 
 /* ------------------------------------------------------------------ */
@@ -573,17 +620,20 @@ template <bool WIDE, uint32_t MODE, bool SKIP, bool SM>
 __device__ __forceinline__ uint32_t process_chunk(const agnes_tally_args& a, const WaveLds& L,
                                                   const Inst& in_, uint64_t c, const Raw& x,
                                                   const Pre<typename std::conditional<WIDE, uint64_t, uint32_t>::type>& P,
-                                                  Sm& st, uint32_t lb, bool ld_carry, bool st_carry) {
+                                                  uint32_t& stv, uint32_t lb, bool ld_carry, bool st_carry) {
     using W = typename std::conditional<WIDE, uint64_t, uint32_t>::type;
     const uint32_t lane = lane_id();
     const uint32_t nv = a.n_vals;
     const bool track = SM || a.carry != nullptr; /* labels: state machine / carried executors */
     const uint32_t p0 = 4u * lane;
-    const uint32_t(&rr)[VPL] = P.rr;
-    const uint32_t(&tt)[VPL] = P.tt;
     const W(&w)[VPL] = P.w;
     const uint32_t f_ok = P.f_ok, f_nil = P.f_nil;
     uint32_t f_acc = f_ok;
+    /* quorum tests of a running sum (round_votes.rs:32, fast path: s > floor(2t/3)) */
+    auto q23 = [&](W v) -> bool {
+        if (WIDE) return (int64_t)(3ull * (uint64_t)v) > (int64_t)(2ull * (uint64_t)in_.total);
+        return (uint32_t)v > in_.q2;
+    };
 
     /* first-vote-wins (DEDUP) / distinct-validator (RoundSkip) tables: atomic max of
      * (epoch << lb | LMASK - local index): the earliest vote of the instance wins,
@@ -592,55 +642,51 @@ __device__ __forceinline__ uint32_t process_chunk(const agnes_tally_args& a, con
     if (MODE == AGNES_MODE_DEDUP || SKIP) {
         const uint32_t lmask = (1u << lb) - 1u;
         const uint32_t loc0 = (uint32_t)(c - in_.beg) + p0; /* wraps only for votes before beg */
-        uint32_t enc[VPL];
 #pragma unroll
         for (uint32_t s = 0; s < VPL; ++s) {
-            enc[s] = (in_.ep << lb) | (lmask - (loc0 + s));
+            const uint32_t enc = (in_.ep << lb) | (lmask - (loc0 + s));
             if ((f_ok >> s) & 1u) {
                 if (MODE == AGNES_MODE_DEDUP)
-                    atomicMax(&L.first_v[(rr[s] * 2u + tt[s]) * nv + x.val[s]], enc[s]);
-                if (SKIP) atomicMax(&L.first_s[rr[s] * nv + x.val[s]], enc[s]);
+                    atomicMax(&L.first_v[(P.rr[s] * 2u + P.tt[s]) * nv + x.val[s]], enc);
+                if (SKIP) atomicMax(&L.first_s[P.rr[s] * nv + x.val[s]], enc);
             }
         }
         __builtin_amdgcn_wave_barrier();
         if (MODE == AGNES_MODE_DEDUP) f_acc = 0;
 #pragma unroll
         for (uint32_t s = 0; s < VPL; ++s) {
+            const uint32_t enc = (in_.ep << lb) | (lmask - (loc0 + s));
             if ((f_ok >> s) & 1u) {
                 if (MODE == AGNES_MODE_DEDUP)
-                    f_acc |= (*(volatile uint32_t*)&L.first_v[(rr[s] * 2u + tt[s]) * nv + x.val[s]] == enc[s]
-                                  ? 1u : 0u) << s;
-                if (SKIP)
-                    f_sfirst |= (*(volatile uint32_t*)&L.first_s[rr[s] * nv + x.val[s]] == enc[s] ? 1u : 0u)
-                                << s;
+                    f_acc |= (uint32_t)(*(volatile uint32_t*)&L.first_v[(P.rr[s] * 2u + P.tt[s]) * nv + x.val[s]] ==
+                                        enc) << s;
+                if (SKIP) f_sfirst |= (uint32_t)(*(volatile uint32_t*)&L.first_s[P.rr[s] * nv + x.val[s]] == enc) << s;
             }
         }
         __builtin_amdgcn_wave_barrier();
     }
 
-    /* K2: per (round,type) slot present, one stream-order scan of the value and nil
-     * buckets over the chunk plus the running executor — VoteCount::add_vote's sums
-     * (round_votes.rs:48-56) */
-    uint32_t slot[VPL];
-    W pv[VPL], pn[VPL];
+    /* K2+K3: per (round,type) slot present, one stream-order scan of the value and
+     * nil buckets over the chunk plus the running executor — VoteCount::add_vote's
+     * sums (round_votes.rs:48-56) — and at once is_quorum with precedence
+     * Value > Nil > Any > Init (:58-66) and to_event (vote_executor.rs:26-36).
+     * codes: byte s = vote s's code; lab[s]: the Thresh::Value payload. */
+    uint32_t codes = 0;
     uint32_t lab[VPL];
 #pragma unroll
-    for (uint32_t s = 0; s < VPL; ++s) {
-        slot[s] = rr[s] * 2u + tt[s];
-        pv[s] = 0;
-        pn[s] = 0;
-        lab[s] = 0;
-    }
+    for (uint32_t s = 0; s < VPL; ++s) lab[s] = 0;
     uint32_t rem = f_acc;
     for (;;) {
         const uint64_t lm = ballot(rem != 0u);
         if (!lm) break;
         const uint32_t kl = (uint32_t)__builtin_ctzll(lm);
         const uint32_t ks = (uint32_t)__builtin_ctz(rdl(rem, kl));
-        const uint32_t key = rdl(pick4(slot, ks), kl);
+        const uint32_t key = rdl(pick4(P.rr, ks) * 2u + pick4(P.tt, ks), kl);
+        const uint32_t kt = key & 1u; /* the slot's vote type */
         uint32_t inb = 0;
 #pragma unroll
-        for (uint32_t s = 0; s < VPL; ++s) inb |= (((rem >> s) & 1u) && slot[s] == key ? 1u : 0u) << s;
+        for (uint32_t s = 0; s < VPL; ++s)
+            inb |= (uint32_t)(((rem >> s) & 1u) && P.rr[s] * 2u + P.tt[s] == key) << s;
         rem &= ~inb;
         W cv = 0, cn = 0;
         uint32_t lbl = 0;
@@ -658,27 +704,25 @@ __device__ __forceinline__ uint32_t process_chunk(const agnes_tally_args& a, con
         }
         const W tv = scan4(av, ov);
         const W tn = scan4(an, on);
+        uint32_t qvb = 0;
 #pragma unroll
         for (uint32_t s = 0; s < VPL; ++s) {
-            if ((inb >> s) & 1u) {
-                pv[s] = cv + ov[s];
-                pn[s] = cn + on[s];
-            }
+            const W pv = cv + ov[s], pn = cn + on[s];
+            const bool qv = q23(pv), qn = q23(pn), qa = q23(pv + pn);
+            const uint32_t ev = qv ? (kt ? AGNES_CODE_PRECOMMIT_VALUE : AGNES_CODE_POLKA_VALUE)
+                              : qn ? (kt ? AGNES_CODE_NONE : AGNES_CODE_POLKA_NIL)
+                              : qa ? (kt ? AGNES_CODE_PRECOMMIT_ANY : AGNES_CODE_POLKA_ANY)
+                                   : AGNES_CODE_NONE;
+            const bool in = (inb >> s) & 1u;
+            codes |= (in ? ev : 0u) << (8u * s);
+            qvb |= (uint32_t)(in && qv) << s;
         }
         if (track) { /* Thresh::Value payload: the last value written (round_votes.rs:53) */
             const uint32_t nnb = inb & ~f_nil; /* this key's value votes in the lane */
             const uint32_t lastv = nnb ? pick4(x.value, 31u - (uint32_t)__builtin_clz(nnb)) : 0u;
             const uint64_t lanes_nn = ballot(nnb != 0u);
             /* a nil vote needs a propagated label only when its value bucket is at quorum */
-            bool need = false;
-#pragma unroll
-            for (uint32_t s = 0; s < VPL; ++s) {
-                bool qv;
-                if (WIDE) qv = (int64_t)(3ull * (uint64_t)pv[s]) > (int64_t)(2ull * (uint64_t)in_.total);
-                else qv = (uint32_t)pv[s] > in_.q2;
-                need |= ((inb & f_nil) >> s) & 1u && qv;
-            }
-            if (ballot(need)) {
+            if (ballot((qvb & f_nil) != 0u)) {
                 const uint64_t le = lanes_nn & lanemask_lt(lane);
                 const uint32_t got = shfl(lastv, le ? 63u - (uint32_t)__builtin_clzll(le) : 0u);
                 uint32_t run = le ? got : lbl;
@@ -704,9 +748,6 @@ __device__ __forceinline__ uint32_t process_chunk(const agnes_tally_args& a, con
 
     /* RoundSkip (+1/3 of distinct validators of the vote's round, extension):
      * the same scheme keyed by round over each validator's first vote */
-    W ps[VPL];
-#pragma unroll
-    for (uint32_t s = 0; s < VPL; ++s) ps[s] = 0;
     if (SKIP) {
         uint32_t rs = f_acc;
         for (;;) {
@@ -714,10 +755,10 @@ __device__ __forceinline__ uint32_t process_chunk(const agnes_tally_args& a, con
             if (!lm) break;
             const uint32_t kl = (uint32_t)__builtin_ctzll(lm);
             const uint32_t ks = (uint32_t)__builtin_ctz(rdl(rs, kl));
-            const uint32_t kr = rdl(pick4(rr, ks), kl);
+            const uint32_t kr = rdl(pick4(P.rr, ks), kl);
             uint32_t inb = 0;
 #pragma unroll
-            for (uint32_t s = 0; s < VPL; ++s) inb |= (((rs >> s) & 1u) && rr[s] == kr ? 1u : 0u) << s;
+            for (uint32_t s = 0; s < VPL; ++s) inb |= (uint32_t)(((rs >> s) & 1u) && P.rr[s] == kr) << s;
             rs &= ~inb;
             const W cs = ld_carry ? (W)L.skw[kr] : (W)0;
             W as[VPL], os[VPL];
@@ -725,43 +766,23 @@ __device__ __forceinline__ uint32_t process_chunk(const agnes_tally_args& a, con
             for (uint32_t s = 0; s < VPL; ++s) as[s] = ((inb & f_sfirst) >> s) & 1u ? w[s] : (W)0;
             const W ts = scan4(as, os);
 #pragma unroll
-            for (uint32_t s = 0; s < VPL; ++s)
-                if ((inb >> s) & 1u) ps[s] = cs + os[s];
+            for (uint32_t s = 0; s < VPL; ++s) {
+                const W ps = cs + os[s];
+                bool q3;
+                if (WIDE) q3 = (int64_t)(3ull * (uint64_t)ps) > in_.total;
+                else q3 = (uint32_t)ps > in_.q1;
+                codes |= (uint32_t)(((inb >> s) & 1u) && q3) << (8u * s + 3u);
+            }
             if (st_carry) L.skw[kr] = (uint64_t)(cs + ts);
             __builtin_amdgcn_wave_barrier();
         }
     }
 
-    /* K3: is_quorum precedence Value > Nil > Any > Init (round_votes.rs:58-66) and
-     * to_event (vote_executor.rs:26-36) */
-    uint32_t code[VPL];
+    /* votes that are not tallied */
 #pragma unroll
     for (uint32_t s = 0; s < VPL; ++s) {
-        if (!((f_ok >> s) & 1u)) {
-            code[s] = AGNES_CODE_INVALID;
-        } else if (!((f_acc >> s) & 1u)) {
-            code[s] = AGNES_CODE_REJECTED;
-        } else {
-            bool qv, qn, qa, q3;
-            if (WIDE) { /* literal i64 wrapping: round_votes.rs:32 */
-                const int64_t t2 = (int64_t)(2ull * (uint64_t)in_.total);
-                qv = (int64_t)(3ull * (uint64_t)pv[s]) > t2;
-                qn = (int64_t)(3ull * (uint64_t)pn[s]) > t2;
-                qa = (int64_t)(3ull * ((uint64_t)pv[s] + (uint64_t)pn[s])) > t2;
-                q3 = (int64_t)(3ull * (uint64_t)ps[s]) > in_.total;
-            } else {
-                qv = (uint32_t)pv[s] > in_.q2;
-                qn = (uint32_t)pn[s] > in_.q2;
-                qa = (uint32_t)pv[s] + (uint32_t)pn[s] > in_.q2;
-                q3 = (uint32_t)ps[s] > in_.q1;
-            }
-            const uint32_t t = tt[s];
-            const uint32_t ev = qv ? (t ? AGNES_CODE_PRECOMMIT_VALUE : AGNES_CODE_POLKA_VALUE)
-                              : qn ? (t ? AGNES_CODE_NONE : AGNES_CODE_POLKA_NIL)
-                              : qa ? (t ? AGNES_CODE_PRECOMMIT_ANY : AGNES_CODE_POLKA_ANY)
-                                   : AGNES_CODE_NONE;
-            code[s] = ev | ((SKIP && q3) ? AGNES_CODE_SKIP : 0u);
-        }
+        if (!((f_ok >> s) & 1u)) codes |= AGNES_CODE_INVALID << (8u * s);
+        else if (!((f_acc >> s) & 1u)) codes |= AGNES_CODE_REJECTED << (8u * s);
     }
 
     /* K4: State::apply(v.round, event) in stream order (consensus_executor.rs:64-68):
@@ -769,51 +790,61 @@ __device__ __forceinline__ uint32_t process_chunk(const agnes_tally_args& a, con
      * (wave-uniform) state; votes before the first state change get their message,
      * the changing vote is applied on the scalar path, repeat */
     if (SM) {
-        uint32_t msg[VPL];
+        uint32_t msgs = 0; /* nibble s: vote s's message */
         uint32_t pend = 0;
 #pragma unroll
-        for (uint32_t s = 0; s < VPL; ++s) {
-            msg[s] = 0;
-            pend |= (((f_acc >> s) & 1u) && (code[s] & 0x0Fu) != 0u ? 1u : 0u) << s;
+        for (uint32_t s = 0; s < VPL; ++s)
+            pend |= (uint32_t)(((f_acc >> s) & 1u) && ((codes >> (8u * s)) & 0x0Fu) != 0u) << s;
+        if (ballot(pend != 0u) && (rdl(stv, SM_LANE + 13u) & 0xFFu) != AGNES_STEP_COMMIT) {
+            Sm st = sm_unpack(stv); /* scalar State for this chunk's passes */
+            bool changed = false;
+            while (st.step != AGNES_STEP_COMMIT && ballot(pend != 0u)) { /* :205 */
+                const SmTab tb = sm_tab(st);
+                uint32_t chb = 0, cm = 0;
+#pragma unroll
+                for (uint32_t s = 0; s < VPL; ++s) {
+                    uint32_t chg, m;
+                    const uint32_t cd = (codes >> (8u * s)) & 0xFFu;
+                    sm_classify(tb, P.rr[s], cd & AGNES_CODE_EVENT_MASK, lab[s], (cd >> 3) & 1u, chg, m);
+                    chb |= chg << s;
+                    cm |= m << (4u * s);
+                }
+                chb &= pend;
+                const uint64_t bk = ballot(chb != 0u);
+                uint32_t first = 0xFFFFFFFFu; /* chunk position 4*lane+s of the first change */
+                uint32_t fl = 0, fs = 0;
+                if (bk) {
+                    fl = (uint32_t)__builtin_ctzll(bk);
+                    fs = (uint32_t)__builtin_ctz(rdl(chb, fl));
+                    first = 4u * fl + fs;
+                }
+                /* votes before the change: their message under this state */
+                uint32_t before = 0;
+#pragma unroll
+                for (uint32_t s = 0; s < VPL; ++s) before |= (uint32_t)(p0 + s < first) << s;
+                before &= pend;
+#pragma unroll
+                for (uint32_t s = 0; s < VPL; ++s)
+                    if ((before >> s) & 1u) msgs = (msgs & ~(0xFu << (4u * s))) | (cm & (0xFu << (4u * s)));
+                if (!bk) break;
+                const int64_t fr = (int64_t)rdl(pick4(P.rr, fs), fl);
+                const uint32_t fcode = (rdl(codes, fl) >> (8u * fs)) & 0xFFu;
+                const uint32_t flab = rdl(pick4(lab, fs), fl);
+                const uint32_t vm = sm_vote(st, fr, fcode, flab);
+                changed = true;
+#pragma unroll
+                for (uint32_t s = 0; s < VPL; ++s) {
+                    if (p0 + s == first) msgs = (msgs & ~(0xFu << (4u * s))) | (vm << (4u * s));
+                    if (p0 + s <= first) pend &= ~(1u << s); /* drop every vote up to the change */
+                }
+            }
+            if (changed) stv = sm_pack(st, stv);
         }
-        while (st.step != AGNES_STEP_COMMIT && ballot(pend != 0u)) {
-            const SmTab tb = sm_tab(st);
-            uint32_t chb = 0, cm[VPL];
 #pragma unroll
-            for (uint32_t s = 0; s < VPL; ++s) {
-                bool chg;
-                sm_classify(tb, rr[s], code[s] & AGNES_CODE_EVENT_MASK, lab[s],
-                            (code[s] & AGNES_CODE_SKIP) != 0u, chg, cm[s]);
-                chb |= (chg ? 1u : 0u) << s;
-            }
-            chb &= pend;
-            const uint64_t bk = ballot(chb != 0u);
-            uint32_t first = 0xFFFFFFFFu; /* chunk position 4*lane+s of the first change */
-            uint32_t fl = 0, fs = 0;
-            if (bk) {
-                fl = (uint32_t)__builtin_ctzll(bk);
-                fs = (uint32_t)__builtin_ctz(rdl(chb, fl));
-                first = 4u * fl + fs;
-            }
-#pragma unroll
-            for (uint32_t s = 0; s < VPL; ++s)
-                if (((pend >> s) & 1u) && p0 + s < first) msg[s] = cm[s];
-            if (!bk) break;
-            const int64_t fr = (int64_t)rdl(pick4(rr, fs), fl);
-            const uint32_t fcode = rdl(pick4(code, fs), fl);
-            const uint32_t flab = rdl(pick4(lab, fs), fl);
-            const uint32_t vm = sm_vote(st, fr, fcode, flab);
-#pragma unroll
-            for (uint32_t s = 0; s < VPL; ++s) {
-                if (p0 + s == first) msg[s] = vm;
-                if (p0 + s <= first) pend &= ~(1u << s); /* drop every vote up to the change */
-            }
-        }
-#pragma unroll
-        for (uint32_t s = 0; s < VPL; ++s) code[s] |= msg[s] << AGNES_CODE_MSG_SHIFT;
+        for (uint32_t s = 0; s < VPL; ++s)
+            codes |= ((msgs >> (4u * s)) & 0xFu) << (8u * s + AGNES_CODE_MSG_SHIFT);
     }
-
-    return code[0] | (code[1] << 8) | (code[2] << 16) | (code[3] << 24);
+    return codes;
 }
 
 /* the lane's 4 code bytes of chunk c: one 4-B store when all 4 belong to the pass */
@@ -925,12 +956,13 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
      * in issue order: a store ahead of a load delays every wait on that load) */
     uint64_t dc_at = ~0ull;      /* chunk whose codes are pending                  */
     uint32_t dc_code = 0, dc_valid = 0;
-    uint32_t ds_i = 0xFFFFFFFFu; /* instance whose State (lanes 0..13) is pending */
+    uint32_t ds_i = 0xFFFFFFFFu; /* instance whose State (lanes 16..29) is pending */
     uint32_t ds_word = 0;
     auto flush = [&]() {
         if (dc_at != ~0ull) store_codes(a.codes, dc_at, dc_code, dc_valid);
         dc_at = ~0ull;
-        if (SM && ds_i != 0xFFFFFFFFu && lane < 14u) reinterpret_cast<uint32_t*>(&a.states[ds_i])[lane] = ds_word;
+        if (SM && ds_i != 0xFFFFFFFFu && lane >= SM_LANE && lane < SM_LANE + 14u)
+            reinterpret_cast<uint32_t*>(&a.states[ds_i])[lane - SM_LANE] = ds_word;
         ds_i = 0xFFFFFFFFu;
     };
 
@@ -1018,22 +1050,7 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
             }
             for (uint32_t k = lane; k < R; k += 64) L.skw[k] = 0;
         }
-        Sm st;
-        if (SM) { /* State from the header lanes 16..29 */
-            st.height = (int64_t)(((uint64_t)rdl(h, 17u) << 32) | rdl(h, 16u));
-            st.round = (int64_t)(((uint64_t)rdl(h, 19u) << 32) | rdl(h, 18u));
-            st.locked_round = (int64_t)(((uint64_t)rdl(h, 21u) << 32) | rdl(h, 20u));
-            st.valid_round = (int64_t)(((uint64_t)rdl(h, 23u) << 32) | rdl(h, 22u));
-            st.decision_round = (int64_t)(((uint64_t)rdl(h, 25u) << 32) | rdl(h, 24u));
-            st.locked_value = rdl(h, 26u);
-            st.valid_value = rdl(h, 27u);
-            st.decision_value = rdl(h, 28u);
-            const uint32_t f = rdl(h, 29u);
-            st.step = f & 0xFFu;
-            st.locked = (f >> 8) & 0xFFu;
-            st.valid = (f >> 16) & 0xFFu;
-            st.decided = f >> 24;
-        }
+        uint32_t stv = h; /* State: header lanes 16..29 */
         __builtin_amdgcn_wave_barrier();
 
         for (uint64_t c = c0; c < I.end; c += CHUNK) {
@@ -1053,35 +1070,15 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
                 load_raw(vb, nc, pf);
                 pf_at = nc;
             }
-            dc_code = process_chunk<WIDE, MODE, SKIP, SM>(a, L, I, c, x, P, st, lb,
+            dc_code = process_chunk<WIDE, MODE, SKIP, SM>(a, L, I, c, x, P, stv, lb,
                                                           /*ld_carry=*/c != c0 || a.carry != nullptr,
                                                           /*st_carry=*/c + CHUNK < I.end || a.carry != nullptr);
             dc_valid = P.f_valid;
             dc_at = c;
             __builtin_amdgcn_wave_barrier();
         }
-        if (SM) { /* State back (deferred): one dword per lane, lanes 0..13 */
-            const uint32_t f = (st.step & 0xFFu) | ((st.locked & 0xFFu) << 8) |
-                               ((st.valid & 0xFFu) << 16) | (st.decided << 24);
-            uint32_t d = 0;
-            switch (lane) {
-            case 0: d = (uint32_t)st.height; break;
-            case 1: d = (uint32_t)((uint64_t)st.height >> 32); break;
-            case 2: d = (uint32_t)st.round; break;
-            case 3: d = (uint32_t)((uint64_t)st.round >> 32); break;
-            case 4: d = (uint32_t)st.locked_round; break;
-            case 5: d = (uint32_t)((uint64_t)st.locked_round >> 32); break;
-            case 6: d = (uint32_t)st.valid_round; break;
-            case 7: d = (uint32_t)((uint64_t)st.valid_round >> 32); break;
-            case 8: d = (uint32_t)st.decision_round; break;
-            case 9: d = (uint32_t)((uint64_t)st.decision_round >> 32); break;
-            case 10: d = st.locked_value; break;
-            case 11: d = st.valid_value; break;
-            case 12: d = st.decision_value; break;
-            case 13: d = f; break;
-            default: break;
-            }
-            ds_word = d;
+        if (SM) { /* State back (deferred) */
+            ds_word = stv;
             ds_i = I.i;
         }
         if (a.carry) { /* persist the executors */
