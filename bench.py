@@ -62,6 +62,18 @@ def start_states(n: int) -> np.ndarray:
     return abi.new_states(n, height=1, step=abi.STEP_PREVOTE, round_=0)
 
 
+def measured_traffic(config: str):
+    """HBM bytes per launch of the tally kernel for this workload, from the
+    rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this same command committed under
+    profiles/ (tools/pmc_traffic.py applies the gfx950 corrections); None if the
+    workload has not been profiled."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
+            return json.load(f).get(config)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(eng, cfg, batch, power, states0, set_of_instance):
     """The checker (oracle/, scalar C, pthreads over instances) on the same batch."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -154,6 +166,7 @@ def main():
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in pairs]))
 
     if rank == 0:
+        traffic = measured_traffic(args.config)
         ms_per_step = elapsed * 1e3 / args.steps
         value = total_votes_step * args.steps / elapsed
         achieved = BYTES_PER_VOTE * batch.n_votes / (kernel_ms * 1e-3) / 1e9
@@ -177,9 +190,12 @@ def main():
                        "flags": w["flags"], "parallelism": f"instance-sharded x{world}"},
             "kernel_ms": kernel_ms,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic.get("traffic_bytes") if traffic else None,
+                         "traffic_source": traffic.get("sources") if traffic else None,
                          "kernel": "agnes::tally_kernel",
-                         "bytes_per_vote": BYTES_PER_VOTE},
+                         "bytes_per_vote": BYTES_PER_VOTE,
+                         "algorithmic_bytes": BYTES_PER_VOTE * batch.n_votes},
         }
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(eng, cfg, batch, power, st0_host, set_of)
