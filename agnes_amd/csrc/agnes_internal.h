@@ -62,6 +62,11 @@ int64_t agnes_lds_per_wave(uint32_t mode, uint32_t flags, uint32_t max_rounds, u
  * defers the instances it cannot prove to the i64 list kernel */
 hipError_t agnes_launch_tally(const agnes_tally_args* a, uint32_t mode, int num_cus, bool wide_all,
                               hipStream_t stream);
+/* the u32 fast-path kernel (agnes_fast.hip): every instance it can prove stays
+ * below 2^31, the rest appended to a->list for the i64 LIST kernel */
+hipError_t agnes_launch_tally_fast(const agnes_tally_args* a, uint32_t mode, int num_cus,
+                                   hipStream_t stream);
+int64_t agnes_fast_lds_per_wave(uint32_t mode, uint32_t flags, uint32_t max_rounds, uint32_t n_vals);
 hipError_t agnes_launch_apply_events(agnes_state* states, uint32_t n, const uint64_t* off,
                                      const agnes_event* ev, agnes_message* msgs, uint32_t flags,
                                      hipStream_t stream);
@@ -70,6 +75,9 @@ hipError_t agnes_launch_gen(const agnes_gen_params* p, const uint64_t* d_offsets
                             uint32_t* validator, hipStream_t stream);
 
 #define AGNES_WAVES_PER_BLOCK 4
+/* list_count[0] counts the deferred list; list_count[1 .. AGNES_QUEUE_WORDS-1] are the
+ * fast kernel's work-queue counters; all zeroed before each launch */
+#define AGNES_QUEUE_WORDS 257
 #define AGNES_MAX_LDS_PER_WAVE (36 * 1024)
 
 #endif

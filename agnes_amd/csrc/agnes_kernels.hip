@@ -32,71 +32,11 @@
  *
  * No MFMA: the path is HBM-bound integer work.
  */
+#include "agnes_device.h"
 #include "agnes_gen.h"
 #include "agnes_internal.h"
 
 namespace agnes {
-
-/* the kernels' dynamic LDS (block caches, then the per-wave executor areas) */
-extern __shared__ __attribute__((aligned(16))) unsigned char agnes_smem[];
-
-__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
-__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
-__device__ __forceinline__ uint32_t rdl(uint32_t x, uint32_t l) {
-    return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l);
-}
-__device__ __forceinline__ uint64_t rdl(uint64_t x, uint32_t l) {
-    uint32_t lo = rdl((uint32_t)x, l), hi = rdl((uint32_t)(x >> 32), l);
-    return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ uint32_t rfl(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
-}
-__device__ __forceinline__ uint64_t rfl64(uint64_t x) {
-    return ((uint64_t)rfl((uint32_t)(x >> 32)) << 32) | rfl((uint32_t)x);
-}
-__device__ __forceinline__ uint64_t lanemask_le(uint32_t l) { return (2ull << l) - 1ull; }
-/* x of lane `src` (ds_bpermute) */
-__device__ __forceinline__ uint32_t shfl(uint32_t x, uint32_t src) {
-    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)x);
-}
-__device__ __forceinline__ uint64_t shfl(uint64_t x, uint32_t src) {
-    return ((uint64_t)shfl((uint32_t)(x >> 32), src) << 32) | shfl((uint32_t)x, src);
-}
-
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ uint32_t dpp(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROW_MASK, 0xf, false);
-}
-
-/* wave64 inclusive scan: row_shr 1,2,4,8 inside 16-lane rows, then row_bcast15
- * (rows 1,3) and row_bcast31 (rows 2,3).  All 64 lanes must be active. */
-__device__ __forceinline__ uint32_t scan(uint32_t x) {
-    x += dpp<0x111, 0xf>(x);
-    x += dpp<0x112, 0xf>(x);
-    x += dpp<0x114, 0xf>(x);
-    x += dpp<0x118, 0xf>(x);
-    x += dpp<0x142, 0xa>(x);
-    x += dpp<0x143, 0xc>(x);
-    return x;
-}
-
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ uint64_t dpp_step64(uint64_t x) {
-    uint32_t lo = dpp<CTRL, ROW_MASK>((uint32_t)x);
-    uint32_t hi = dpp<CTRL, ROW_MASK>((uint32_t)(x >> 32));
-    return x + (((uint64_t)hi << 32) | lo);
-}
-
-__device__ __forceinline__ uint64_t scan(uint64_t x) {
-    x = dpp_step64<0x111, 0xf>(x);
-    x = dpp_step64<0x112, 0xf>(x);
-    x = dpp_step64<0x114, 0xf>(x);
-    x = dpp_step64<0x118, 0xf>(x);
-    x = dpp_step64<0x142, 0xa>(x);
-    x = dpp_step64<0x143, 0xc>(x);
-    return x;
-}
 
 /* ------------------------------------------------------------------ */
 /* State machine (state_machine.rs:183-322)                            */
@@ -417,24 +357,21 @@ __device__ __forceinline__ Sm sm_unpack(uint32_t v) {
     s.decided = f >> 24;
     return s;
 }
-__device__ __forceinline__ uint32_t wrl(uint32_t v, uint32_t l, uint32_t x) {
-    return lane_id() == l ? x : v;
-}
 __device__ __forceinline__ uint32_t sm_pack(const Sm& s, uint32_t v) {
-    v = wrl(v, SM_LANE + 0u, (uint32_t)s.height);
-    v = wrl(v, SM_LANE + 1u, (uint32_t)((uint64_t)s.height >> 32));
-    v = wrl(v, SM_LANE + 2u, (uint32_t)s.round);
-    v = wrl(v, SM_LANE + 3u, (uint32_t)((uint64_t)s.round >> 32));
-    v = wrl(v, SM_LANE + 4u, (uint32_t)s.locked_round);
-    v = wrl(v, SM_LANE + 5u, (uint32_t)((uint64_t)s.locked_round >> 32));
-    v = wrl(v, SM_LANE + 6u, (uint32_t)s.valid_round);
-    v = wrl(v, SM_LANE + 7u, (uint32_t)((uint64_t)s.valid_round >> 32));
-    v = wrl(v, SM_LANE + 8u, (uint32_t)s.decision_round);
-    v = wrl(v, SM_LANE + 9u, (uint32_t)((uint64_t)s.decision_round >> 32));
-    v = wrl(v, SM_LANE + 10u, s.locked_value);
-    v = wrl(v, SM_LANE + 11u, s.valid_value);
-    v = wrl(v, SM_LANE + 12u, s.decision_value);
-    v = wrl(v, SM_LANE + 13u, (s.step & 0xFFu) | ((s.locked & 0xFFu) << 8) | ((s.valid & 0xFFu) << 16) |
+    v = wrl<SM_LANE + 0u>(v, (uint32_t)s.height);
+    v = wrl<SM_LANE + 1u>(v, (uint32_t)((uint64_t)s.height >> 32));
+    v = wrl<SM_LANE + 2u>(v, (uint32_t)s.round);
+    v = wrl<SM_LANE + 3u>(v, (uint32_t)((uint64_t)s.round >> 32));
+    v = wrl<SM_LANE + 4u>(v, (uint32_t)s.locked_round);
+    v = wrl<SM_LANE + 5u>(v, (uint32_t)((uint64_t)s.locked_round >> 32));
+    v = wrl<SM_LANE + 6u>(v, (uint32_t)s.valid_round);
+    v = wrl<SM_LANE + 7u>(v, (uint32_t)((uint64_t)s.valid_round >> 32));
+    v = wrl<SM_LANE + 8u>(v, (uint32_t)s.decision_round);
+    v = wrl<SM_LANE + 9u>(v, (uint32_t)((uint64_t)s.decision_round >> 32));
+    v = wrl<SM_LANE + 10u>(v, s.locked_value);
+    v = wrl<SM_LANE + 11u>(v, s.valid_value);
+    v = wrl<SM_LANE + 12u>(v, s.decision_value);
+    v = wrl<SM_LANE + 13u>(v, (s.step & 0xFFu) | ((s.locked & 0xFFu) << 8) | ((s.valid & 0xFFu) << 16) |
                                   (s.decided << 24));
     return v;
 }
@@ -454,8 +391,6 @@ struct WaveLds {
     uint32_t* first_s; /* SKIP  [R][nv]:  same per (round, validator)                    */
 };
 
-__host__ __device__ inline uint64_t align16(uint64_t x) { return (x + 15u) & ~15ull; }
-
 __host__ __device__ inline void lds_layout(uint32_t mode, uint32_t flags, uint32_t R, uint32_t nv,
                                            uint64_t* o_first_v, uint64_t* o_first_s,
                                            uint64_t* total) {
@@ -465,14 +400,6 @@ __host__ __device__ inline void lds_layout(uint32_t mode, uint32_t flags, uint32
     *o_first_s = o;
     if (flags & AGNES_FLAG_ROUND_SKIP) o = align16(o + (uint64_t)R * nv * 4u);
     *total = o;
-}
-
-__device__ inline void fill_u32(uint32_t* p, uint64_t n, uint32_t v, uint32_t lane) {
-    const uint64_t n4 = n >> 2;
-    uint4* q = reinterpret_cast<uint4*>(p);
-    const uint4 vv = make_uint4(v, v, v, v);
-    for (uint64_t k = lane; k < n4; k += 64) q[k] = vv;
-    for (uint64_t k = (n4 << 2) + lane; k < n; k += 64) p[k] = v;
 }
 
 /* ------------------------------------------------------------------ */
@@ -528,8 +455,6 @@ __device__ __forceinline__ W scan4(const W (&a)[VPL], W (&o)[VPL]) {
     o[3] = ex + l3;
     return rdl(inc, 63u);
 }
-
-__device__ __forceinline__ uint64_t lanemask_lt(uint32_t l) { return (1ull << l) - 1ull; }
 
 /* uniform facts of the instance being tallied */
 struct Inst {
@@ -1244,8 +1169,8 @@ template <uint32_t MODE, bool SKIP, bool SM>
 static hipError_t launch_mode(const agnes_tally_args* a, uint32_t lpw, int num_cus, bool wide_all,
                               hipStream_t st) {
     if (wide_all) return launch_k<true, MODE, SKIP, SM, false>(a, lpw, num_cus, st);
-    hipError_t e = hipMemsetAsync(a->list_count, 0, sizeof(uint32_t), st);
-    if (e == hipSuccess) e = launch_k<false, MODE, SKIP, SM, false>(a, lpw, num_cus, st);
+    hipError_t e = hipMemsetAsync(a->list_count, 0, AGNES_QUEUE_WORDS * sizeof(uint32_t), st);
+    if (e == hipSuccess) e = agnes_launch_tally_fast(a, MODE, num_cus, st);
     if (e == hipSuccess) e = launch_k<true, MODE, SKIP, SM, true>(a, lpw, num_cus, st);
     return e;
 }
