@@ -43,6 +43,10 @@ constexpr uint32_t SL = 16u; /* State dword k lives in lane SL + k of the header
 constexpr uint32_t BQ = 4u;  /* instances per work-queue batch            */
 constexpr uint32_t QN = AGNES_QUEUE_WORDS - 1u; /* work-queue counters (at most) */
 constexpr uint32_t NONE = 0xFFFFFFFFu;
+#ifndef AGNES_FAST_NT
+#define AGNES_FAST_NT 0 /* cache policy of the streamed vote/code traffic (2 = nt: slower here, the
+                            * over-fetched tail of a chunk is re-read as the next instance's start) */
+#endif
 
 /* per-wave LDS: carried u32 executors (only for instances longer than a chunk)
  * and the first-vote tables (DEDUP [2R][nv], RoundSkip [R][nv]) */
@@ -63,11 +67,12 @@ __host__ __device__ inline void layout(uint32_t mode, bool skip, bool pf, uint32
     *total = o;
 }
 
+/* the vote stream is read once: nontemporal (aux = nt) */
 __device__ __forceinline__ void glds16(const void* g, unsigned char* l) {
-    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 16, 0, AGNES_FAST_NT);
 }
 __device__ __forceinline__ void glds4(const void* g, unsigned char* l) {
-    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 4, 0, 0);
+    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 4, 0, AGNES_FAST_NT);
 }
 
 __device__ __forceinline__ uint32_t byte_of(uint32_t x, uint32_t s) { return (x >> (8u * s)) & 0xFFu; }
@@ -355,7 +360,8 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
         if (dc_at != ~0ull) {
             const uint64_t j = dc_at + 4u * lane;
             if (dc_pos == 0xFu) {
-                *reinterpret_cast<uint32_t*>(a.codes + j) = dc_code;
+                if (AGNES_FAST_NT) __builtin_nontemporal_store(dc_code, reinterpret_cast<uint32_t*>(a.codes + j));
+                else *reinterpret_cast<uint32_t*>(a.codes + j) = dc_code;
             } else {
 #pragma unroll
                 for (uint32_t s = 0; s < VPL; ++s)
@@ -610,7 +616,157 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
 #pragma unroll
                 for (uint32_t s = 0; s < VPL; ++s)
                     pend |= (uint32_t)(((acc >> s) & 1u) && (code[s] & 0xFu) != 0u) << s;
-                if (ballot(pend != 0u)) {
+                /* the payload of the changing vote (fl, fs) at chunk position `first`:
+                 * its own value, or the last value written before it in its bucket
+                 * (round_votes.rs:53) for a nil vote */
+                auto label_at = [&](uint32_t fl, uint32_t fs, uint32_t first) -> uint32_t {
+                    const uint32_t fv = rdl(sel4(x.value, fs), fl);
+                    if (fv != AGNES_NIL) return fv;
+                    const uint32_t K = rdl(sel4(x.key, fs), fl);
+                    uint32_t cand = 0;
+#pragma unroll
+                    for (uint32_t s = 0; s < VPL; ++s)
+                        cand |= (uint32_t)(x.key[s] == K && x.value[s] != AGNES_NIL && p0 + s < first) << s;
+                    const uint64_t cl = ballot(cand != 0u);
+                    if (cl) {
+                        const uint32_t hl = 63u - (uint32_t)__builtin_clzll(cl);
+                        const uint32_t hs = 31u - (uint32_t)__builtin_clz(rdl(cand, hl));
+                        return rdl(sel4(x.value, hs), hl);
+                    }
+                    /* earlier chunks of this instance, newest first: one vote per lane at
+                     * a time (rare path, few registers) */
+                    for (uint64_t pc = c; pc != c0;) {
+                        pc -= CHUNK;
+                        uint32_t hit = 0, hv = 0;
+#pragma unroll 1
+                        for (int s = (int)VPL - 1; s >= 0; --s) {
+                            const uint64_t j = pc + p0 + (uint32_t)s;
+                            if (!hit && j >= I.beg && j < I.end) {
+                                /* opaque bases: keep this rare path's address arithmetic
+                                 * from being hoisted into the chunk loop */
+                                const uint8_t *br = a.vb.round, *bt = a.vb.type;
+                                const uint32_t *bx = a.vb.validator, *bv = a.vb.value, *bi = a.vb.instance;
+                                asm volatile("" : "+s"(br), "+s"(bt), "+s"(bx), "+s"(bv), "+s"(bi));
+                                const uint32_t vr = br[j], vt = bt[j];
+                                const uint32_t vx = bx[j], vv = bv[j];
+                                bool ok = bi[j] == I.i && vr < R && vt <= 1u && vx < nv && vr * 2u + vt == K &&
+                                          vv != AGNES_NIL;
+                                if (MODE == AGNES_MODE_DEDUP && ok)
+                                    ok = first_v[K * nv + vx] == ((I.ep << lb) | (lmask - (uint32_t)(j - I.beg)));
+                                if (ok) {
+                                    hit = 1;
+                                    hv = vv;
+                                }
+                            }
+                        }
+                        const uint64_t hl = ballot(hit != 0u);
+                        if (hl) return rdl(hv, 63u - (uint32_t)__builtin_clzll(hl));
+                    }
+                    return 0u; /* unreachable in the fast domain (a nil vote at value quorum
+                                  always has a value vote before it in its bucket) */
+                };
+                /* apply the changing vote (fl, fs) on the scalar path; its message into its code */
+                auto change_at = [&](uint32_t fl, uint32_t fs) {
+                    const uint32_t fcode = rdl(sel4(code, fs), fl);
+                    const uint32_t fr = byte_of(rdl(x.r4, fl), fs);
+                    const uint32_t ev = fcode & 7u;
+                    const uint32_t lab = (ev == AGNES_CODE_POLKA_VALUE || ev == AGNES_CODE_PRECOMMIT_VALUE)
+                                             ? label_at(fl, fs, 4u * fl + fs) : 0u;
+                    const uint32_t vm = apply_change(stv, V, fcode, fr, lab);
+                    sm_changed = true;
+                    if (lane == fl) {
+#pragma unroll
+                        for (uint32_t s = 0; s < VPL; ++s)
+                            if (s == fs) code[s] |= vm << AGNES_CODE_MSG_SHIFT;
+                    }
+                };
+                if (!SKIP && ballot(pend != 0u)) {
+                    /* The vote's round never moves State.round here, so eqr is fixed per vote
+                     * and a non-changing event's message depends on two positions only:
+                     * PolkaAny at eqr -> TimeoutPrevote while the State is in Prevote (before
+                     * P1, the first change out of Prevote; vote events never re-enter it),
+                     * PrecommitAny at eqr -> TimeoutPrecommit until the commit (P2).  The
+                     * changes themselves are found lane-wise: E = the set of event indices
+                     * (event | eqr << 3) of the lane's pending votes. */
+                    uint32_t nib = 0, E = 0;
+#pragma unroll
+                    for (uint32_t s = 0; s < VPL; ++s) {
+                        const uint32_t ix = ((pend >> s) & 1u)
+                                                ? ((code[s] & 7u) | ((uint32_t)(byte_of(x.r4, s) == V.eq8) << 3)) : 0u;
+                        nib |= ix << (4u * s);
+                        E |= 1u << ix;
+                    }
+                    /* bit 16: PolkaValue at eqr whose value differs from valid.value (it
+                     * changes the State when the State is in Precommit with valid at this round) */
+                    auto mark_pv = [&]() {
+                        E &= 0xFFFFu;
+#pragma unroll
+                        for (uint32_t s = 0; s < VPL; ++s)
+                            E |= (uint32_t)(((nib >> (4u * s)) & 0xFu) == (AGNES_CODE_POLKA_VALUE | 8u) &&
+                                            x.value[s] != AGNES_NIL && x.value[s] != V.vval) << 16;
+                    };
+                    const bool prevote0 = (V.flags & 0xFFu) == AGNES_STEP_PREVOTE;
+                    uint32_t P1 = prevote0 ? CHUNK : 0u, P2 = CHUNK;
+                    uint32_t pvv = V.pvchk ? (mark_pv(), V.vval) : 0xFFFFFFFFu;
+                    int32_t pl = -1; /* last change: lane pl, vote ps */
+                    uint32_t ps = VPL - 1u;
+                    for (;;) {
+                        const uint32_t CH = V.chg | (V.pvchk ? 0x10000u : 0u);
+                        if (V.pvchk && pvv != V.vval) { /* entered Precommit-at-round or valid changed */
+                            mark_pv();
+                            pvv = V.vval;
+                        }
+                        /* first changing vote after (pl, ps): the rest of lane pl, then later lanes */
+                        uint32_t fl = 0, fs = VPL;
+                        auto scan_lane = [&](uint32_t L, uint32_t s0) {
+                            const uint32_t nl = rdl(nib, L);
+                            for (uint32_t s = s0; s < VPL; ++s) {
+                                const uint32_t ix = (nl >> (4u * s)) & 0xFu;
+                                bool ch = (CH >> ix) & 1u;
+                                if (!ch && V.pvchk && ix == (AGNES_CODE_POLKA_VALUE | 8u)) {
+                                    const uint32_t vv = rdl(sel4(x.value, s), L);
+                                    ch = vv != AGNES_NIL && vv != V.vval;
+                                }
+                                if (ch) {
+                                    fl = L;
+                                    fs = s;
+                                    return;
+                                }
+                            }
+                        };
+                        if (pl >= 0 && ps + 1u < VPL) scan_lane((uint32_t)pl, ps + 1u);
+                        if (fs == VPL) {
+                            uint64_t bk = ballot((E & CH) != 0u);
+                            if (pl >= 0) bk &= ~lanemask_le((uint32_t)pl);
+                            if (!bk) break;
+                            scan_lane((uint32_t)__builtin_ctzll(bk), 0u);
+                        }
+                        const bool was_prevote = (V.flags & 0xFFu) == AGNES_STEP_PREVOTE;
+                        change_at(fl, fs);
+                        const uint32_t pos = 4u * fl + fs;
+                        if (was_prevote && (V.flags & 0xFFu) != AGNES_STEP_PREVOTE && P1 == CHUNK) P1 = pos;
+                        if ((V.flags & 0xFFu) == AGNES_STEP_COMMIT) { /* :205 every later event: None */
+                            P2 = pos;
+                            sm_live = false;
+                            break;
+                        }
+                        pl = (int32_t)fl;
+                        ps = fs;
+                    }
+                    /* messages of the non-changing events */
+#pragma unroll
+                    for (uint32_t s = 0; s < VPL; ++s) {
+                        const uint32_t ix = (nib >> (4u * s)) & 0xFu;
+                        const uint32_t m = (ix == (AGNES_CODE_POLKA_ANY | 8u) && p0 + s < P1) ? AGNES_VMSG_TIMEOUT_PREVOTE
+                                         : (ix == (AGNES_CODE_PRECOMMIT_ANY | 8u) && p0 + s < P2) ? AGNES_VMSG_TIMEOUT_PRECOMMIT
+                                                                                                   : 0u;
+                        code[s] |= m << AGNES_CODE_MSG_SHIFT;
+                    }
+                } else if (SKIP && ballot(pend != 0u)) {
+                    /* RoundSkip moves State.round, so eqr changes with the State: each pass
+                     * classifies every pending vote against the current State (change mask and
+                     * message table indexed by event | eqr << 3), assigns the messages of the
+                     * votes before the first change and applies that change */
                     uint32_t idx[VPL];
 #pragma unroll
                     for (uint32_t s = 0; s < VPL; ++s)
@@ -623,8 +779,7 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
                             if (V.pvchk)
                                 ch |= (uint32_t)(idx[s] == (AGNES_CODE_POLKA_VALUE | 8u)) &
                                       (uint32_t)(x.value[s] != V.vval) & (uint32_t)(x.value[s] != AGNES_NIL);
-                            if (SKIP)
-                                ch |= ((code[s] >> 3) & 1u) & (uint32_t)((int32_t)byte_of(x.r4, s) > V.rlt);
+                            ch |= ((code[s] >> 3) & 1u) & (uint32_t)((int32_t)byte_of(x.r4, s) > V.rlt);
                             chb |= ch << s;
                         }
                         chb &= pend;
@@ -635,7 +790,6 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
                             fs = (uint32_t)__builtin_ctz(rdl(chb, fl));
                             first = 4u * fl + fs;
                         }
-                        /* every pending vote before the change: its message under this State */
 #pragma unroll
                         for (uint32_t s = 0; s < VPL; ++s) {
                             if (((pend >> s) & 1u) && p0 + s < first)
@@ -643,78 +797,14 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
                             if (p0 + s <= first) pend &= ~(1u << s);
                         }
                         if (!bk) break;
-                        /* the changing vote, applied on the scalar path */
-                        const uint32_t fcode = rdl(sel4(code, fs), fl);
-                        const uint32_t fr = byte_of(rdl(x.r4, fl), fs);
-                        uint32_t lab = 0;
-                        const uint32_t ev = fcode & 7u;
-                        if (ev == AGNES_CODE_POLKA_VALUE || ev == AGNES_CODE_PRECOMMIT_VALUE) {
-                            const uint32_t fv = rdl(sel4(x.value, fs), fl);
-                            if (fv != AGNES_NIL) {
-                                lab = fv;
-                            } else { /* the last value written before it in its bucket (round_votes.rs:53) */
-                                const uint32_t K = rdl(sel4(x.key, fs), fl);
-                                uint32_t cand = 0;
-#pragma unroll
-                                for (uint32_t s = 0; s < VPL; ++s)
-                                    cand |= (uint32_t)(x.key[s] == K && x.value[s] != AGNES_NIL && p0 + s < first) << s;
-                                const uint64_t cl = ballot(cand != 0u);
-                                if (cl) {
-                                    const uint32_t hl = 63u - (uint32_t)__builtin_clzll(cl);
-                                    const uint32_t hs = 31u - (uint32_t)__builtin_clz(rdl(cand, hl));
-                                    lab = rdl(sel4(x.value, hs), hl);
-                                } else { /* earlier chunks of this instance, newest first:
-                                          * one vote per lane at a time (rare path, few registers) */
-                                    for (uint64_t pc = c; pc != c0;) {
-                                        pc -= CHUNK;
-                                        uint32_t hit = 0, hv = 0;
-#pragma unroll 1
-                                        for (int s = (int)VPL - 1; s >= 0; --s) {
-                                            const uint64_t j = pc + p0 + (uint32_t)s;
-                                            if (!hit && j >= I.beg && j < I.end) {
-                                                /* opaque bases: keep the address arithmetic of this
-                                                 * rare path from being hoisted into the chunk loop */
-                                                const uint8_t *br = a.vb.round, *bt = a.vb.type;
-                                                const uint32_t *bx = a.vb.validator, *bv = a.vb.value, *bi = a.vb.instance;
-                                                asm volatile("" : "+s"(br), "+s"(bt), "+s"(bx), "+s"(bv), "+s"(bi));
-                                                const uint32_t vr = br[j], vt = bt[j];
-                                                const uint32_t vx = bx[j], vv = bv[j];
-                                                bool ok = bi[j] == I.i && vr < R && vt <= 1u && vx < nv &&
-                                                          vr * 2u + vt == K && vv != AGNES_NIL;
-                                                if (MODE == AGNES_MODE_DEDUP && ok)
-                                                    ok = first_v[K * nv + vx] ==
-                                                         ((I.ep << lb) | (lmask - (uint32_t)(j - I.beg)));
-                                                if (ok) {
-                                                    hit = 1;
-                                                    hv = vv;
-                                                }
-                                            }
-                                        }
-                                        const uint64_t hl = ballot(hit != 0u);
-                                        if (hl) {
-                                            lab = rdl(hv, 63u - (uint32_t)__builtin_clzll(hl));
-                                            break;
-                                        }
-                                    }
-                                }
-                            }
-                        }
-                        const uint32_t vm = apply_change(stv, V, fcode, fr, lab);
-                        sm_changed = true;
-                        if (lane == fl) {
-#pragma unroll
-                            for (uint32_t s = 0; s < VPL; ++s)
-                                if (s == fs) code[s] |= vm << AGNES_CODE_MSG_SHIFT;
-                        }
+                        change_at(fl, fs);
                         if ((V.flags & 0xFFu) == AGNES_STEP_COMMIT) { /* :205 every later event: None */
                             sm_live = false;
                             break;
                         }
-                        if (SKIP) {
 #pragma unroll
-                            for (uint32_t s = 0; s < VPL; ++s)
-                                idx[s] = (code[s] & 7u) | ((uint32_t)(byte_of(x.r4, s) == V.eq8) << 3);
-                        }
+                        for (uint32_t s = 0; s < VPL; ++s)
+                            idx[s] = (code[s] & 7u) | ((uint32_t)(byte_of(x.r4, s) == V.eq8) << 3);
                     }
                 }
             }
