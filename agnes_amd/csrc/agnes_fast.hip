@@ -31,29 +31,10 @@
  */
 #include <cstdlib>
 
-#include "agnes_device.h"
-#include "agnes_internal.h"
+#include "agnes_fast.h"
 
 namespace agnes {
 namespace fast {
-
-constexpr uint32_t VPL = 4;
-constexpr uint32_t CHUNK = 64u * VPL;
-constexpr uint32_t SL = 16u; /* State dword k lives in lane SL + k of the header VGPR */
-constexpr uint32_t BQ = 4u;  /* instances per work-queue batch            */
-constexpr uint32_t QN = AGNES_QUEUE_WORDS - 1u; /* work-queue counters (at most) */
-constexpr uint32_t NONE = 0xFFFFFFFFu;
-#ifndef AGNES_FAST_NT
-#define AGNES_FAST_NT 0 /* cache policy of the streamed vote/code traffic (2 = nt: slower here, the
-                            * over-fetched tail of a chunk is re-read as the next instance's start) */
-#endif
-
-/* per-wave LDS: carried u32 executors (only for instances longer than a chunk)
- * and the first-vote tables (DEDUP [2R][nv], RoundSkip [R][nv]) */
-/* LDS-DMA prefetch buffer of one chunk: instance, value, validator (1 KiB each,
- * lane l's 16 B at 16 l), round, type (256 B each, lane l's 4 B at 4 l) */
-constexpr uint32_t PF_INST = 0, PF_VALUE = 1024, PF_VAL = 2048, PF_ROUND = 3072, PF_TYPE = 3328,
-                   PF_BYTES = 3584;
 
 __host__ __device__ inline void layout(uint32_t mode, bool skip, bool pf, uint32_t R, uint32_t nv,
                                        uint32_t* o_fv, uint32_t* o_fs, uint32_t* o_pf, uint32_t* total) {
@@ -65,138 +46,6 @@ __host__ __device__ inline void layout(uint32_t mode, bool skip, bool pf, uint32
     *o_pf = o;
     if (pf) o += PF_BYTES;
     *total = o;
-}
-
-/* the vote stream is read once: nontemporal (aux = nt) */
-__device__ __forceinline__ void glds16(const void* g, unsigned char* l) {
-    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 16, 0, AGNES_FAST_NT);
-}
-__device__ __forceinline__ void glds4(const void* g, unsigned char* l) {
-    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 4, 0, AGNES_FAST_NT);
-}
-
-__device__ __forceinline__ uint32_t byte_of(uint32_t x, uint32_t s) { return (x >> (8u * s)) & 0xFFu; }
-
-/* the uniform view of the State that vote events read (state_machine.rs:196-211) */
-struct View {
-    uint32_t flags; /* State dword 13: step | locked << 8 | valid << 16 | decided << 24 */
-    uint32_t eq8;   /* State.round when in [0, 255], else 0x100 (no u8 vote round equals it) */
-    int32_t rlt;    /* clamp(State.round, -1, 256): u8 round r > rlt <=> State.round < r     */
-    uint32_t vval;  /* valid.value                                                           */
-    uint32_t vsame; /* valid == Some{round: State.round, ..}                                 */
-    uint32_t chg;   /* bit idx: the event changes the State (idx = event | eqr << 3)          */
-    uint32_t mt;    /* 2-bit message of a non-changing event at idx (1 TimeoutPrevote, 2 TimeoutPrecommit) */
-    uint32_t pvchk; /* Precommit with valid at this round: PolkaValue changes iff its value differs */
-};
-
-__device__ __forceinline__ int64_t lanes64(uint32_t stv, uint32_t k) {
-    return (int64_t)(((uint64_t)rdl(stv, SL + k + 1u) << 32) | rdl(stv, SL + k));
-}
-
-__device__ __forceinline__ void view_tables(View& v) {
-    const uint32_t step = v.flags & 0xFFu;
-    v.chg = (1u << AGNES_CODE_PRECOMMIT_VALUE) | (1u << (AGNES_CODE_PRECOMMIT_VALUE | 8u)); /* :211 */
-    v.mt = 2u << (2u * (AGNES_CODE_PRECOMMIT_ANY | 8u));                                       /* :208 */
-    v.pvchk = 0;
-    if (step == AGNES_STEP_PREVOTE) { /* :196-199 */
-        v.chg |= (1u << (AGNES_CODE_POLKA_NIL | 8u)) | (1u << (AGNES_CODE_POLKA_VALUE | 8u));
-        v.mt |= 1u << (2u * (AGNES_CODE_POLKA_ANY | 8u));
-    } else if (step == AGNES_STEP_PRECOMMIT) { /* :202 set_valid_value */
-        if (v.vsame) v.pvchk = 1;
-        else v.chg |= 1u << (AGNES_CODE_POLKA_VALUE | 8u);
-    }
-}
-
-__device__ __forceinline__ void view_round(View& v, int64_t round, uint32_t stv) {
-    v.eq8 = (round >= 0 && round <= 255) ? (uint32_t)round : 0x100u;
-    v.rlt = round < -1 ? -1 : (round > 256 ? 256 : (int32_t)round);
-    v.vsame = ((v.flags >> 16) & 0xFFu) != 0u && lanes64(stv, 6) == round;
-}
-
-__device__ __forceinline__ View view_of(uint32_t stv) {
-    View v;
-    v.flags = rdl(stv, SL + 13u);
-    v.vval = rdl(stv, SL + 11u);
-    view_round(v, lanes64(stv, 2), stv);
-    view_tables(v);
-    return v;
-}
-
-/* Apply one state-changing vote event (RoundSkip first, then the tally event at
- * the vote's round; state_machine.rs:196-211 via consensus_executor.rs:64-68)
- * to the State lanes; returns the message nibble.  Mirrors sm_vote in
- * agnes_kernels.hip. */
-__device__ __forceinline__ uint32_t apply_change(uint32_t& stv, View& v, uint32_t code, uint32_t r,
-                                                 uint32_t lab) {
-    uint32_t step = v.flags & 0xFFu;
-    bool nr = false;
-    if ((code & AGNES_CODE_SKIP) && (int32_t)r > v.rlt) { /* :210 round_skip(s, r) */
-        stv = wrl<SL + 2u>(stv, r);
-        stv = wrl<SL + 3u>(stv, 0u);
-        step = AGNES_STEP_NEW_ROUND;
-        view_round(v, (int64_t)r, stv);
-        nr = true;
-    }
-    const bool eqr = r == v.eq8;
-    uint32_t b = AGNES_VMSG_NONE;
-    switch (code & AGNES_CODE_EVENT_MASK) {
-    case AGNES_CODE_POLKA_ANY: /* :196 */
-        if (eqr && step == AGNES_STEP_PREVOTE) b = AGNES_VMSG_TIMEOUT_PREVOTE;
-        break;
-    case AGNES_CODE_POLKA_NIL: /* :197 */
-        if (eqr && step == AGNES_STEP_PREVOTE) {
-            step = AGNES_STEP_PRECOMMIT;
-            b = AGNES_VMSG_PRECOMMIT_NIL;
-        }
-        break;
-    case AGNES_CODE_POLKA_VALUE:
-        if (eqr && (step == AGNES_STEP_PREVOTE || step == AGNES_STEP_PRECOMMIT)) {
-            const uint32_t rl = rdl(stv, SL + 2u), rh = rdl(stv, SL + 3u);
-            if (step == AGNES_STEP_PREVOTE) { /* :198 precommit: locked = valid = {round, v} */
-                stv = wrl<SL + 4u>(stv, rl);
-                stv = wrl<SL + 5u>(stv, rh);
-                stv = wrl<SL + 10u>(stv, lab);
-                v.flags = (v.flags & ~0xFF00u) | 0x100u;
-                step = AGNES_STEP_PRECOMMIT;
-                b = AGNES_VMSG_PRECOMMIT_VALUE;
-            }
-            stv = wrl<SL + 6u>(stv, rl); /* :202 set_valid_value */
-            stv = wrl<SL + 7u>(stv, rh);
-            stv = wrl<SL + 11u>(stv, lab);
-            v.flags = (v.flags & ~0xFF0000u) | 0x10000u;
-            v.vval = lab;
-            v.vsame = 1;
-        }
-        break;
-    case AGNES_CODE_PRECOMMIT_ANY: /* :208 */
-        if (eqr) b = AGNES_VMSG_TIMEOUT_PRECOMMIT;
-        break;
-    case AGNES_CODE_PRECOMMIT_VALUE: /* :211 commit */
-        step = AGNES_STEP_COMMIT;
-        v.flags = (v.flags & 0x00FFFFFFu) | 0x01000000u;
-        stv = wrl<SL + 8u>(stv, r);
-        stv = wrl<SL + 9u>(stv, 0u);
-        stv = wrl<SL + 12u>(stv, lab);
-        b = AGNES_VMSG_DECISION;
-        break;
-    default:
-        break;
-    }
-    v.flags = (v.flags & ~0xFFu) | step;
-    stv = wrl<SL + 13u>(stv, v.flags);
-    view_tables(v);
-    if (nr) return b == AGNES_VMSG_TIMEOUT_PRECOMMIT ? AGNES_VMSG_NEW_ROUND_TIMEOUT_PRECOMMIT
-                 : b == AGNES_VMSG_DECISION           ? AGNES_VMSG_NEW_ROUND_DECISION
-                                                      : AGNES_VMSG_NEW_ROUND;
-    return b;
-}
-
-template <typename T>
-__device__ __forceinline__ T sel4(const T (&x)[VPL], uint32_t s) { /* s wave-uniform */
-    if (s == 0) return x[0];
-    if (s == 1) return x[1];
-    if (s == 2) return x[2];
-    return x[3];
 }
 
 /* uniform facts of the instance being tallied */
@@ -295,7 +144,8 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
     auto load_chunk = [&](const Inst& I, uint64_t c, Chunk& x, uint32_t (&val)[VPL], uint32_t& t4) {
         const uint64_t j = c + 4u * lane;
         uint32_t inst[VPL];
-        if (PF && pf_at == c) { /* prefetched by LDS-DMA (the compiler waits vmcnt for it) */
+        if (PF && pf_at == c) { /* prefetched by LDS-DMA */
+            dma_wait();
             const uint4 ia = *reinterpret_cast<const uint4*>(pfb + PF_INST + 16u * lane);
             const uint4 va = *reinterpret_cast<const uint4*>(pfb + PF_VALUE + 16u * lane);
             const uint4 da = *reinterpret_cast<const uint4*>(pfb + PF_VAL + 16u * lane);
@@ -483,6 +333,12 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
             /* first-vote tables: atomic max of (epoch << lb | LMASK - local index), so
              * the earliest vote of the instance wins (DEDUP: per (round, type,
              * validator); RoundSkip: per (round, validator)) */
+            if (a.dbg & 1u) { /* development knob (AGNES_DEBUG_SKIP=1): memory traffic only */
+                dc_code = (x.value[0] ^ x.key[1] ^ w[2] ^ w[3] ^ x.r4) & 0x07070707u;
+                dc_pos = x.pos;
+                dc_at = c;
+                continue;
+            }
             uint32_t acc = x.ok, sfirst = 0;
             if (TABLES) {
                 const uint32_t loc0 = (uint32_t)(c - I.beg) + p0;
@@ -612,6 +468,9 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
 
             /* K4: State::apply(v.round, event) in stream order (consensus_executor.rs:64-68) */
             if (SM && sm_live) {
+                /* fresh copies: keep the compiler from carrying per-vote values derived
+                 * before the slot loop (round bytes, nil tests) across it for this stage */
+                asm volatile("" : "+v"(x.r4), "+v"(x.value[0]), "+v"(x.value[1]), "+v"(x.value[2]), "+v"(x.value[3]));
                 uint32_t pend = 0;
 #pragma unroll
                 for (uint32_t s = 0; s < VPL; ++s)
@@ -682,85 +541,55 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
                 };
                 if (!SKIP && ballot(pend != 0u)) {
                     /* The vote's round never moves State.round here, so eqr is fixed per vote
-                     * and a non-changing event's message depends on two positions only:
-                     * PolkaAny at eqr -> TimeoutPrevote while the State is in Prevote (before
-                     * P1, the first change out of Prevote; vote events never re-enter it),
-                     * PrecommitAny at eqr -> TimeoutPrecommit until the commit (P2).  The
-                     * changes themselves are found lane-wise: E = the set of event indices
-                     * (event | eqr << 3) of the lane's pending votes. */
-                    uint32_t nib = 0, E = 0;
-#pragma unroll
-                    for (uint32_t s = 0; s < VPL; ++s) {
-                        const uint32_t ix = ((pend >> s) & 1u)
-                                                ? ((code[s] & 7u) | ((uint32_t)(byte_of(x.r4, s) == V.eq8) << 3)) : 0u;
-                        nib |= ix << (4u * s);
-                        E |= 1u << ix;
-                    }
-                    /* bit 16: PolkaValue at eqr whose value differs from valid.value (it
-                     * changes the State when the State is in Precommit with valid at this round) */
-                    auto mark_pv = [&]() {
-                        E &= 0xFFFFu;
-#pragma unroll
-                        for (uint32_t s = 0; s < VPL; ++s)
-                            E |= (uint32_t)(((nib >> (4u * s)) & 0xFu) == (AGNES_CODE_POLKA_VALUE | 8u) &&
-                                            x.value[s] != AGNES_NIL && x.value[s] != V.vval) << 16;
+                     * and vote events drive a tiny automaton: Prevote --PolkaNil/PolkaValue at
+                     * eqr--> Precommit --PolkaValue at eqr with another value--> Precommit
+                     * (valid), any step --PrecommitValue--> Commit.  Every change is found as
+                     * the first set bit of per-sub-vote ballots (lane l, vote s = position
+                     * 4l + s) restricted to a position window; the non-changing messages are
+                     * PolkaAny at eqr -> TimeoutPrevote before the State leaves Prevote (P1)
+                     * and PrecommitAny at eqr -> TimeoutPrecommit before the commit (PC). */
+                    /* event of vote s with the eqr bit (event | eqr << 3); 6/7 (invalid /
+                     * rejected) match nothing below */
+                    auto ev_of = [&](uint32_t s) -> uint32_t {
+                        return (code[s] & 7u) | ((uint32_t)(byte_of(x.r4, s) == V.eq8) << 3);
                     };
+                    /* one change per pass: the first PrecommitValue (commit), and before it
+                     * the first vote that moves the current step (Prevote: PolkaNil /
+                     * PolkaValue at eqr; Precommit: PolkaValue at eqr with another value) */
                     const bool prevote0 = (V.flags & 0xFFu) == AGNES_STEP_PREVOTE;
-                    uint32_t P1 = prevote0 ? CHUNK : 0u, P2 = CHUNK;
-                    uint32_t pvv = V.pvchk ? (mark_pv(), V.vval) : 0xFFFFFFFFu;
-                    int32_t pl = -1; /* last change: lane pl, vote ps */
-                    uint32_t ps = VPL - 1u;
+                    uint32_t P1 = prevote0 ? CHUNK : 0u, pc = CHUNK, lo = 0;
                     for (;;) {
-                        const uint32_t CH = V.chg | (V.pvchk ? 0x10000u : 0u);
-                        if (V.pvchk && pvv != V.vval) { /* entered Precommit-at-round or valid changed */
-                            mark_pv();
-                            pvv = V.vval;
+                        const uint32_t step = V.flags & 0xFFu;
+                        uint64_t b[VPL];
+#pragma unroll
+                        for (uint32_t s = 0; s < VPL; ++s) {
+                            const uint32_t ix = ev_of(s);
+                            const bool pv = ix == (AGNES_CODE_POLKA_VALUE | 8u);
+                            const bool mv = step == AGNES_STEP_PREVOTE
+                                                ? (pv || ix == (AGNES_CODE_POLKA_NIL | 8u))
+                                                : (step == AGNES_STEP_PRECOMMIT && pv &&
+                                                   (!V.vsame || (x.value[s] != AGNES_NIL && x.value[s] != V.vval)));
+                            b[s] = ballot(mv || (ix & 7u) == AGNES_CODE_PRECOMMIT_VALUE);
                         }
-                        /* first changing vote after (pl, ps): the rest of lane pl, then later lanes */
-                        uint32_t fl = 0, fs = VPL;
-                        auto scan_lane = [&](uint32_t L, uint32_t s0) {
-                            const uint32_t nl = rdl(nib, L);
-                            for (uint32_t s = s0; s < VPL; ++s) {
-                                const uint32_t ix = (nl >> (4u * s)) & 0xFu;
-                                bool ch = (CH >> ix) & 1u;
-                                if (!ch && V.pvchk && ix == (AGNES_CODE_POLKA_VALUE | 8u)) {
-                                    const uint32_t vv = rdl(sel4(x.value, s), L);
-                                    ch = vv != AGNES_NIL && vv != V.vval;
-                                }
-                                if (ch) {
-                                    fl = L;
-                                    fs = s;
-                                    return;
-                                }
-                            }
-                        };
-                        if (pl >= 0 && ps + 1u < VPL) scan_lane((uint32_t)pl, ps + 1u);
-                        if (fs == VPL) {
-                            uint64_t bk = ballot((E & CH) != 0u);
-                            if (pl >= 0) bk &= ~lanemask_le((uint32_t)pl);
-                            if (!bk) break;
-                            scan_lane((uint32_t)__builtin_ctzll(bk), 0u);
-                        }
-                        const bool was_prevote = (V.flags & 0xFFu) == AGNES_STEP_PREVOTE;
-                        change_at(fl, fs);
-                        const uint32_t pos = 4u * fl + fs;
-                        if (was_prevote && (V.flags & 0xFFu) != AGNES_STEP_PREVOTE && P1 == CHUNK) P1 = pos;
-                        if ((V.flags & 0xFFu) == AGNES_STEP_COMMIT) { /* :205 every later event: None */
-                            P2 = pos;
+                        const uint32_t f = first_of(b, lo, CHUNK);
+                        if (f >= CHUNK) break;
+                        change_at(f >> 2, f & 3u);
+                        if (step == AGNES_STEP_PREVOTE && P1 == CHUNK) P1 = f; /* left Prevote */
+                        if ((V.flags & 0xFFu) == AGNES_STEP_COMMIT) { /* :211; :205 every later event: None */
+                            pc = f;
                             sm_live = false;
                             break;
                         }
-                        pl = (int32_t)fl;
-                        ps = fs;
+                        lo = f + 1u;
                     }
                     /* messages of the non-changing events */
 #pragma unroll
                     for (uint32_t s = 0; s < VPL; ++s) {
-                        const uint32_t ix = (nib >> (4u * s)) & 0xFu;
-                        const uint32_t m = (ix == (AGNES_CODE_POLKA_ANY | 8u) && p0 + s < P1) ? AGNES_VMSG_TIMEOUT_PREVOTE
-                                         : (ix == (AGNES_CODE_PRECOMMIT_ANY | 8u) && p0 + s < P2) ? AGNES_VMSG_TIMEOUT_PRECOMMIT
-                                                                                                   : 0u;
-                        code[s] |= m << AGNES_CODE_MSG_SHIFT;
+                        const uint32_t ix = ev_of(s);
+                        const bool m1 = ix == (AGNES_CODE_POLKA_ANY | 8u) && ((win(s, 0u, P1) >> lane) & 1u);
+                        const bool m2 = ix == (AGNES_CODE_PRECOMMIT_ANY | 8u) && ((win(s, 0u, pc) >> lane) & 1u);
+                        code[s] |= (m1 ? AGNES_VMSG_TIMEOUT_PREVOTE : (m2 ? AGNES_VMSG_TIMEOUT_PRECOMMIT : 0u))
+                                   << AGNES_CODE_MSG_SHIFT;
                     }
                 } else if (SKIP && ballot(pend != 0u)) {
                     /* RoundSkip moves State.round, so eqr changes with the State: each pass

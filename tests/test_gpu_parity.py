@@ -368,6 +368,53 @@ def test_early_quorum_labels(eng, mode, flags):
     assert_same(g, o)
 
 
+@pytest.mark.parametrize("stream", ["1", "2"])  # 2: the State machine on the stream kernel too
+@pytest.mark.parametrize("flags", [0, abi.FLAG_STATE_MACHINE])
+@pytest.mark.parametrize("lengths", [
+    [0, 4, 8, 12, 60, 64, 68, 200, 252, 256, 260, 300, 516],   # lane-aligned: stream batches
+    [4, 8, 12, 16, 20, 24, 28, 32],                            # many segments per chunk
+    [200], [300, 600, 900, 1200]])                             # C2 / C3 shapes
+def test_stream_segments(eng, monkeypatch, stream, flags, lengths):
+    """Instance lengths that are multiples of 4 make every batch a vote stream
+    whose chunks straddle instances (agnes_stream.hip): segments, per-segment
+    thresholds and carries, per-segment State::apply, several power sets."""
+    if stream == "2" and not flags:
+        pytest.skip("same launch as stream=1 without the State machine")
+    monkeypatch.setenv("AGNES_STREAM", stream)
+    hb = _ragged_batch(31 + len(lengths), 6000, 17, 3, lengths)
+    power = ol.gen_power(3, 5, 17, abi.POWER_UNIFORM, 1, 50)
+    hb.instance_set = (np.arange(hb.n_instances) * 7 % 5).astype(np.uint32)
+    cfg = abi.config(abi.MODE_REFERENCE, flags, 3)
+    st = _start_states(hb.n_instances) if flags & abi.FLAG_STATE_MACHINE else None
+    g, o = run_both(eng, cfg, hb, power, None, st)
+    assert_same(g, o)
+    assert (g[0] & abi.CODE_EVENT_MASK != 0).any()
+
+
+@pytest.mark.parametrize("name", ["c2_sm", "c3_small", "c4_small"])
+def test_stream_state_machine_generated(eng, monkeypatch, name):
+    """The generated configs with the State machine forced onto the stream
+    kernel (AGNES_STREAM=2); c4 (RoundSkip) stays on the per-instance kernel."""
+    monkeypatch.setenv("AGNES_STREAM", "2")
+    p, hb, power, cfg = _make(name)
+    states = _start_states(p.n_instances) if cfg.flags & abi.FLAG_STATE_MACHINE else None
+    g, o = run_both(eng, cfg, hb, power, None, states)
+    assert_same(g, o)
+
+
+def test_stream_mixed_domains(eng):
+    """Lane-aligned batches with instances outside the stream domain (i64 powers
+    for some sets; an instance_set beyond n_sets): those batches run instance by
+    instance, the out-of-domain instances on the i64 kernel."""
+    hb = _ragged_batch(77, 4000, 11, 2, [0, 8, 40, 96, 200])
+    power = ol.gen_power(7, 4, 11, abi.POWER_UNIFORM, 1, 30)
+    power[3, :] = (1 << 40)  # set 3 needs i64 sums
+    hb.instance_set = (np.arange(hb.n_instances) % 5).astype(np.uint32)  # set 4 does not exist
+    cfg = abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 2)
+    g, o = run_both(eng, cfg, hb, power, None, _start_states(hb.n_instances))
+    assert_same(g, o)
+
+
 def test_epoch_table_recycling(eng, monkeypatch):
     """DEDUP/RoundSkip tables tag entries with per-instance epochs; with few
     epoch bits the tables are cleared every 3 instances (chunks cut there)."""
