@@ -1,0 +1,348 @@
+/*
+ * agnes_apply.hip — batched State::apply over a tallied vote stream, one
+ * instance per lane (K4 of the hot path; consensus_executor.rs:64-68 ->
+ * state_machine.rs:196-211 for the events a vote can produce).
+ *
+ * The tally kernels leave one code byte per vote (event bits 0..2, RoundSkip bit
+ * 3).  This pass walks each instance's codes in stream order and ORs the message
+ * nibble (bits 4..7) into the votes that produce one, and leaves the final State.
+ *
+ * What makes it a light pass: the message of a vote depends only on (event,
+ * vote round == State.round, step), never on the event's value.  Values matter
+ * only for the State fields written at three places — the Prevote -> Precommit
+ * PolkaValue (locked = valid = {round, v}, :198), the last set_valid_value
+ * (:202: later writes overwrite earlier ones and emit nothing) and the commit
+ * (:211).  The walk records those vote positions and resolves their values
+ * afterwards (the vote's value, or for a nil vote the last value written into
+ * its bucket before it: round_votes.rs:50-54), so the loop streams 2 B per vote
+ * (code, round) and writes back only the bytes that gain a message.
+ *
+ * Instances the tally kernel deferred to the i64 LIST kernel (sums may reach
+ * 2^31) are skipped here: that kernel applies their events itself.
+ */
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "agnes_device.h"
+#include "agnes_fast.h"
+#include "agnes_internal.h"
+
+namespace agnes {
+namespace apply {
+
+constexpr uint32_t NOPOS = 0xFFFFFFFFu;
+
+/* Each lane walks its instance in 64-B blocks of the code and round columns,
+ * fetched by LDS-DMA into lane-private slots (4 x 16 B per column, double
+ * buffered): a block is one half of an L2 line, consumed before the next block
+ * is needed, so a line is fetched once although the 64 lanes of a wave read 64
+ * different lines.  LDS per wave: [stage 2][column 2][k 4][lane 64][16 B]. */
+constexpr uint32_t BLK = 64u, LDS_PER_WAVE = 2u * 2u * 4u * 64u * 16u, WAVES = 4u;
+
+/* the bytes of a 16-B window that runs past the batch end, into the lane's slot
+ * (the batch's last instance only) */
+__device__ __attribute__((noinline)) void tail_fill(const uint8_t* col, uint64_t w, uint64_t NV, unsigned char* slot) {
+    uint32_t o[4] = {0, 0, 0, 0};
+    for (uint32_t b = 0; b < 16u && w + b < NV; ++b) o[b >> 2] |= (uint32_t)col[w + b] << (8u * (b & 3u));
+    *reinterpret_cast<uint4*>(slot) = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+/* 0xFF in byte i of the result for bit i of x (x < 16) */
+__device__ __forceinline__ uint32_t bytes_of(uint32_t x) {
+    const uint32_t b = (x * 0x00204081u) & 0x01010101u;
+    return (b << 8) - b;
+}
+/* 0xFF in the bytes of x that are zero (exact, no borrow) */
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
+    const uint32_t t = (x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+    const uint32_t z = ~(t | x) & 0x80808080u;
+    return z | (z - (z >> 7));
+}
+/* 0x01 in the bytes of x greater than k (-1 <= k <= 254) */
+__device__ __forceinline__ uint32_t bytes_gt(uint32_t x, int32_t k) {
+    const uint32_t c = (uint32_t)(255 - k) * 0x00010001u; /* byte + 255 - k carries into bit 8 iff byte > k */
+    const uint32_t te = (x & 0x00FF00FFu) + c, to = ((x >> 8) & 0x00FF00FFu) + c;
+    return ((te >> 8) & 0x00010001u) | (to & 0x01000100u);
+}
+
+/* Per-byte lookup tables over the event (bits 0..2 of a code), one per eqr:
+ * bits 4..7 the message of a non-changing event, bit 0 CHG (the vote changes the
+ * step: PolkaNil / PolkaValue at eqr in Prevote, PrecommitValue anywhere), bit 1
+ * VUPD (PolkaValue at eqr in Precommit: set_valid_value, no message).  Table
+ * bytes 0..3 in lo, 4..7 in hi (v_perm_b32 selectors 0..7). */
+constexpr uint32_t CHG = 0x01u, VUPD = 0x02u;
+constexpr uint32_t T0LO = 0u, T0HI = CHG << 8; /* not eqr: PrecommitValue commits (:211) */
+constexpr uint32_t T1HI = (AGNES_VMSG_TIMEOUT_PRECOMMIT << 4) | (CHG << 8); /* PrecommitAny :208, PrecommitValue */
+__device__ __forceinline__ uint32_t t1lo_of(uint32_t step) {
+    return step == AGNES_STEP_PREVOTE ? ((AGNES_VMSG_TIMEOUT_PREVOTE << 4) << 8) | (CHG << 16) | ((CHG | VUPD) << 24)
+         : step == AGNES_STEP_PRECOMMIT ? (VUPD << 24)
+                                        : 0u;
+}
+
+/* the value a Value event at vote j carries: the vote's own, or (nil vote) the last
+ * value counted into its (round, type) bucket before it, 0 if none (VoteCount::new
+ * label; one value slot, last writer wins: round_votes.rs:36-54) */
+__device__ uint32_t label_of(const agnes_tally_args& a, uint64_t lo, uint64_t j) {
+    if (a.dbg & 16u) return 0u; /* development knob 16: no label reads */
+    const uint32_t v = a.vb.value[j];
+    if (v != AGNES_NIL) return v;
+    const uint8_t r = a.vb.round[j], t = a.vb.type[j];
+    for (uint64_t k = j; k-- > lo;) {
+        const uint32_t ev = a.codes[k] & AGNES_CODE_EVENT_MASK;
+        if (a.vb.round[k] == r && a.vb.type[k] == t && ev != AGNES_CODE_INVALID && ev != AGNES_CODE_REJECTED) {
+            const uint32_t u = a.vb.value[k];
+            if (u != AGNES_NIL) return u;
+        }
+    }
+    return 0u;
+}
+
+template <bool SKIP>
+__global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = a.vb.n_instances, ns = a.n_sets;
+    if (i >= n) return;
+    const uint64_t NV = a.vb.n_votes;
+    uint64_t lo = a.vb.offsets[i], hi = a.vb.offsets[i + 1u];
+    lo = lo < NV ? lo : NV;
+    hi = hi < NV ? hi : NV;
+    if (hi <= lo) return;
+    /* the same u32-domain test as the tally kernels: the rest is the LIST kernel's */
+    const uint32_t set = a.vb.instance_set ? a.vb.instance_set[i] : (ns ? i % ns : 0u);
+    if (set < ns) {
+        const agnes_set_info si = a.sets[set];
+        const uint64_t len = hi - lo;
+        if (!si.fast || len >= (1ull << 32) || len * (uint64_t)si.maxpow >= (1ull << 31)) return;
+    }
+
+    uint4* const sp = reinterpret_cast<uint4*>(a.states + i);
+    const uint4 s3 = sp[3];
+    const uint32_t step0 = s3.y & 0xFFu; /* dword 13: step | locked << 8 | valid << 16 | decided << 24 */
+    if (step0 == AGNES_STEP_COMMIT) return; /* :205 every later event: None */
+    const uint4 s0 = sp[0];
+    const int64_t round0 = (int64_t)(((uint64_t)s0.w << 32) | s0.z);
+    uint32_t step = step0;
+    uint32_t eq8 = (round0 >= 0 && round0 <= 255) ? (uint32_t)round0 : 0x100u; /* no u8 round equals 0x100 */
+    int32_t rlt = round0 < -1 ? -1 : (round0 > 256 ? 256 : (int32_t)round0);
+    bool skipped = false;
+    /* the positions (relative to lo) whose values the State takes */
+    uint32_t lock_at = NOPOS, valid_at = NOPOS, dec_at = NOPOS, dec_round = 0;
+
+    /* one 16-B window at w of this instance (cq, rq: its code and round bytes) */
+    auto walk = [&](uint64_t w, uint4 cq, uint4 rq) {
+        const uint32_t c4[4] = {cq.x, cq.y, cq.z, cq.w}, r4[4] = {rq.x, rq.y, rq.z, rq.w};
+        const int32_t rel = (int32_t)((int64_t)w - (int64_t)lo); /* > -16 */
+        const uint32_t a0 = rel < 0 ? (uint32_t)(-rel) : 0u;
+        const uint64_t rem = hi - w;
+        const uint32_t a1 = rem < 16u ? (uint32_t)rem : 16u;
+        uint32_t allowed = ((1u << a1) - 1u) & ~((1u << a0) - 1u); /* bytes of this instance not yet walked */
+        uint32_t ow[4] = {c4[0], c4[1], c4[2], c4[3]};
+        /* one pass per step change inside the window (at most a few per instance) */
+        for (;;) {
+            const uint32_t t1lo = eq8 < 0x100u ? t1lo_of(step) : T0LO;
+            const uint32_t t1hi = eq8 < 0x100u ? T1HI : T0HI;
+            const uint32_t eqrep = (eq8 & 0xFFu) * 0x01010101u;
+            uint32_t o[4], any_c = 0, any_v = 0;
+#pragma unroll
+            for (uint32_t d = 0; d < 4u; ++d) {
+                const uint32_t e = c4[d] & 0x07070707u;
+                const uint32_t q = zero_bytes(r4[d] ^ eqrep);
+                uint32_t od = (__builtin_amdgcn_perm(t1hi, t1lo, e) & q) | (__builtin_amdgcn_perm(T0HI, T0LO, e) & ~q);
+                if (SKIP) od |= (c4[d] >> 3) & bytes_gt(r4[d], rlt); /* RoundSkip to a higher round: CHG */
+                od &= bytes_of((allowed >> (4u * d)) & 0xFu);
+                o[d] = od;
+                any_c |= od & 0x01010101u;
+                any_v |= od & 0x02020202u;
+            }
+            uint32_t fb = 16u; /* first changing byte */
+            if (any_c) {
+#pragma unroll
+                for (int d = 3; d >= 0; --d) {
+                    const uint32_t m = o[d] & 0x01010101u;
+                    if (m) fb = 4u * (uint32_t)d + ((uint32_t)__builtin_ctz(m) >> 3);
+                }
+            }
+            const uint32_t before = fb < 16u ? (1u << fb) - 1u : 0xFFFFu;
+            /* messages of the bytes before it; the last set_valid_value among them */
+#pragma unroll
+            for (uint32_t d = 0; d < 4u; ++d) ow[d] |= o[d] & 0xF0F0F0F0u & bytes_of((before >> (4u * d)) & 0xFu);
+            if (any_v) {
+#pragma unroll
+                for (uint32_t d = 0; d < 4u; ++d) {
+                    const uint32_t m = o[d] & 0x02020202u & bytes_of((before >> (4u * d)) & 0xFu);
+                    if (m) valid_at = (uint32_t)(rel + (int32_t)(4u * d + ((31u - (uint32_t)__builtin_clz(m)) >> 3)));
+                }
+            }
+            if (fb >= 16u) break;
+            /* the changing vote (state_machine.rs:196-211 via sm_vote's arms) */
+            const uint32_t sh = 8u * (fb & 3u);
+            const uint32_t cdw = fb < 8u ? (fb < 4u ? c4[0] : c4[1]) : (fb < 12u ? c4[2] : c4[3]);
+            const uint32_t rdw = fb < 8u ? (fb < 4u ? r4[0] : r4[1]) : (fb < 12u ? r4[2] : r4[3]);
+            const uint32_t c = (cdw >> sh) & 0xFFu, r = (rdw >> sh) & 0xFFu;
+            const uint32_t jo = (uint32_t)(rel + (int32_t)fb);
+            bool nr = false;
+            if (SKIP && (c & AGNES_CODE_SKIP) && (int32_t)r > rlt) { /* :210 round_skip(s, r) */
+                eq8 = r;
+                rlt = (int32_t)r;
+                step = AGNES_STEP_NEW_ROUND;
+                skipped = true;
+                nr = true;
+            }
+            const uint32_t ev = c & AGNES_CODE_EVENT_MASK;
+            const bool eqr = r == eq8;
+            uint32_t m = AGNES_VMSG_NONE;
+            if (ev == AGNES_CODE_POLKA_ANY && eqr && step == AGNES_STEP_PREVOTE) {
+                m = AGNES_VMSG_TIMEOUT_PREVOTE; /* :196 */
+            } else if (ev == AGNES_CODE_POLKA_NIL && eqr && step == AGNES_STEP_PREVOTE) { /* :197 */
+                m = AGNES_VMSG_PRECOMMIT_NIL;
+                step = AGNES_STEP_PRECOMMIT;
+            } else if (ev == AGNES_CODE_POLKA_VALUE && eqr && step == AGNES_STEP_PREVOTE) {
+                m = AGNES_VMSG_PRECOMMIT_VALUE; /* :198 precommit: locked = valid = {round, v} */
+                step = AGNES_STEP_PRECOMMIT;
+                lock_at = valid_at = jo;
+            } else if (ev == AGNES_CODE_POLKA_VALUE && eqr && step == AGNES_STEP_PRECOMMIT) {
+                valid_at = jo; /* :202 */
+            } else if (ev == AGNES_CODE_PRECOMMIT_ANY && eqr) {
+                m = AGNES_VMSG_TIMEOUT_PRECOMMIT; /* :208 */
+            } else if (ev == AGNES_CODE_PRECOMMIT_VALUE) {
+                m = AGNES_VMSG_DECISION; /* :211 commit */
+                step = AGNES_STEP_COMMIT;
+                dec_at = jo;
+                dec_round = r;
+            }
+            if (SKIP && nr)
+                m = m == AGNES_VMSG_TIMEOUT_PRECOMMIT ? AGNES_VMSG_NEW_ROUND_TIMEOUT_PRECOMMIT
+                  : m == AGNES_VMSG_DECISION           ? AGNES_VMSG_NEW_ROUND_DECISION
+                                                       : AGNES_VMSG_NEW_ROUND;
+#pragma unroll
+            for (uint32_t d = 0; d < 4u; ++d) ow[d] |= (d == (fb >> 2)) ? (m << (sh + AGNES_CODE_MSG_SHIFT)) : 0u;
+            allowed &= ~((2u << fb) - 1u);
+            if (step == AGNES_STEP_COMMIT || !allowed) break;
+        }
+        if ((ow[0] ^ c4[0]) | (ow[1] ^ c4[1]) | (ow[2] ^ c4[2]) | (ow[3] ^ c4[3])) {
+            /* whole window when it is all this instance's, else its changed bytes only */
+            if (rel >= 0 && rem >= 16u) {
+                *reinterpret_cast<uint4*>(a.codes + w) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+            } else {
+                for (uint32_t b = 0; b < 16u; ++b) {
+                    const uint32_t x = (ow[b >> 2] >> (8u * (b & 3u))) & 0xFFu;
+                    if (x != ((c4[b >> 2] >> (8u * (b & 3u))) & 0xFFu)) a.codes[w + b] = (uint8_t)x;
+                }
+            }
+        }
+    };
+
+    /* the lane's 64-B blocks by LDS-DMA; a window past the batch end is clamped to
+     * an in-bounds one (16 <= NV: the launcher) and filled byte-wise after the wait */
+    const uint32_t lane = threadIdx.x & 63u;
+    unsigned char* const wbase = agnes_smem + rfl(threadIdx.x >> 6) * LDS_PER_WAVE; /* wave-uniform: m0 */
+    const uint64_t wmax = (NV & ~15ull) - 16u; /* the last window fully inside [0, NV) */
+    auto issue = [&](uint32_t stg, uint64_t blk) {
+#pragma unroll
+        for (uint32_t k = 0; k < 4u; ++k) {
+            const uint64_t w = blk + 16u * k;
+            const uint64_t ws = w <= wmax ? w : wmax;
+            fast::glds16(a.codes + ws, wbase + ((stg * 2u + 0u) * 4u + k) * 1024u);
+            fast::glds16(a.vb.round + ws, wbase + ((stg * 2u + 1u) * 4u + k) * 1024u);
+        }
+    };
+    uint64_t blk = lo & ~(uint64_t)(BLK - 1u);
+    uint32_t stg = 0;
+    issue(0u, blk);
+    for (;;) {
+        const uint64_t nb = blk + BLK;
+        const bool more = nb < hi;
+        const bool any_more = __builtin_amdgcn_ballot_w64(more) != 0ull;
+        if (more) issue(stg ^ 1u, nb);
+        /* this block's DMA: everything but the (wave-level) 8 just issued */
+        if (any_more) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else fast::dma_wait();
+#pragma unroll 1
+        for (uint32_t k = 0; k < 4u; ++k) {
+            const uint64_t w = blk + 16u * k;
+            if (w >= hi) break;
+            unsigned char* const cs = wbase + ((stg * 2u + 0u) * 4u + k) * 1024u + 16u * lane;
+            unsigned char* const rs = wbase + ((stg * 2u + 1u) * 4u + k) * 1024u + 16u * lane;
+            if (w + 16u > lo && w > wmax) { /* past the batch end: the real bytes */
+                tail_fill(a.codes, w, NV, cs);
+                tail_fill(a.vb.round, w, NV, rs);
+            }
+            if (w + 16u > lo && !(a.dbg & 32u)) /* development knob 32: DMA only */
+                walk(w, *reinterpret_cast<const uint4*>(cs), *reinterpret_cast<const uint4*>(rs));
+            if (step == AGNES_STEP_COMMIT) break;
+        }
+        if (!more || step == AGNES_STEP_COMMIT) break;
+        blk = nb;
+        stg ^= 1u;
+    }
+    /* the wave's other lanes may still be streaming: nothing of this lane's in flight */
+    fast::dma_wait();
+
+    if (lock_at == NOPOS && valid_at == NOPOS && dec_at == NOPOS && !skipped && step == step0) return;
+    /* the State back: round (RoundSkip), locked, valid, decision, step/flags.  Only
+     * the starting round can see Polka events: a RoundSkip leaves NewRound, where
+     * vote events change nothing but a commit (:196-211) */
+    const uint4 s1 = sp[1], s2 = sp[2];
+    uint32_t d[16] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w, s2.x, s2.y, s2.z, s2.w, s3.x, s3.y, s3.z, s3.w};
+    uint32_t flags = s3.y;
+    if (skipped) {
+        d[2] = eq8; /* the last RoundSkip's round */
+        d[3] = 0u;
+    }
+    if (lock_at != NOPOS) {
+        d[4] = s0.z;
+        d[5] = s0.w;
+        d[10] = label_of(a, lo, lo + lock_at);
+        flags |= 1u << 8;
+    }
+    if (valid_at != NOPOS) {
+        d[6] = s0.z;
+        d[7] = s0.w;
+        d[11] = valid_at == lock_at ? d[10] : label_of(a, lo, lo + valid_at);
+        flags |= 1u << 16;
+    }
+    if (dec_at != NOPOS) {
+        d[8] = dec_round;
+        d[9] = 0u;
+        d[12] = label_of(a, lo, lo + dec_at);
+        flags |= 1u << 24;
+    }
+    d[13] = (flags & ~0xFFu) | step;
+    sp[0] = make_uint4(d[0], d[1], d[2], d[3]);
+    sp[1] = make_uint4(d[4], d[5], d[6], d[7]);
+    sp[2] = make_uint4(d[8], d[9], d[10], d[11]);
+    sp[3] = make_uint4(d[12], d[13], d[14], d[15]);
+}
+
+} // namespace apply
+} // namespace agnes
+
+/* ------------------------------------------------------------------ */
+
+bool agnes_apply_codes_supported(const agnes_tally_args* a) {
+    /* 16-B windows of the u8 columns */
+    return ((reinterpret_cast<uintptr_t>(a->codes) | reinterpret_cast<uintptr_t>(a->vb.round)) & 15u) == 0u &&
+           a->vb.n_votes >= 32u && a->states != nullptr && (a->flags & AGNES_FLAG_STATE_MACHINE) != 0;
+}
+
+hipError_t agnes_launch_apply_codes(const agnes_tally_args* a, hipStream_t st) {
+    const uint32_t n = a->vb.n_instances;
+    if (n == 0) return hipSuccess;
+    const uint32_t blocks = (n + 255u) / 256u;
+    const size_t lds = (size_t)agnes::apply::LDS_PER_WAVE * agnes::apply::WAVES;
+    static thread_local bool attr[2] = {false, false};
+    const bool skip = (a->flags & AGNES_FLAG_ROUND_SKIP) != 0;
+    if (!attr[skip]) {
+        const void* fn = skip ? reinterpret_cast<const void*>(&agnes::apply::apply_codes<true>)
+                              : reinterpret_cast<const void*>(&agnes::apply::apply_codes<false>);
+        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr[skip] = true;
+    }
+    if (skip)
+        hipLaunchKernelGGL(agnes::apply::apply_codes<true>, dim3(blocks), dim3(256), lds, st, *a);
+    else
+        hipLaunchKernelGGL(agnes::apply::apply_codes<false>, dim3(blocks), dim3(256), lds, st, *a);
+    return hipGetLastError();
+}

@@ -69,6 +69,10 @@ hipError_t agnes_launch_tally_fast(const agnes_tally_args* a, uint32_t mode, int
 /* the stream kernel (agnes_stream.hip): REFERENCE mode without RoundSkip, batches of
  * consecutive instances walked as one vote stream; same deferral protocol */
 hipError_t agnes_launch_tally_stream(const agnes_tally_args* a, int num_cus, hipStream_t stream);
+/* the batched State::apply pass over the codes a tally kernel left (agnes_apply.hip):
+ * one instance per lane, skipping the instances deferred to the LIST kernel */
+bool agnes_apply_codes_supported(const agnes_tally_args* a);
+hipError_t agnes_launch_apply_codes(const agnes_tally_args* a, hipStream_t stream);
 int64_t agnes_fast_lds_per_wave(uint32_t mode, uint32_t flags, uint32_t max_rounds, uint32_t n_vals);
 hipError_t agnes_launch_apply_events(agnes_state* states, uint32_t n, const uint64_t* off,
                                      const agnes_event* ev, agnes_message* msgs, uint32_t flags,

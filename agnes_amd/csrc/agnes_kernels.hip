@@ -1173,14 +1173,29 @@ static hipError_t launch_mode(const agnes_tally_args* a, uint32_t lpw, int num_c
     if (wide_all) return launch_k<true, MODE, SKIP, SM, false>(a, lpw, num_cus, st);
     hipError_t e = hipMemsetAsync(a->list_count, 0, AGNES_QUEUE_WORDS * sizeof(uint32_t), st);
     if (e == hipSuccess) {
-        /* REFERENCE without RoundSkip or State: instance-straddling stream chunks
-         * (measured faster on C2: 0.74 vs 0.88 ms); with the State machine the
-         * per-instance fast kernel (C2 1.39 vs 1.82 ms, C3 0.98 vs 1.25 ms).
-         * AGNES_STREAM (development): 0 never stream, 2 stream the State machine too */
-        const char* d = std::getenv("AGNES_STREAM"); /* per launch: tests switch it */
+        /* REFERENCE without RoundSkip: instance-straddling stream chunks (C2 tally
+         * 0.74 vs 0.88 ms per-instance).  With the State machine the tally kernel
+         * leaves codes only and the one-instance-per-lane apply pass (agnes_apply.hip)
+         * follows: the fused State machine costs the tally kernels registers and
+         * serial ballot loops (C2 1.39 ms per-instance fused, 1.82 ms stream fused).
+         * Development knobs, read per launch (tests switch them):
+         *   AGNES_STREAM 0 never stream, 2 the stream kernel with its fused State machine;
+         *   AGNES_APPLY  0 never the apply pass, 2 also after the per-instance kernel. */
+        const char* d = std::getenv("AGNES_STREAM");
         const int stream_lvl = d && d[0] >= '0' && d[0] <= '2' ? d[0] - '0' : 1;
-        const bool stream = MODE == AGNES_MODE_REFERENCE && !SKIP && stream_lvl > (SM ? 1 : 0);
-        e = stream ? agnes_launch_tally_stream(a, num_cus, st) : agnes_launch_tally_fast(a, MODE, num_cus, st);
+        const char* p = std::getenv("AGNES_APPLY");
+        const int apply_lvl = p && p[0] >= '0' && p[0] <= '2' ? p[0] - '0' : 1;
+        const bool stream = MODE == AGNES_MODE_REFERENCE && !SKIP && stream_lvl >= 1;
+        const bool fused_stream = SM && stream_lvl == 2;
+        const bool split = SM && !fused_stream && agnes_apply_codes_supported(a) &&
+                           (stream ? apply_lvl >= 1 : apply_lvl == 2);
+        agnes_tally_args b = *a;
+        if (split) b.flags &= ~AGNES_FLAG_STATE_MACHINE;
+        if (stream && (!SM || fused_stream || split))
+            e = agnes_launch_tally_stream(&b, num_cus, st);
+        else
+            e = agnes_launch_tally_fast(&b, MODE, num_cus, st);
+        if (e == hipSuccess && split) e = agnes_launch_apply_codes(a, st);
     }
     if (e == hipSuccess) e = launch_k<true, MODE, SKIP, SM, true>(a, lpw, num_cus, st);
     return e;

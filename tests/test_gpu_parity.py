@@ -448,3 +448,69 @@ def test_c3_shard_parity(eng):
     cfg = abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 4)
     g, o = run_both(eng, cfg, hb, power, None, _start_states(125000), threads=16)
     assert_same(g, o)
+
+
+# Every route the launcher can take with the State machine on (agnes_kernels.hip
+# launch_mode): the default split (tally kernel, then the apply pass), the fused
+# per-instance kernel, the fused stream kernel, the per-instance tally + apply pass.
+ROUTES = {
+    "split": {},
+    "fused": {"AGNES_APPLY": "0"},
+    "stream_fused": {"AGNES_STREAM": "2"},
+    "fast_split": {"AGNES_STREAM": "0", "AGNES_APPLY": "2"},
+}
+
+
+def _route(monkeypatch, route):
+    for k in ("AGNES_STREAM", "AGNES_APPLY"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in ROUTES[route].items():
+        monkeypatch.setenv(k, v)
+
+
+@pytest.mark.parametrize("route", list(ROUTES))
+@pytest.mark.parametrize("name", ["c2_sm", "c3_small", "c4_small"])
+def test_routes_generated(eng, monkeypatch, route, name):
+    _route(monkeypatch, route)
+    p, hb, power, cfg = _make(name)
+    g, o = run_both(eng, cfg, hb, power, None, _start_states(p.n_instances))
+    assert_same(g, o)
+
+
+@pytest.mark.parametrize("route", list(ROUTES))
+@pytest.mark.parametrize("mode,flags", [
+    (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE),
+    (abi.MODE_DEDUP, abi.FLAG_STATE_MACHINE | abi.FLAG_ROUND_SKIP)])
+def test_routes_ragged_and_labels(eng, monkeypatch, route, mode, flags):
+    """Ragged instances (many per chunk, empty ones) and early quorums whose nil
+    votes carry labels from earlier lanes / chunks."""
+    _route(monkeypatch, route)
+    hb = _ragged_batch(21, 20000, 9, 3, [0, 0, 1, 2, 3, 5, 8, 13, 63, 64, 65, 130, 200])
+    power = ol.gen_power(21, 13, 9, abi.POWER_UNIFORM, 1, 20)
+    g, o = run_both(eng, abi.config(mode, flags, 3), hb, power, None, _start_states(hb.n_instances))
+    assert_same(g, o)
+    hb = _ragged_batch(8, 30000, 2, 2, [1, 2, 3, 4, 5, 7, 9, 17, 33, 80, 200, 400])
+    power = np.ones((1, 2), np.int64)
+    g, o = run_both(eng, abi.config(mode, flags, 2), hb, power, None, _start_states(hb.n_instances))
+    assert_same(g, o)
+
+
+@pytest.mark.parametrize("route", list(ROUTES))
+def test_routes_valid_from_input(eng, monkeypatch, route):
+    """States entering in Precommit with `valid` already at their round
+    (set_valid_value, state_machine.rs:202): a nil vote that reaches the value
+    quorum first must set valid to its bucket's last value (round_votes.rs:50-54)."""
+    _route(monkeypatch, route)
+    rng = np.random.default_rng(44)
+    hb = _ragged_batch(44, 8000, 3, 2, [4, 8, 12, 40, 200])
+    power = np.ones((1, 3), np.int64)
+    st = _start_states(hb.n_instances)
+    k = rng.random(hb.n_instances)
+    sel = k < 0.6
+    st["step"][sel] = abi.STEP_PRECOMMIT
+    st["round"][sel] = 0
+    st["valid_present"][sel] = 1
+    st["valid_round"][sel] = 0
+    st["valid_value"][sel] = 7  # a value no vote carries
+    g, o = run_both(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 2), hb, power, None, st)
+    assert_same(g, o)

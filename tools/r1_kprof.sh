@@ -1,0 +1,13 @@
+#!/bin/bash
+# per-kernel durations of kbench variants (rocprofv3 kernel trace + stats, csv)
+cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out && export TMPDIR=/tmp
+rm -rf gpurun_out/kprof
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kprof -o run -- python3 tools/kbench.py --iters 5 ${KB:-c2_sm} > gpurun_out/kprof.log 2>&1 || { tail -30 gpurun_out/kprof.log; exit 1; }
+grep '^{' gpurun_out/kprof.log
+f=$(find gpurun_out/kprof -name '*kernel_stats.csv' | head -1)
+python3 - "$f" <<'PY'
+import csv, sys
+rows = list(csv.DictReader(open(sys.argv[1])))
+for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:12]:
+    print(f'{int(r["Calls"]):5d} {float(r["AverageNs"])/1e3:10.1f} us  {r["Name"][:110]}')
+PY
