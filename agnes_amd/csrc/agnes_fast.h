@@ -200,6 +200,20 @@ __device__ __forceinline__ uint32_t first_of(const uint64_t (&b)[VPL], uint32_t 
     return f;
 }
 
+/* the last chunk position in [lo, hi) whose vote s is set in ballot b[s]; CHUNK if none */
+__device__ __forceinline__ uint32_t last_of(const uint64_t (&b)[VPL], uint32_t lo, uint32_t hi) {
+    uint32_t f = CHUNK;
+#pragma unroll
+    for (uint32_t s = 0; s < VPL; ++s) {
+        const uint64_t m = b[s] & win(s, lo, hi);
+        if (m) {
+            const uint32_t p = 4u * (63u - (uint32_t)__builtin_clzll(m)) + s;
+            f = (f == CHUNK || p > f) ? p : f;
+        }
+    }
+    return f;
+}
+
 } // namespace fast
 } // namespace agnes
 

@@ -45,7 +45,26 @@ constexpr uint32_t SMALL = 4u; /* batch size of the work queue's tail           
  * (state machine) the current batch's States */
 __host__ __device__ inline uint32_t carry_words(uint32_t R) { return (uint32_t)(align16(16ull * R) / 4u); }
 __host__ __device__ inline uint32_t lds_bytes(bool sm, uint32_t R) {
-    return PF_BYTES + 8u * carry_words(R) + (sm ? SBQ * 64u : 0u);
+    return PF_BYTES + 8u * carry_words(R) + (sm ? SBQ * 64u + SBQ * 32u : 0u);
+}
+
+/* State::apply shadow of a batch instance (LDS, 8 dwords): what the votes did to
+ * its State, applied to the staged State when the batch ends */
+constexpr uint32_t SH_STEP = 0, SH_EQ8 = 1, SH_FLAGS = 2, SH_LOCK = 3, SH_VALID = 4, SH_DEC = 5, SH_DECR = 6;
+constexpr uint32_t F_STEP = 1u, F_LOCK = 2u, F_VALID = 4u, F_DEC = 8u;
+
+/* 0xFF in the bytes of x that are zero (exact, no borrow) */
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
+    const uint32_t t = (x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+    const uint32_t z = ~(t | x) & 0x80808080u;
+    return z | (z - (z >> 7));
+}
+/* 0xFF in the bytes below byte i (i <= 4) */
+__device__ __forceinline__ uint32_t below_bytes(uint32_t i) { return i >= 4u ? 0xFFFFFFFFu : (1u << (8u * i)) - 1u; }
+/* 0xFF in byte i of the result for bit i of x (x < 16) */
+__device__ __forceinline__ uint32_t bytes_of(uint32_t x) {
+    const uint32_t b = (x * 0x00204081u) & 0x01010101u;
+    return (b << 8) - b;
 }
 
 __device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
@@ -65,7 +84,12 @@ struct Hdr {
 };
 
 template <bool SM, bool PC>
-__global__ __launch_bounds__(256) void tally_stream(agnes_tally_args a, uint32_t lds_per_wave) {
+#ifdef AGNES_STREAM_WPE /* development: minimum waves per SIMD the register allocator must allow */
+#define AGNES_STREAM_ATTR __attribute__((amdgpu_waves_per_eu(AGNES_STREAM_WPE)))
+#else
+#define AGNES_STREAM_ATTR
+#endif
+__global__ __launch_bounds__(256) AGNES_STREAM_ATTR void tally_stream(agnes_tally_args a, uint32_t lds_per_wave) {
     const uint32_t lane = lane_id();
     const uint32_t wave = rfl(threadIdx.x >> 6);
     const uint32_t R = a.max_rounds, nv = a.n_vals, ns = a.n_sets, n = a.vb.n_instances;
@@ -84,6 +108,7 @@ __global__ __launch_bounds__(256) void tally_stream(agnes_tally_args a, uint32_t
     uint32_t* const crow = reinterpret_cast<uint32_t*>(base + PF_BYTES);
     const uint32_t cw = carry_words(R); /* one copy: vw[2R] then vn[2R] */
     unsigned char* const sb = base + PF_BYTES + 8u * cw;
+    uint32_t* const shw = reinterpret_cast<uint32_t*>(sb + SBQ * 64u); /* State::apply shadows */
     uint32_t cpar = 0;
     uint64_t pf_at = ~0ull;
     uint32_t bad = 0;
@@ -221,6 +246,7 @@ __global__ __launch_bounds__(256) void tally_stream(agnes_tally_args a, uint32_t
         const uint32_t m = H.e0 - H.s0;
         const bool S = H.stream;
         bool fresh = true; /* the batch's first chunk step */
+        bool smf = SM;     /* the shadows are not yet set up from the staged States */
         uint32_t si = 0;
         for (;;) { /* streams of the batch: one (stream batch) or one per instance */
             uint64_t slo, shi;
@@ -478,133 +504,183 @@ __global__ __launch_bounds__(256) void tally_stream(agnes_tally_args a, uint32_t
                 }
                 if (lastc) cpar ^= 1u;
 
-                /* ---- K4: State::apply(v.round, event) per segment, stream order
-                 * (consensus_executor.rs:64-68) ---- */
+                /* ---- K4: State::apply(v.round, event), stream order (consensus_executor.rs:64-68)
+                 * Without RoundSkip the vote-driven steps form the monoid {id, Prevote ->
+                 * Precommit, -> Commit} (state_machine.rs:196-211): in a segment every
+                 * vote is decided by two positions, the first PrecommitValue (commit, any
+                 * round: :211) and P1, the first PolkaNil / PolkaValue at eqr before it
+                 * while in Prevote (:197-198).  Messages: TimeoutPrevote for PolkaAny at
+                 * eqr before P1 in Prevote (:196), TimeoutPrecommit for PrecommitAny at eqr
+                 * before the commit (:208), the step messages at P1 and the commit.  The
+                 * State takes locked at P1 (a PolkaValue), valid = the last PolkaValue at
+                 * eqr in Prevote / Precommit before the commit (:198, :202; its value is
+                 * the last non-nil one among them, round_votes.rs:50-54) and the decision.
+                 * Segments start at lane boundaries, so all of it is lane-parallel: byte
+                 * masks per lane, "earlier in my segment" from two ballots, the results
+                 * into the instance's LDS shadow (rare: a nil vote's label, label_at). */
+                uint32_t smmsg = 0;
                 if (SM) {
-                    for (uint32_t d = 0; d <= D; ++d) {
-                        const uint32_t kseg = D ? rdl(segk, d) : k0;
-                        const uint32_t La = d ? rdl(segL, d) : 0u;
-                        const uint32_t Lb = d < D ? rdl(segL, d + 1u) : 64u;
-                        const uint32_t plo = 4u * La > lo_r ? 4u * La : lo_r;
-                        const uint32_t phi = 4u * Lb < hi_r ? 4u * Lb : hi_r;
-                        const uint64_t ibeg = S ? u64of(rdl(H.olo, kseg), rdl(H.ohi, kseg)) : slo;
-                        const uint32_t iid = H.s0 + kseg;
-                        unsigned char* const sp = sb + 64u * kseg;
-                        const bool sl = lane >= SL && lane < SL + 14u;
-                        uint32_t stv = sl ? *reinterpret_cast<const uint32_t*>(sp + 4u * (lane - SL)) : 0u;
-                        View V = view_of(stv);
-                        if ((V.flags & 0xFFu) == AGNES_STEP_COMMIT) continue; /* :205 */
-                        /* event of vote s with the eqr bit; 6 (invalid) matches nothing */
-                        auto ev_of = [&](uint32_t s) -> uint32_t {
-                            return (code[s] & 7u) | ((uint32_t)(byte_of(r4, s) == V.eq8) << 3);
-                        };
-                        /* the payload of the changing vote at chunk position f: its value, or
-                         * the last value written before it in its bucket (round_votes.rs:53) */
-                        auto label_at = [&](uint32_t f) -> uint32_t {
-                            const uint32_t fl = f >> 2, fs = f & 3u;
-                            const uint32_t fv = rdl(sel4(value, fs), fl);
-                            if (fv != AGNES_NIL) return fv;
-                            const uint32_t K = rdl(sel4(key, fs), fl);
-                            uint32_t cand = 0;
+                    if (smf) { /* the batch's staged States have landed (dma_wait above) */
+                        if (lane < m) {
+                            const uint32_t* const sp = reinterpret_cast<const uint32_t*>(sb + 64u * lane);
+                            const int64_t rnd = (int64_t)u64of(sp[2], sp[3]);
+                            shw[8u * lane + SH_STEP] = sp[13] & 0xFFu;
+                            shw[8u * lane + SH_EQ8] = (rnd >= 0 && rnd <= 255) ? (uint32_t)rnd : 0x100u;
+                            shw[8u * lane + SH_FLAGS] = 0u;
+                        }
+                        smf = false;
+                    }
+                    /* the value of the Value event at chunk position f of a nil vote: the
+                     * last value counted into its bucket before it (round_votes.rs:50-54),
+                     * searched in the chunk's segment [plo, f), then in the instance's
+                     * earlier chunks (newest first, one vote per lane: rare, few registers) */
+                    auto label_at = [&](uint32_t f, uint32_t plo, uint64_t ibeg, uint32_t iid) -> uint32_t {
+                        const uint32_t fl = f >> 2, fs = f & 3u;
+                        const uint32_t K = rdl(sel4(key, fs), fl);
+                        uint32_t cand = 0;
 #pragma unroll
-                            for (uint32_t s = 0; s < VPL; ++s)
-                                cand |= (uint32_t)(key[s] == K && value[s] != AGNES_NIL && p0 + s < f && p0 + s >= plo) << s;
-                            const uint64_t cl = ballot(cand != 0u);
-                            if (cl) {
-                                const uint32_t hl = 63u - (uint32_t)__builtin_clzll(cl);
-                                const uint32_t hs = 31u - (uint32_t)__builtin_clz(rdl(cand, hl));
-                                return rdl(sel4(value, hs), hl);
-                            }
-                            /* earlier chunks of the instance, newest first, one vote per lane
-                             * at a time (rare path, few registers) */
-                            for (uint64_t pcz = c; pcz > (ibeg & ~3ull);) {
-                                pcz -= CHUNK;
-                                uint32_t hit = 0, hv = 0;
+                        for (uint32_t s2 = 0; s2 < VPL; ++s2)
+                            cand |= (uint32_t)(key[s2] == K && value[s2] != AGNES_NIL && p0 + s2 < f && p0 + s2 >= plo) << s2;
+                        const uint64_t cl = ballot(cand != 0u);
+                        if (cl) {
+                            const uint32_t hl = 63u - (uint32_t)__builtin_clzll(cl);
+                            const uint32_t hs = 31u - (uint32_t)__builtin_clz(rdl(cand, hl));
+                            return rdl(sel4(value, hs), hl);
+                        }
+                        for (uint64_t pcz = c; pcz > (ibeg & ~3ull);) {
+                            pcz -= CHUNK;
+                            uint32_t hit = 0, hv = 0;
 #pragma unroll 1
-                                for (int s = (int)VPL - 1; s >= 0; --s) {
-                                    const uint64_t j = pcz + p0 + (uint32_t)s;
-                                    if (!hit && j >= ibeg && j < c) {
-                                        const uint8_t *br = a.vb.round, *bt = a.vb.type;
-                                        const uint32_t *bx = a.vb.validator, *bv = a.vb.value, *bi = a.vb.instance;
-                                        asm volatile("" : "+s"(br), "+s"(bt), "+s"(bx), "+s"(bv), "+s"(bi));
-                                        const uint32_t vr = br[j], vt = bt[j], vx = bx[j], vv = bv[j];
-                                        if (bi[j] == iid && vr < R && vt <= 1u && vx < nv && vr * 2u + vt == K &&
-                                            vv != AGNES_NIL) {
-                                            hit = 1;
-                                            hv = vv;
-                                        }
+                            for (int s2 = (int)VPL - 1; s2 >= 0; --s2) {
+                                const uint64_t j = pcz + p0 + (uint32_t)s2;
+                                if (!hit && j >= ibeg && j < c) {
+                                    const uint8_t *br = a.vb.round, *bt = a.vb.type;
+                                    const uint32_t *bx = a.vb.validator, *bv = a.vb.value, *bi = a.vb.instance;
+                                    asm volatile("" : "+s"(br), "+s"(bt), "+s"(bx), "+s"(bv), "+s"(bi));
+                                    const uint32_t vr = br[j], vt = bt[j], vx = bx[j], vv = bv[j];
+                                    if (bi[j] == iid && vr < R && vt <= 1u && vx < nv && vr * 2u + vt == K &&
+                                        vv != AGNES_NIL) {
+                                        hit = 1;
+                                        hv = vv;
                                     }
                                 }
-                                const uint64_t hl = ballot(hit != 0u);
-                                if (hl) return rdl(hv, 63u - (uint32_t)__builtin_clzll(hl));
                             }
-                            return 0u; /* unreachable: a nil vote at value quorum has a value vote
-                                          before it in its bucket */
-                        };
-                        /* One change per pass: the first PrecommitValue (commit) and, before it,
-                         * the first vote that moves the current step (Prevote: PolkaNil /
-                         * PolkaValue at eqr; Precommit: PolkaValue at eqr with another value);
-                         * the non-changing messages are PolkaAny at eqr -> TimeoutPrevote while
-                         * in Prevote (before P1) and PrecommitAny at eqr -> TimeoutPrecommit
-                         * before the commit (pc). */
-                        const bool prevote0 = (V.flags & 0xFFu) == AGNES_STEP_PREVOTE;
-                        uint32_t P1 = prevote0 ? phi : plo, pc = phi, lo = plo;
-                        bool changed = false;
-                        for (;;) {
-                            const uint32_t step = V.flags & 0xFFu;
-                            uint64_t b[VPL];
-#pragma unroll
-                            for (uint32_t s = 0; s < VPL; ++s) {
-                                const uint32_t ix = ev_of(s);
-                                const bool pv = ix == (AGNES_CODE_POLKA_VALUE | 8u);
-                                const bool mv = step == AGNES_STEP_PREVOTE
-                                                    ? (pv || ix == (AGNES_CODE_POLKA_NIL | 8u))
-                                                    : (step == AGNES_STEP_PRECOMMIT && pv &&
-                                                       (!V.vsame || (value[s] != AGNES_NIL && value[s] != V.vval)));
-                                b[s] = ballot(mv || (ix & 7u) == AGNES_CODE_PRECOMMIT_VALUE);
-                            }
-                            const uint32_t f = first_of(b, lo, phi);
-                            if (f >= phi) break;
-                            const uint32_t fl = f >> 2, fs = f & 3u;
-                            const uint32_t fcode = rdl(sel4(code, fs), fl);
-                            const uint32_t fev = fcode & 7u;
-                            const uint32_t lab = (fev == AGNES_CODE_POLKA_VALUE || fev == AGNES_CODE_PRECOMMIT_VALUE)
-                                                     ? label_at(f) : 0u;
-                            const uint32_t vm = apply_change(stv, V, fcode, byte_of(rdl(r4, fl), fs), lab);
-                            changed = true;
-                            if (lane == fl) {
-#pragma unroll
-                                for (uint32_t s = 0; s < VPL; ++s)
-                                    if (s == fs) code[s] |= vm << AGNES_CODE_MSG_SHIFT;
-                            }
-                            if (step == AGNES_STEP_PREVOTE && P1 == phi) P1 = f; /* left Prevote */
-                            if ((V.flags & 0xFFu) == AGNES_STEP_COMMIT) { /* :211; :205 later events: None */
-                                pc = f;
-                                break;
-                            }
-                            lo = f + 1u;
+                            const uint64_t hl = ballot(hit != 0u);
+                            if (hl) return rdl(hv, 63u - (uint32_t)__builtin_clzll(hl));
                         }
-                        /* messages of the non-changing events */
+                        return 0u; /* VoteCount::new's label (round_votes.rs:36-45) */
+                    };
+                    uint32_t* const sh = shw + 8u * kln;
+                    const uint32_t step = sh[SH_STEP], eq8 = sh[SH_EQ8], vset = sh[SH_FLAGS] & F_VALID;
+                    const uint32_t c4 = code[0] | (code[1] << 8) | (code[2] << 16) | (code[3] << 24);
+                    const uint32_t e4 = c4 & 0x07070707u;
+                    const uint32_t live0 = step != AGNES_STEP_COMMIT ? bytes_of(pos) : 0u; /* :205 */
+                    const uint32_t eqm = eq8 < 0x100u ? zero_bytes(r4 ^ (eq8 * 0x01010101u)) & live0 : 0u;
+                    const uint32_t cvb = zero_bytes(e4 ^ 0x05050505u) & live0;
+                    const uint32_t pvb = zero_bytes(e4 ^ 0x03030303u) & eqm;
+                    const uint32_t pnb = zero_bytes(e4 ^ 0x02020202u) & eqm;
+                    const uint32_t pab = zero_bytes(e4 ^ 0x01010101u) & eqm;
+                    const uint32_t cab = zero_bytes(e4 ^ 0x04040404u) & eqm;
+                    const bool prevote = step == AGNES_STEP_PREVOTE;
+                    const uint32_t p1b = prevote ? (pvb | pnb) : 0u;
+                    /* my segment: [first lane ss, next start ns) */
+                    const uint64_t SSm = BL | 1ull;
+                    const uint64_t upto = lane == 63u ? ~0ull : ((2ull << lane) - 1ull);
+                    const uint32_t ss = 63u - (uint32_t)__builtin_clzll(SSm & upto);
+                    const uint64_t nsm = SSm & ~upto;
+                    const uint64_t before = ((1ull << lane) - 1ull) & ~((1ull << ss) - 1ull);
+                    const uint64_t after = (nsm ? ((nsm & (0ull - nsm)) - 1ull) : ~0ull) & ~upto;
+                    const uint64_t MCV = ballot(cvb != 0u), MP1 = ballot(p1b != 0u);
+                    const bool cv_before = (MCV & before) != 0ull, p1_before = (MP1 & before) != 0ull;
+                    const uint32_t cs = cvb ? ((uint32_t)__builtin_ctz(cvb) >> 3) : 4u; /* my first commit slot */
+                    const uint32_t alive = cv_before ? 0u : below_bytes(cs);
+                    const uint32_t p1m = (!p1_before && !cv_before) ? (p1b & below_bytes(cs)) : 0u;
+                    const uint32_t ps = p1m ? ((uint32_t)__builtin_ctz(p1m) >> 3) : 4u; /* my P1 slot */
+                    const uint32_t tpr = (prevote && !p1_before) ? below_bytes(ps) : 0u;
+                    smmsg = (pab & alive & tpr & (AGNES_VMSG_TIMEOUT_PREVOTE * 0x10101010u)) |
+                            (cab & alive & (AGNES_VMSG_TIMEOUT_PRECOMMIT * 0x10101010u));
+                    const bool p1_pv = p1m && ((pvb >> (8u * ps)) & 1u);
+                    if (p1m) smmsg |= (p1_pv ? AGNES_VMSG_PRECOMMIT_VALUE : AGNES_VMSG_PRECOMMIT_NIL) << (8u * ps + 4u);
+                    const bool commit = !cv_before && cvb != 0u;
+                    if (commit) smmsg |= AGNES_VMSG_DECISION << (8u * cs + 4u);
+                    /* valid: the PolkaValues at eqr in Prevote (after P1) / Precommit, alive */
+                    const uint32_t vcand = (prevote || step == AGNES_STEP_PRECOMMIT) ? (pvb & alive) : 0u;
+                    uint32_t nilb = 0;
 #pragma unroll
-                        for (uint32_t s = 0; s < VPL; ++s) {
-                            const uint32_t ix = ev_of(s);
-                            const bool m1 = ix == (AGNES_CODE_POLKA_ANY | 8u) && ((win(s, plo, P1) >> lane) & 1u);
-                            const bool m2 = ix == (AGNES_CODE_PRECOMMIT_ANY | 8u) && ((win(s, plo, pc) >> lane) & 1u);
-                            code[s] |= (m1 ? AGNES_VMSG_TIMEOUT_PREVOTE : (m2 ? AGNES_VMSG_TIMEOUT_PRECOMMIT : 0u))
-                                       << AGNES_CODE_MSG_SHIFT;
+                    for (uint32_t s2 = 0; s2 < VPL; ++s2) nilb |= (uint32_t)(value[s2] == AGNES_NIL) << s2;
+                    const uint32_t vnn = vcand & ~bytes_of(nilb);
+                    const uint64_t MV = ballot(vcand != 0u), MVN = ballot(vnn != 0u);
+                    const uint64_t seg = before | after | (1ull << lane);
+                    /* the shadow (one lane per segment and kind: no two lanes write one word) */
+                    const bool p1_nil = p1_pv && value[ps & 3u] == AGNES_NIL;
+                    if (p1m) {
+                        atomicMax(sh + SH_STEP, (uint32_t)AGNES_STEP_PRECOMMIT);
+                        atomicOr(sh + SH_FLAGS, p1_pv ? (F_STEP | F_LOCK) : F_STEP);
+                        if (p1_pv && !p1_nil) sh[SH_LOCK] = value[ps & 3u];
+                    }
+                    const bool dec_nil = commit && value[cs & 3u] == AGNES_NIL;
+                    if (commit) {
+                        atomicMax(sh + SH_STEP, (uint32_t)AGNES_STEP_COMMIT);
+                        atomicOr(sh + SH_FLAGS, F_STEP | F_DEC);
+                        sh[SH_DECR] = byte_of(r4, cs & 3u);
+                        if (!dec_nil) sh[SH_DEC] = value[cs & 3u];
+                    }
+                    if (vnn && !(MVN & after)) { /* the segment's last non-nil candidate */
+                        sh[SH_VALID] = value[(31u - (uint32_t)__builtin_clz(vnn)) >> 3];
+                        atomicOr(sh + SH_FLAGS, F_VALID);
+                    }
+                    /* only nil candidates in the segment and valid not yet set in this batch:
+                     * the label of the first one (round_votes.rs:50-54) */
+                    const bool fp_nil = vcand && !(MV & before) && !(MVN & seg) && !vset;
+                    /* rare: labels of nil votes, by the bucket search */
+                    uint64_t need = ballot(p1_nil || dec_nil || fp_nil);
+                    while (need) {
+                        const uint32_t L = (uint32_t)__builtin_ctzll(need);
+                        need &= need - 1ull;
+                        const uint32_t kk = rdl(kln, L), ssl = rdl(ss, L);
+                        const uint32_t plo = 4u * ssl > lo_r ? 4u * ssl : lo_r;
+                        const uint64_t ibeg = S ? u64of(rdl(H.olo, kk), rdl(H.ohi, kk)) : slo;
+                        const uint32_t iid = H.s0 + kk;
+                        uint32_t* const shk = shw + 8u * kk;
+                        if (rdl((uint32_t)p1_nil, L)) {
+                            const uint32_t lab = label_at(4u * L + rdl(ps, L), plo, ibeg, iid);
+                            if (lane == 0u) shk[SH_LOCK] = lab;
                         }
-                        if (changed && sl) *reinterpret_cast<uint32_t*>(sp + 4u * (lane - SL)) = stv;
+                        if (rdl((uint32_t)dec_nil, L)) {
+                            const uint32_t lab = label_at(4u * L + rdl(cs, L), plo, ibeg, iid);
+                            if (lane == 0u) shk[SH_DEC] = lab;
+                        }
+                        if (rdl((uint32_t)fp_nil, L)) {
+                            const uint32_t fs = (uint32_t)__builtin_ctz(rdl(vcand, L)) >> 3;
+                            const uint32_t lab = label_at(4u * L + fs, plo, ibeg, iid);
+                            if (lane == 0u) {
+                                shk[SH_VALID] = lab;
+                                atomicOr(shk + SH_FLAGS, F_VALID);
+                            }
+                        }
                     }
                 }
 
                 /* codes (deferred): one 4-B store when all 4 votes belong to the stream */
-                dc_code = code[0] | (code[1] << 8) | (code[2] << 16) | (code[3] << 24);
+                dc_code = code[0] | (code[1] << 8) | (code[2] << 16) | (code[3] << 24) | smmsg;
                 dc_pos = pos;
                 dc_at = c;
                 __builtin_amdgcn_wave_barrier();
             }
         }
-        /* batch end: States back, then the next batch */
+        /* batch end: the shadows into the staged States, States back, then the next batch */
+        if (SM && !smf && lane < m) {
+            const uint32_t* const sh = shw + 8u * lane;
+            const uint32_t f = sh[SH_FLAGS];
+            if (f) {
+                uint32_t* const sp = reinterpret_cast<uint32_t*>(sb + 64u * lane);
+                uint32_t fl = (sp[13] & ~0xFFu) | sh[SH_STEP];
+                if (f & F_LOCK) { sp[4] = sp[2]; sp[5] = sp[3]; sp[10] = sh[SH_LOCK]; fl |= 1u << 8; }
+                if (f & F_VALID) { sp[6] = sp[2]; sp[7] = sp[3]; sp[11] = sh[SH_VALID]; fl |= 1u << 16; }
+                if (f & F_DEC) { sp[8] = sh[SH_DECR]; sp[9] = 0u; sp[12] = sh[SH_DEC]; fl |= 1u << 24; }
+                sp[13] = fl;
+            }
+        }
         store_states(H);
         if (N.s0 >= N.e0) break;
         if (!N.ready) hdr2(N);
