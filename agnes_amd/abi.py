@@ -69,6 +69,12 @@ class StateRec(C.Structure):
                 ("decided", C.c_uint8), ("pad", C.c_uint8 * 8)]
 
 
+class KernelTime(C.Structure):
+    """agnes_kernel_time (include/agnes.h): per-kernel launch count and total ms."""
+    _fields_ = [("name", C.c_char * 40), ("launches", C.c_uint32), ("pad", C.c_uint32),
+                ("total_ms", C.c_double)]
+
+
 class Config(C.Structure):
     _fields_ = [("mode", C.c_uint32), ("flags", C.c_uint32), ("max_rounds", C.c_uint32),
                 ("reserved", C.c_uint32)]

@@ -110,6 +110,68 @@ int scalar_ctx(agnes_ctx** out) {
 
 extern "C" {
 
+namespace {
+struct KtRec {
+    const char* name;
+    hipEvent_t b, e;
+};
+bool kt_on = false;
+std::vector<KtRec> kt_recs;
+size_t kt_used = 0;
+std::mutex kt_mu;
+} // namespace
+
+void agnes_kt_mark(const char* name, hipStream_t st, bool begin) {
+    if (!kt_on) return;
+    std::lock_guard<std::mutex> g(kt_mu);
+    if (begin) {
+        if (kt_used == kt_recs.size()) {
+            KtRec r{name, nullptr, nullptr};
+            if (hipEventCreate(&r.b) != hipSuccess || hipEventCreate(&r.e) != hipSuccess) return;
+            kt_recs.push_back(r);
+        }
+        kt_recs[kt_used].name = name;
+        (void)hipEventRecord(kt_recs[kt_used].b, st);
+    } else if (kt_used < kt_recs.size()) {
+        (void)hipEventRecord(kt_recs[kt_used].e, st);
+        ++kt_used;
+    }
+}
+
+int agnes_kernel_timing(int enable) {
+    std::lock_guard<std::mutex> g(kt_mu);
+    kt_on = enable != 0;
+    kt_used = 0;
+    return AGNES_OK;
+}
+
+int agnes_kernel_times(agnes_kernel_time* out, uint32_t cap, uint32_t* n) {
+    if (!n || (cap && !out)) return AGNES_E_INVALID;
+    std::lock_guard<std::mutex> g(kt_mu);
+    uint32_t k = 0;
+    for (size_t i = 0; i < kt_used; ++i) {
+        const KtRec& r = kt_recs[i];
+        AGNES_TRY(hipEventSynchronize(r.e));
+        float ms = 0.f;
+        AGNES_TRY(hipEventElapsedTime(&ms, r.b, r.e));
+        uint32_t j = 0;
+        while (j < k && j < cap && std::strncmp(out[j].name, r.name, sizeof(out[j].name) - 1) != 0) ++j;
+        if (j == k) {
+            if (k < cap) {
+                std::memset(&out[k], 0, sizeof(out[k]));
+                std::strncpy(out[k].name, r.name, sizeof(out[k].name) - 1);
+            }
+            ++k;
+        }
+        if (j < cap) {
+            out[j].launches += 1;
+            out[j].total_ms += ms;
+        }
+    }
+    *n = k;
+    return AGNES_OK;
+}
+
 uint32_t agnes_abi_version(void) { return AGNES_ABI_VERSION; }
 
 int agnes_ctx_create(int device, agnes_ctx** out) {

@@ -53,6 +53,15 @@ typedef struct agnes_tally_args {
     uint32_t power_cache; /* bytes of block LDS holding the u32 power table (0: gather from HBM) */
 } agnes_tally_args;
 
+/* agnes_kernel_timing: HIP events around each launch while enabled (agnes_api.cpp) */
+extern "C" void agnes_kt_mark(const char* name, hipStream_t st, bool begin);
+struct AgnesKt {
+    const char* name;
+    hipStream_t st;
+    AgnesKt(const char* n, hipStream_t s) : name(n), st(s) { agnes_kt_mark(name, st, true); }
+    ~AgnesKt() { agnes_kt_mark(name, st, false); }
+};
+
 /* bytes of dynamic LDS one wave uses */
 int64_t agnes_lds_per_wave(uint32_t mode, uint32_t flags, uint32_t max_rounds, uint32_t n_vals);
 

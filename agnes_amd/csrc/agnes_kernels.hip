@@ -1170,8 +1170,15 @@ static hipError_t launch_k(const agnes_tally_args* a, uint32_t lpw, int num_cus,
 template <uint32_t MODE, bool SKIP, bool SM>
 static hipError_t launch_mode(const agnes_tally_args* a, uint32_t lpw, int num_cus, bool wide_all,
                               hipStream_t st) {
-    if (wide_all) return launch_k<true, MODE, SKIP, SM, false>(a, lpw, num_cus, st);
-    hipError_t e = hipMemsetAsync(a->list_count, 0, AGNES_QUEUE_WORDS * sizeof(uint32_t), st);
+    if (wide_all) {
+        AgnesKt kt("tally_wide", st);
+        return launch_k<true, MODE, SKIP, SM, false>(a, lpw, num_cus, st);
+    }
+    hipError_t e;
+    {
+        AgnesKt kt("queue_reset", st);
+        e = hipMemsetAsync(a->list_count, 0, AGNES_QUEUE_WORDS * sizeof(uint32_t), st);
+    }
     if (e == hipSuccess) {
         /* REFERENCE without RoundSkip: instance-straddling stream chunks (C2 tally
          * 0.74 vs 0.88 ms per-instance).  With the State machine the tally kernel
@@ -1191,13 +1198,22 @@ static hipError_t launch_mode(const agnes_tally_args* a, uint32_t lpw, int num_c
                            (stream ? apply_lvl >= 1 : apply_lvl == 2);
         agnes_tally_args b = *a;
         if (split) b.flags &= ~AGNES_FLAG_STATE_MACHINE;
-        if (stream && (!SM || fused_stream || split))
+        if (stream && (!SM || fused_stream || split)) {
+            AgnesKt kt("tally_stream", st);
             e = agnes_launch_tally_stream(&b, num_cus, st);
-        else
+        } else {
+            AgnesKt kt("tally_fast", st);
             e = agnes_launch_tally_fast(&b, MODE, num_cus, st);
-        if (e == hipSuccess && split) e = agnes_launch_apply_codes(a, st);
+        }
+        if (e == hipSuccess && split) {
+            AgnesKt kt("apply_codes", st);
+            e = agnes_launch_apply_codes(a, st);
+        }
     }
-    if (e == hipSuccess) e = launch_k<true, MODE, SKIP, SM, true>(a, lpw, num_cus, st);
+    if (e == hipSuccess) {
+        AgnesKt kt("tally_list", st);
+        e = launch_k<true, MODE, SKIP, SM, true>(a, lpw, num_cus, st);
+    }
     return e;
 }
 

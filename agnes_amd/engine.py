@@ -136,6 +136,20 @@ class Engine:
         check(self.lib.agnes_last_error_count(self.ctx, C.byref(v)), "agnes_last_error_count")
         return int(v.value)
 
+    # -- measurement ----------------------------------------------------------
+    def kernel_timing(self, enable: bool):
+        """Bracket every kernel the engine enqueues with HIP events (clears records)."""
+        check(self.lib.agnes_kernel_timing(1 if enable else 0), "agnes_kernel_timing")
+
+    def kernel_times(self) -> dict:
+        """{kernel name: (launches, total ms)} of the launches since kernel_timing(True)."""
+        cap = 16
+        out = (abi.KernelTime * cap)()
+        n = C.c_uint32(0)
+        check(self.lib.agnes_kernel_times(out, cap, C.byref(n)), "agnes_kernel_times")
+        return {out[i].name.decode(): (int(out[i].launches), float(out[i].total_ms))
+                for i in range(min(n.value, cap))}
+
     def lds_bytes_per_wave(self, cfg: abi.Config) -> int:
         return int(self.lib.agnes_lds_bytes_per_wave(C.byref(cfg), self.n_vals))
 

@@ -57,6 +57,8 @@ def load():
     P = C.c_void_p
     sig = {
         "agnes_abi_version": ([], C.c_uint32),
+        "agnes_kernel_timing": ([C.c_int], C.c_int),
+        "agnes_kernel_times": ([C.POINTER(abi.KernelTime), C.c_uint32, C.POINTER(C.c_uint32)], C.c_int),
         "agnes_ctx_create": ([C.c_int, C.POINTER(P)], C.c_int),
         "agnes_ctx_destroy": ([P], None),
         "agnes_ctx_device": ([P], C.c_int),

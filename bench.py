@@ -32,6 +32,19 @@ from agnes_amd.engine import Engine, states_to_device  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
 BYTES_PER_VOTE = 15            # 14 B canonical SoA in + 1 B code out
+# algorithmic bytes per vote of each engine kernel (names: agnes_kernel_times)
+KERNEL_BYTES_PER_VOTE = {
+    "tally_stream": 15,  # instance, value, validator u32 + round, type u8 in; code u8 out
+    "tally_fast": 15,
+    "tally_wide": 15,
+    "apply_codes": 2,    # code + round u8 in (messages written back sparsely)
+}
+KERNEL_SYMBOLS = {
+    "tally_stream": "agnes::stream::tally_stream<false, *>",
+    "tally_fast": "agnes::fast::tally_fast<...>",
+    "tally_wide": "agnes::tally_kernel<true, ...>",
+    "apply_codes": "agnes::apply::apply_codes<false>",
+}
 
 WORKLOADS = {
     # BASELINE configs[1] = C2, timed over 100 batched heights
@@ -62,16 +75,18 @@ def start_states(n: int) -> np.ndarray:
     return abi.new_states(n, height=1, step=abi.STEP_PREVOTE, round_=0)
 
 
-def measured_traffic(config: str):
+def measured_traffic(config: str, kernel: str):
     """HBM bytes per launch of the tally kernel for this workload, from the
     rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this same command committed under
     profiles/ (tools/pmc_traffic.py applies the gfx950 corrections); None if the
     workload has not been profiled."""
     try:
         with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
-            return json.load(f).get(config)
+            rec = json.load(f).get(config)
     except (OSError, ValueError):
         return None
+    # only a record of the kernel that is measured now
+    return rec if rec and kernel in rec.get("kernel_match", "") else None
 
 
 def cpu_baseline(eng, cfg, batch, power, states0, set_of_instance):
@@ -154,11 +169,14 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    eng.kernel_timing(True)  # HIP events around each engine kernel, on `stream`
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(pairs[k])
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    ktimes = eng.kernel_times()
+    eng.kernel_timing(False)
     elapsed = adist.max_over_ranks(elapsed)
     total_votes_step = adist.sum_over_ranks(batch.n_votes)
     if world > 1:
@@ -166,10 +184,21 @@ def main():
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in pairs]))
 
     if rank == 0:
-        traffic = measured_traffic(args.config)
         ms_per_step = elapsed * 1e3 / args.steps
         value = total_votes_step * args.steps / elapsed
-        achieved = BYTES_PER_VOTE * batch.n_votes / (kernel_ms * 1e-3) / 1e9
+        # per-kernel: launches, average ms, algorithmic bytes per launch
+        kernels = {}
+        for name, (launches, total) in ktimes.items():
+            avg = total / max(launches, 1)
+            ab = KERNEL_BYTES_PER_VOTE.get(name, 0) * batch.n_votes
+            kernels[name] = {"launches": launches, "avg_ms": avg, "algorithmic_bytes": ab,
+                             "GBps": ab / (avg * 1e-3) / 1e9 if ab and avg > 0 else None}
+        dom = max(kernels, key=lambda k: kernels[k]["avg_ms"] * kernels[k]["launches"])
+        dom_ms = kernels[dom]["avg_ms"]
+        achieved = KERNEL_BYTES_PER_VOTE[dom] * batch.n_votes / (dom_ms * 1e-3) / 1e9
+        step_kernel_ms = sum(v["avg_ms"] * v["launches"] for v in kernels.values()) / args.steps
+        step_achieved = BYTES_PER_VOTE * batch.n_votes / (step_kernel_ms * 1e-3) / 1e9
+        traffic = measured_traffic(args.config, dom)
         out = {
             "metric": "votes_tallied_per_sec",
             "value": value,
@@ -193,9 +222,15 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic.get("traffic_bytes") if traffic else None,
                          "traffic_source": traffic.get("sources") if traffic else None,
-                         "kernel": "agnes::tally_kernel",
-                         "bytes_per_vote": BYTES_PER_VOTE,
-                         "algorithmic_bytes": BYTES_PER_VOTE * batch.n_votes},
+                         "kernel": KERNEL_SYMBOLS.get(dom, dom),
+                         "kernel_avg_ms": dom_ms,
+                         "bytes_per_vote": KERNEL_BYTES_PER_VOTE[dom],
+                         "algorithmic_bytes": KERNEL_BYTES_PER_VOTE[dom] * batch.n_votes},
+            # the whole hot path (every kernel agnes_tally enqueues) against the same
+            # peak: 15 B/vote algorithmic over the summed kernel time of one step
+            "step_roofline": {"achieved": step_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": step_achieved / HBM_PEAK_GBS, "kernel_ms": step_kernel_ms},
+            "kernels": kernels,
         }
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(eng, cfg, batch, power, st0_host, set_of)

@@ -330,6 +330,20 @@ int agnes_gen_votes_device(agnes_ctx* ctx, const agnes_gen_params* p, const uint
 int agnes_gen_power(uint64_t seed, uint32_t n_sets, uint32_t n_vals, uint32_t kind, int64_t lo,
                     int64_t hi, int64_t* power);
 
+/* Per-kernel timing of the engine's own launches (measurement; off by default).
+ * agnes_kernel_timing(1) clears the records and brackets every kernel the engine
+ * enqueues from then on with HIP events on the caller's stream; (0) stops.
+ * agnes_kernel_times synchronises on the recorded events and writes, per kernel
+ * name in first-launch order, the launch count and total milliseconds. */
+typedef struct agnes_kernel_time {
+    char name[40];
+    uint32_t launches;
+    uint32_t pad;
+    double total_ms;
+} agnes_kernel_time;
+int agnes_kernel_timing(int enable);
+int agnes_kernel_times(agnes_kernel_time* out, uint32_t cap, uint32_t* n);
+
 /* ABI probe */
 uint32_t agnes_abi_version(void);
 
