@@ -31,7 +31,8 @@ struct agnes_ctx {
     unsigned long long* d_err = nullptr;
     hipStream_t last_stream = nullptr;
     bool all_fast = false;     /* every set inside the u32 fast domain */
-    uint32_t* d_list = nullptr; /* [list_cap] deferred instances, then the list counter and
+    uint32_t* d_list = nullptr; /* [list_cap] deferred instances, [list_cap] first-event hints
+                                   (split route), then the list counter and
                                    AGNES_QUEUE_WORDS - 1 work-queue counters */
     uint32_t list_cap = 0;
 };
@@ -270,13 +271,14 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     if (lpw < 0) return (int)lpw;
     AGNES_TRY(hipSetDevice(c->device));
     const bool wide_all = b->weight != nullptr || carry != nullptr || !sets_fast;
-    if (!wide_all && c->list_cap < b->n_instances + AGNES_QUEUE_WORDS) { /* deferred-instance list */
+    if (!wide_all && (!c->d_list || c->list_cap < b->n_instances)) {
+        /* [list_cap] deferred instances | [list_cap] first-event hints | counters */
         AGNES_TRY(hipStreamSynchronize(st));
         if (c->d_list) (void)hipFree(c->d_list);
         c->d_list = nullptr;
         c->list_cap = 0;
-        AGNES_TRY(hipMalloc(&c->d_list, ((size_t)b->n_instances + AGNES_QUEUE_WORDS) * sizeof(uint32_t)));
-        c->list_cap = b->n_instances + AGNES_QUEUE_WORDS;
+        AGNES_TRY(hipMalloc(&c->d_list, (2 * (size_t)b->n_instances + AGNES_QUEUE_WORDS) * sizeof(uint32_t)));
+        c->list_cap = b->n_instances;
     }
     AGNES_TRY(hipMemsetAsync(c->d_err, 0, sizeof(unsigned long long), st));
     agnes_tally_args a;
@@ -294,7 +296,8 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     a.carry = carry;
     a.n_invalid = c->d_err;
     a.list = c->d_list;
-    a.list_count = c->d_list ? c->d_list + (c->list_cap - AGNES_QUEUE_WORDS) : nullptr;
+    a.list_count = c->d_list ? c->d_list + 2 * (size_t)c->list_cap : nullptr;
+    a.hint = c->d_list ? c->d_list + c->list_cap : nullptr; /* used by the split route only */
     /* DEDUP / RoundSkip tables tag entries with (instance epoch, local vote index):
      * the local index of any vote is < n_votes, so it needs bit_length(n_votes - 1) bits */
     if (cfg->mode == AGNES_MODE_DEDUP || (cfg->flags & AGNES_FLAG_ROUND_SKIP)) {

@@ -38,7 +38,7 @@ constexpr uint32_t NOPOS = 0xFFFFFFFFu;
  * buffered): a block is one half of an L2 line, consumed before the next block
  * is needed, so a line is fetched once although the 64 lanes of a wave read 64
  * different lines.  LDS per wave: [stage 2][column 2][k 4][lane 64][16 B]. */
-constexpr uint32_t BLK = 64u, LDS_PER_WAVE = 2u * 2u * 4u * 64u * 16u, WAVES = 4u;
+constexpr uint32_t BLK = 64u, LDS_PER_WAVE = 2u * 4u * 64u * 16u, WAVES = 4u;
 
 /* the bytes of a 16-B window that runs past the batch end, into the lane's slot
  * (the batch's last instance only) */
@@ -87,13 +87,53 @@ __device__ uint32_t label_of(const agnes_tally_args& a, uint64_t lo, uint64_t j)
     if (a.dbg & 16u) return 0u; /* development knob 16: no label reads */
     const uint32_t v = a.vb.value[j];
     if (v != AGNES_NIL) return v;
-    const uint8_t r = a.vb.round[j], t = a.vb.type[j];
-    for (uint64_t k = j; k-- > lo;) {
-        const uint32_t ev = a.codes[k] & AGNES_CODE_EVENT_MASK;
-        if (a.vb.round[k] == r && a.vb.type[k] == t && ev != AGNES_CODE_INVALID && ev != AGNES_CODE_REJECTED) {
-            const uint32_t u = a.vb.value[k];
-            if (u != AGNES_NIL) return u;
+    const uint32_t r = a.vb.round[j], t = a.vb.type[j];
+    /* 16 votes per round trip, newest window first (aligned 16-vote windows of the
+     * columns; a window straddling lo is read byte-wise) */
+    for (uint64_t w = j & ~15ull;; w -= 16u) {
+        const uint64_t b = w > lo ? w : lo;
+        const uint64_t e = w + 16u < j ? w + 16u : j;
+        if (b < e) {
+            uint32_t cand = 0, vals[16];
+            if (b == w && e == w + 16u) {
+                const uint4 rq = *reinterpret_cast<const uint4*>(a.vb.round + w);
+                const uint4 tq = *reinterpret_cast<const uint4*>(a.vb.type + w);
+                const uint4 cq = *reinterpret_cast<const uint4*>(a.codes + w);
+                const uint4* vq = reinterpret_cast<const uint4*>(a.vb.value + w);
+                const uint4 vv4[4] = {vq[0], vq[1], vq[2], vq[3]};
+                const uint32_t rr[4] = {rq.x, rq.y, rq.z, rq.w}, tt[4] = {tq.x, tq.y, tq.z, tq.w};
+                const uint32_t cc[4] = {cq.x, cq.y, cq.z, cq.w};
+#pragma unroll
+                for (uint32_t q = 0; q < 16u; ++q) {
+                    const uint32_t sh = 8u * (q & 3u);
+                    const uint32_t ev = (cc[q >> 2] >> sh) & AGNES_CODE_EVENT_MASK;
+                    const uint4 vx = vv4[q >> 2];
+                    vals[q] = (q & 3u) == 0u ? vx.x : (q & 3u) == 1u ? vx.y : (q & 3u) == 2u ? vx.z : vx.w;
+                    cand |= (uint32_t)(((rr[q >> 2] >> sh) & 0xFFu) == r && ((tt[q >> 2] >> sh) & 0xFFu) == t &&
+                                       ev != AGNES_CODE_INVALID && ev != AGNES_CODE_REJECTED && vals[q] != AGNES_NIL)
+                            << q;
+                }
+            } else {
+                for (uint32_t q = 0; q < 16u; ++q) {
+                    const uint64_t k = w + q;
+                    vals[q] = 0u;
+                    if (k < b || k >= e) continue;
+                    const uint32_t ev = a.codes[k] & AGNES_CODE_EVENT_MASK;
+                    vals[q] = a.vb.value[k];
+                    cand |= (uint32_t)(a.vb.round[k] == r && a.vb.type[k] == t && ev != AGNES_CODE_INVALID &&
+                                       ev != AGNES_CODE_REJECTED && vals[q] != AGNES_NIL)
+                            << q;
+                }
+            }
+            if (cand) {
+                const uint32_t q = 31u - (uint32_t)__builtin_clz(cand);
+                uint32_t out = vals[0];
+#pragma unroll
+                for (uint32_t x = 1; x < 16u; ++x) out = x == q ? vals[x] : out;
+                return out;
+            }
         }
+        if (w <= lo) break;
     }
     return 0u;
 }
@@ -103,24 +143,29 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n = a.vb.n_instances, ns = a.n_sets;
     if (i >= n) return;
-    const uint64_t NV = a.vb.n_votes;
+    /* every per-instance input at once (one latency, not a chain) */
+    uint4* const sp = reinterpret_cast<uint4*>(a.states + i);
+    const uint32_t hint = a.hint ? a.hint[i] : 0u;
     uint64_t lo = a.vb.offsets[i], hi = a.vb.offsets[i + 1u];
+    const uint4 s0 = sp[0], s1 = sp[1], s2 = sp[2], s3 = sp[3];
+    /* the stream tally's first-event hint: no event (or deferred to the LIST kernel):
+     * nothing to apply; else the walk starts there — earlier votes have no event */
+    if (hint == AGNES_NOHINT) return;
+    const uint64_t NV = a.vb.n_votes;
     lo = lo < NV ? lo : NV;
     hi = hi < NV ? hi : NV;
     if (hi <= lo) return;
-    /* the same u32-domain test as the tally kernels: the rest is the LIST kernel's */
-    const uint32_t set = a.vb.instance_set ? a.vb.instance_set[i] : (ns ? i % ns : 0u);
-    if (set < ns) {
-        const agnes_set_info si = a.sets[set];
-        const uint64_t len = hi - lo;
-        if (!si.fast || len >= (1ull << 32) || len * (uint64_t)si.maxpow >= (1ull << 31)) return;
+    if (!a.hint) { /* the same u32-domain test as the tally kernels: the rest is the LIST kernel's */
+        const uint32_t set = a.vb.instance_set ? a.vb.instance_set[i] : (ns ? i % ns : 0u);
+        if (set < ns) {
+            const agnes_set_info si = a.sets[set];
+            const uint64_t len = hi - lo;
+            if (!si.fast || len >= (1ull << 32) || len * (uint64_t)si.maxpow >= (1ull << 31)) return;
+        }
     }
 
-    uint4* const sp = reinterpret_cast<uint4*>(a.states + i);
-    const uint4 s3 = sp[3];
     const uint32_t step0 = s3.y & 0xFFu; /* dword 13: step | locked << 8 | valid << 16 | decided << 24 */
     if (step0 == AGNES_STEP_COMMIT) return; /* :205 every later event: None */
-    const uint4 s0 = sp[0];
     const int64_t round0 = (int64_t)(((uint64_t)s0.w << 32) | s0.z);
     uint32_t step = step0;
     uint32_t eq8 = (round0 >= 0 && round0 <= 255) ? (uint32_t)round0 : 0x100u; /* no u8 round equals 0x100 */
@@ -238,32 +283,27 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
     const uint32_t lane = threadIdx.x & 63u;
     unsigned char* const wbase = agnes_smem + rfl(threadIdx.x >> 6) * LDS_PER_WAVE; /* wave-uniform: m0 */
     const uint64_t wmax = (NV & ~15ull) - 16u; /* the last window fully inside [0, NV) */
-    auto issue = [&](uint32_t stg, uint64_t blk) {
+    /* single-buffered: with the hint a walk is one or two blocks, and 8 KB per wave
+     * keeps 20 waves per CU resident to cover the latency instead */
+    auto issue = [&](uint64_t blk) {
 #pragma unroll
         for (uint32_t k = 0; k < 4u; ++k) {
             const uint64_t w = blk + 16u * k;
             const uint64_t ws = w <= wmax ? w : wmax;
-            fast::glds16(a.codes + ws, wbase + ((stg * 2u + 0u) * 4u + k) * 1024u);
-            fast::glds16(a.vb.round + ws, wbase + ((stg * 2u + 1u) * 4u + k) * 1024u);
+            fast::glds16(a.codes + ws, wbase + k * 1024u);
+            fast::glds16(a.vb.round + ws, wbase + (4u + k) * 1024u);
         }
     };
-    uint64_t blk = lo & ~(uint64_t)(BLK - 1u);
-    uint32_t stg = 0;
-    issue(0u, blk);
+    uint64_t blk = (lo + hint) & ~(uint64_t)(BLK - 1u);
+    issue(blk);
     for (;;) {
-        const uint64_t nb = blk + BLK;
-        const bool more = nb < hi;
-        const bool any_more = __builtin_amdgcn_ballot_w64(more) != 0ull;
-        if (more) issue(stg ^ 1u, nb);
-        /* this block's DMA: everything but the (wave-level) 8 just issued */
-        if (any_more) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else fast::dma_wait();
+        fast::dma_wait();
 #pragma unroll 1
         for (uint32_t k = 0; k < 4u; ++k) {
             const uint64_t w = blk + 16u * k;
             if (w >= hi) break;
-            unsigned char* const cs = wbase + ((stg * 2u + 0u) * 4u + k) * 1024u + 16u * lane;
-            unsigned char* const rs = wbase + ((stg * 2u + 1u) * 4u + k) * 1024u + 16u * lane;
+            unsigned char* const cs = wbase + k * 1024u + 16u * lane;
+            unsigned char* const rs = wbase + (4u + k) * 1024u + 16u * lane;
             if (w + 16u > lo && w > wmax) { /* past the batch end: the real bytes */
                 tail_fill(a.codes, w, NV, cs);
                 tail_fill(a.vb.round, w, NV, rs);
@@ -272,9 +312,10 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
                 walk(w, *reinterpret_cast<const uint4*>(cs), *reinterpret_cast<const uint4*>(rs));
             if (step == AGNES_STEP_COMMIT) break;
         }
-        if (!more || step == AGNES_STEP_COMMIT) break;
+        const uint64_t nb = blk + BLK;
+        if (nb >= hi || step == AGNES_STEP_COMMIT) break;
+        issue(nb); /* this block's LDS reads are consumed: the slot is free */
         blk = nb;
-        stg ^= 1u;
     }
     /* the wave's other lanes may still be streaming: nothing of this lane's in flight */
     fast::dma_wait();
@@ -283,29 +324,34 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
     /* the State back: round (RoundSkip), locked, valid, decision, step/flags.  Only
      * the starting round can see Polka events: a RoundSkip leaves NewRound, where
      * vote events change nothing but a commit (:196-211) */
-    const uint4 s1 = sp[1], s2 = sp[2];
     uint32_t d[16] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w, s2.x, s2.y, s2.z, s2.w, s3.x, s3.y, s3.z, s3.w};
     uint32_t flags = s3.y;
     if (skipped) {
         d[2] = eq8; /* the last RoundSkip's round */
         d[3] = 0u;
     }
+    /* the three value sources: their votes' values in one round trip, the bucket
+     * search only for a nil one */
+    uint32_t lv = 0, vv = 0, dv = 0;
+    if (lock_at != NOPOS) lv = a.vb.value[lo + lock_at];
+    if (valid_at != NOPOS) vv = a.vb.value[lo + valid_at];
+    if (dec_at != NOPOS) dv = a.vb.value[lo + dec_at];
     if (lock_at != NOPOS) {
         d[4] = s0.z;
         d[5] = s0.w;
-        d[10] = label_of(a, lo, lo + lock_at);
+        d[10] = lv != AGNES_NIL ? lv : label_of(a, lo, lo + lock_at);
         flags |= 1u << 8;
     }
     if (valid_at != NOPOS) {
         d[6] = s0.z;
         d[7] = s0.w;
-        d[11] = valid_at == lock_at ? d[10] : label_of(a, lo, lo + valid_at);
+        d[11] = valid_at == lock_at ? d[10] : (vv != AGNES_NIL ? vv : label_of(a, lo, lo + valid_at));
         flags |= 1u << 16;
     }
     if (dec_at != NOPOS) {
         d[8] = dec_round;
         d[9] = 0u;
-        d[12] = label_of(a, lo, lo + dec_at);
+        d[12] = dv != AGNES_NIL ? dv : label_of(a, lo, lo + dec_at);
         flags |= 1u << 24;
     }
     d[13] = (flags & ~0xFFu) | step;
@@ -322,7 +368,8 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
 
 bool agnes_apply_codes_supported(const agnes_tally_args* a) {
     /* 16-B windows of the u8 columns */
-    return ((reinterpret_cast<uintptr_t>(a->codes) | reinterpret_cast<uintptr_t>(a->vb.round)) & 15u) == 0u &&
+    return ((reinterpret_cast<uintptr_t>(a->codes) | reinterpret_cast<uintptr_t>(a->vb.round) |
+             reinterpret_cast<uintptr_t>(a->vb.type)) & 15u) == 0u &&
            a->vb.n_votes >= 32u && a->states != nullptr && (a->flags & AGNES_FLAG_STATE_MACHINE) != 0;
 }
 

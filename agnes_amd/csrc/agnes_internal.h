@@ -51,7 +51,11 @@ typedef struct agnes_tally_args {
     uint32_t set_cache;   /* bytes of block LDS caching the set constants (0: read them from HBM);
                              set by the launcher only when it costs no occupancy */
     uint32_t power_cache; /* bytes of block LDS holding the u32 power table (0: gather from HBM) */
+    uint32_t* hint;       /* [n_instances] split route: position of the instance's first vote with
+                             an event (relative to its first vote), AGNES_NOHINT if none or if the
+                             instance was deferred to the LIST kernel; nullptr: not recorded */
 } agnes_tally_args;
+#define AGNES_NOHINT 0xFFFFFFFFu
 
 /* agnes_kernel_timing: HIP events around each launch while enabled (agnes_api.cpp) */
 extern "C" void agnes_kt_mark(const char* name, hipStream_t st, bool begin);

@@ -1198,6 +1198,9 @@ static hipError_t launch_mode(const agnes_tally_args* a, uint32_t lpw, int num_c
                            (stream ? apply_lvl >= 1 : apply_lvl == 2);
         agnes_tally_args b = *a;
         if (split) b.flags &= ~AGNES_FLAG_STATE_MACHINE;
+        /* first-event hints: the stream kernel records them for the apply pass */
+        const bool hints = split && stream && a->hint != nullptr;
+        if (!hints) b.hint = nullptr;
         if (stream && (!SM || fused_stream || split)) {
             AgnesKt kt("tally_stream", st);
             e = agnes_launch_tally_stream(&b, num_cus, st);
@@ -1207,7 +1210,9 @@ static hipError_t launch_mode(const agnes_tally_args* a, uint32_t lpw, int num_c
         }
         if (e == hipSuccess && split) {
             AgnesKt kt("apply_codes", st);
-            e = agnes_launch_apply_codes(a, st);
+            agnes_tally_args ap = *a;
+            ap.hint = hints ? a->hint : nullptr;
+            e = agnes_launch_apply_codes(&ap, st);
         }
     }
     if (e == hipSuccess) {

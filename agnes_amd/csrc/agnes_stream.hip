@@ -45,7 +45,7 @@ constexpr uint32_t SMALL = 4u; /* batch size of the work queue's tail           
  * (state machine) the current batch's States */
 __host__ __device__ inline uint32_t carry_words(uint32_t R) { return (uint32_t)(align16(16ull * R) / 4u); }
 __host__ __device__ inline uint32_t lds_bytes(bool sm, uint32_t R) {
-    return PF_BYTES + 8u * carry_words(R) + (sm ? SBQ * 64u + SBQ * 32u : 0u);
+    return PF_BYTES + 8u * carry_words(R) + SBQ * 4u + (sm ? SBQ * 64u + SBQ * 32u : 0u);
 }
 
 /* State::apply shadow of a batch instance (LDS, 8 dwords): what the votes did to
@@ -107,7 +107,8 @@ __global__ __launch_bounds__(256) AGNES_STREAM_ATTR void tally_stream(agnes_tall
     unsigned char* const pfb = base;
     uint32_t* const crow = reinterpret_cast<uint32_t*>(base + PF_BYTES);
     const uint32_t cw = carry_words(R); /* one copy: vw[2R] then vn[2R] */
-    unsigned char* const sb = base + PF_BYTES + 8u * cw;
+    uint32_t* const hs = reinterpret_cast<uint32_t*>(base + PF_BYTES + 8u * cw); /* first-event hints */
+    unsigned char* const sb = base + PF_BYTES + 8u * cw + SBQ * 4u;
     uint32_t* const shw = reinterpret_cast<uint32_t*>(sb + SBQ * 64u); /* State::apply shadows */
     uint32_t cpar = 0;
     uint64_t pf_at = ~0ull;
@@ -246,6 +247,7 @@ __global__ __launch_bounds__(256) AGNES_STREAM_ATTR void tally_stream(agnes_tall
         const uint32_t m = H.e0 - H.s0;
         const bool S = H.stream;
         bool fresh = true; /* the batch's first chunk step */
+        if (a.hint && lane < SBQ) hs[lane] = AGNES_NOHINT;
         bool smf = SM;     /* the shadows are not yet set up from the staged States */
         uint32_t si = 0;
         for (;;) { /* streams of the batch: one (stream batch) or one per instance */
@@ -428,6 +430,7 @@ __global__ __launch_bounds__(256) AGNES_STREAM_ATTR void tally_stream(agnes_tall
                     __builtin_amdgcn_wave_barrier();
                 }
                 const uint32_t q2s = D ? shfl(H.q2, HI + segk) : rdl(H.q2, HI + k0);
+                const uint32_t qd = D ? shfl(q2s, dl) : q2s; /* the q2 of the lane's own segment */
 
                 /* K2+K3 per (round, type) bucket present: one stream-order scan of its value
                  * and nil weights over the chunk (VoteCount::add_vote, round_votes.rs:48-56)
@@ -461,7 +464,6 @@ __global__ __launch_bounds__(256) AGNES_STREAM_ATTR void tally_stream(agnes_tall
                     if (D == 0u) {
                         tv = (int32_t)(q2s - cv - exv);
                         tn = (int32_t)(q2s - cn - exn);
-                        ta = (int32_t)(q2s - cv - cn - exv - exn);
                     } else {
                         /* the lane before segment d's first; the shuffles run in every lane
                          * (a lane outside a ds_bpermute's exec mask reads as 0 to the others) */
@@ -473,10 +475,11 @@ __global__ __launch_bounds__(256) AGNES_STREAM_ATTR void tally_stream(agnes_tall
                         const uint32_t Tn = q2s + bn - (lane == 0u ? cn : 0u);
                         tv = (int32_t)(shfl(Tv, dl) - exv);
                         tn = (int32_t)(shfl(Tn, dl) - exn);
-                        ta = (int32_t)(shfl(Tv + Tn - q2s, dl) - exv - exn);
                         bvl = rdl(bv, D);
                         bnl = rdl(bn, D);
                     }
+                    /* value + nil > q2: the two thresholds' sum less one q2 (mod 2^32) */
+                    ta = (int32_t)((uint32_t)tv + (uint32_t)tn - qd);
                     if (K & 1u) { /* precommits: Value -> PrecommitValue, Nil -> None, Any -> PrecommitAny */
 #pragma unroll
                         for (uint32_t s = 0; s < VPL; ++s) {
@@ -518,6 +521,18 @@ __global__ __launch_bounds__(256) AGNES_STREAM_ATTR void tally_stream(agnes_tall
                  * Segments start at lane boundaries, so all of it is lane-parallel: byte
                  * masks per lane, "earlier in my segment" from two ballots, the results
                  * into the instance's LDS shadow (rare: a nil vote's label, label_at). */
+                /* the split route's first-event hint: the earliest vote of each instance
+                 * whose code carries an event (1..5); apply_codes starts its walk there */
+                if (!SM && a.hint) {
+                    uint32_t fs = VPL;
+#pragma unroll
+                    for (int s2 = (int)VPL - 1; s2 >= 0; --s2) {
+                        const uint32_t ev = code[s2] & 7u;
+                        if (ev != 0u && ev <= AGNES_CODE_PRECOMMIT_VALUE) fs = (uint32_t)s2;
+                    }
+                    const uint32_t ilo = D ? shfl(H.olo, kln) : rdl(H.olo, k0); /* low 32 bits of its start */
+                    if (fs < VPL) atomicMin(hs + kln, (uint32_t)c + p0 + fs - ilo);
+                }
                 uint32_t smmsg = 0;
                 if (SM) {
                     if (smf) { /* the batch's staged States have landed (dma_wait above) */
@@ -668,6 +683,7 @@ __global__ __launch_bounds__(256) AGNES_STREAM_ATTR void tally_stream(agnes_tall
                 __builtin_amdgcn_wave_barrier();
             }
         }
+        if (a.hint && lane < m) a.hint[H.s0 + lane] = hs[lane];
         /* batch end: the shadows into the staged States, States back, then the next batch */
         if (SM && !smf && lane < m) {
             const uint32_t* const sh = shw + 8u * lane;
