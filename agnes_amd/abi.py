@@ -32,6 +32,7 @@ CODE_EVENT_MASK, CODE_SKIP, CODE_MSG_SHIFT = 0x07, 0x08, 4
 
 MODE_REFERENCE, MODE_DEDUP = 0, 1
 FLAG_ROUND_SKIP, FLAG_STATE_MACHINE, FLAG_DISTINCT_VALUES = 0x1, 0x2, 0x4
+FLAG_ONE_INSTANCE = 0x8  # agnes_tally_carried: segments are slices of one instance (id cfg.reserved)
 
 ORDER_SHUFFLED, ORDER_PHASED, ORDER_SORTED = 0, 1, 2
 POWER_UNIFORM, POWER_ZIPF, POWER_EQUAL = 0, 1, 2
@@ -114,7 +115,10 @@ EVENT_DTYPE = np.dtype([("round", "<i8"), ("pol_round", "<i8"), ("value", "<u4")
 MESSAGE_DTYPE = np.dtype([("round", "<i8"), ("pol_round", "<i8"), ("value", "<u4"),
                           ("kind", "u1"), ("vote_type", "u1"), ("timeout_step", "u1"),
                           ("pad", "u1")])
+VOTE_COUNT_DTYPE = np.dtype([("value_w", "<i8"), ("nil_w", "<i8"), ("value", "<u4"),
+                             ("reserved", "<u4")])  # agnes_vote_count
 assert STATE_DTYPE.itemsize == 64 and EVENT_DTYPE.itemsize == 24 and MESSAGE_DTYPE.itemsize == 24
+assert VOTE_COUNT_DTYPE.itemsize == 24
 
 
 def gen_params(seed=0xA6E5, n_instances=1, n_vals=4, rounds_min=1, rounds_max=1, nil_permille=0,
@@ -124,8 +128,8 @@ def gen_params(seed=0xA6E5, n_instances=1, n_vals=4, rounds_min=1, rounds_max=1,
                      dup_permille, equiv_permille, higher_permille, order, instance_base)
 
 
-def config(mode=MODE_REFERENCE, flags=0, max_rounds=1) -> Config:
-    return Config(mode, flags, max_rounds, 0)
+def config(mode=MODE_REFERENCE, flags=0, max_rounds=1, reserved=0) -> Config:
+    return Config(mode, flags, max_rounds, reserved)
 
 
 def new_states(n: int, height: int = 1, step: int = STEP_NEW_ROUND, round_: int = 0) -> np.ndarray:

@@ -87,7 +87,7 @@ agnes_set_info set_info(const int64_t* pw, uint32_t n_vals, int64_t total) {
 bool cfg_ok(const agnes_config* cfg) {
     return cfg && cfg->max_rounds >= 1 && cfg->max_rounds <= 256 && cfg->mode <= AGNES_MODE_DEDUP &&
            (cfg->flags & ~(AGNES_FLAG_ROUND_SKIP | AGNES_FLAG_STATE_MACHINE |
-                           AGNES_FLAG_DISTINCT_VALUES)) == 0;
+                           AGNES_FLAG_DISTINCT_VALUES | AGNES_FLAG_ONE_INSTANCE)) == 0;
 }
 
 /* ---- scalar mirror: one process-wide context ---- */
@@ -291,6 +291,8 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     a.n_vals = c->n_vals;
     a.max_rounds = cfg->max_rounds;
     a.flags = cfg->flags;
+    a.one_inst = (cfg->flags & AGNES_FLAG_ONE_INSTANCE) ? 1u : 0u;
+    a.one_id = cfg->reserved;
     a.codes = codes;
     a.states = (cfg->flags & AGNES_FLAG_STATE_MACHINE) ? states : nullptr;
     a.carry = carry;
@@ -320,9 +322,20 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
 
 int agnes_tally(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint8_t* codes,
                 agnes_state* states, void* stream) {
-    if (!c) return AGNES_E_INVALID;
+    if (!c || !cfg || (cfg->flags & AGNES_FLAG_ONE_INSTANCE)) return AGNES_E_INVALID; /* needs counts */
     return tally_impl(c, cfg, b, codes, states, nullptr, c->d_sets, c->n_sets, c->all_fast,
                       (hipStream_t)stream);
+}
+
+static_assert(sizeof(agnes_vote_count) == sizeof(agnes_carry_rec), "agnes_vote_count is the carried executor");
+
+int agnes_tally_carried(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint8_t* codes,
+                        agnes_vote_count* counts, void* stream) {
+    if (!c || !cfg || !b || (b->n_instances && !counts)) return AGNES_E_INVALID;
+    if (cfg->mode != AGNES_MODE_REFERENCE || (cfg->flags & (AGNES_FLAG_ROUND_SKIP | AGNES_FLAG_STATE_MACHINE)))
+        return AGNES_E_UNSUPPORTED;
+    return tally_impl(c, cfg, b, codes, nullptr, reinterpret_cast<agnes_carry_rec*>(counts), c->d_sets,
+                      c->n_sets, c->all_fast, (hipStream_t)stream);
 }
 
 int agnes_last_error_count(agnes_ctx* c, uint64_t* out) {

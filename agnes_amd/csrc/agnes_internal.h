@@ -51,6 +51,8 @@ typedef struct agnes_tally_args {
     uint32_t set_cache;   /* bytes of block LDS caching the set constants (0: read them from HBM);
                              set by the launcher only when it costs no occupancy */
     uint32_t power_cache; /* bytes of block LDS holding the u32 power table (0: gather from HBM) */
+    uint32_t one_inst;    /* AGNES_FLAG_ONE_INSTANCE: every segment is a slice of instance one_id */
+    uint32_t one_id;
     uint32_t* hint;       /* [n_instances] split route: position of the instance's first vote with
                              an event (relative to its first vote), AGNES_NOHINT if none or if the
                              instance was deferred to the LIST kernel; nullptr: not recorded */

@@ -510,7 +510,7 @@ __device__ __forceinline__ void prep_chunk(const agnes_tally_args& a, const Inst
         /* bitwise, not short-circuit: no divergent branches */
         const uint32_t valid = (uint32_t)(p0 + s >= lo) & (uint32_t)(p0 + s < hi);
         const uint32_t vidx_ok = need_val ? ((uint32_t)set_ok & (uint32_t)(x.val[s] < nv)) : 1u;
-        const uint32_t ok = valid & (uint32_t)(x.inst[s] == in_.i) & (uint32_t)(P.rr[s] < R) &
+        const uint32_t ok = valid & (uint32_t)(x.inst[s] == (a.one_inst ? a.one_id : in_.i)) & (uint32_t)(P.rr[s] < R) &
                             (uint32_t)(P.tt[s] <= 1u) & vidx_ok & (uint32_t)vote_ok_u;
         bad_lane += valid & (ok ^ 1u);
         P.f_valid |= valid << s;
@@ -898,7 +898,7 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
     auto load_hdr = [&](uint32_t k) -> uint32_t {
         uint32_t h = 0;
         if (lane < 4u) h = reinterpret_cast<const uint32_t*>(vb.offsets + k)[lane];
-        else if (lane == 4u) h = vb.instance_set ? vb.instance_set[k] : (ns ? k % ns : 0u);
+        else if (lane == 4u) h = vb.instance_set ? vb.instance_set[k] : (ns ? (a.one_inst ? a.one_id : k) % ns : 0u);
         else if (SM && lane >= 16u && lane < 30u) h = reinterpret_cast<const uint32_t*>(&a.states[k])[lane - 16u];
         return h;
     };

@@ -114,5 +114,93 @@ def gather_decisions(local: np.ndarray, group=None) -> np.ndarray:
     return np.concatenate(parts) if parts else local
 
 
+# ---------------------------------------------------------------------------
+# C5: ONE instance split into contiguous stream slices — the
+# path's one real exchange step.  is_quorum (round_votes.rs:31-33) needs the
+# exact running sum at every vote, so a slice can only be tallied once the
+# weights of every vote before it are known: each slice first computes its own
+# partial VoteCounts, one all_gather of the K x 3 int64 slice totals gives every
+# rank the sum of the ranks before it, and each slice is tallied again from its
+# exact carry-in.
+
+NIL = abi.NIL
+
+
+def segment_offsets(n_votes: int, n_segments: int, align: int = 4) -> np.ndarray:
+    """Boundaries (n_segments + 1, u64) of balanced contiguous slices of one
+    instance's votes, multiples of `align` (a slice starts on a lane boundary)."""
+    k = np.arange(n_segments + 1, dtype=np.int64)
+    b = (k * n_votes // n_segments) // align * align
+    b[-1] = n_votes
+    return b.astype(np.uint64)
+
+
+def fold_counts(w: torch.Tensor, lab: torch.Tensor):
+    """Folds of consecutive VoteCount partials along dim 0 (slices in stream order):
+    weights add (i64, wrapping like the reference's release build), the label is
+    the last slice's that wrote a value (round_votes.rs:50-54; NIL = none).
+    w int64 [S, K, 2], lab int64 [S, K] -> (exclusive w, exclusive lab, total w
+    [K, 2], total lab [K])."""
+    S = w.shape[0]
+    incl = torch.cumsum(w, dim=0)
+    excl = incl - w
+    idx = torch.arange(S, device=w.device, dtype=torch.int64).view(S, 1).expand_as(lab)
+    last = torch.cummax(torch.where(lab != NIL, idx, torch.full_like(idx, -1)), dim=0).values
+    prev = torch.cat([torch.full_like(last[:1], -1), last[:-1]], dim=0)
+
+    def pick(at):
+        g = torch.gather(lab, 0, at.clamp(min=0))
+        return torch.where(at >= 0, g, torch.full_like(g, NIL))
+
+    return excl, pick(prev), incl[-1], pick(last)[-1]
+
+
+def tally_one_instance(tally_carried, n_votes: int, cfg: abi.Config, n_segments: int, device,
+                       inst_id: int = 0, group=None, prior=None):
+    """C5 driver.  This rank holds a contiguous slice (n_votes votes) of ONE
+    instance's stream; ranks hold consecutive slices in rank order.  The slice is
+    cut into n_segments segments (one wave each) and tallied twice:
+      A. every segment from an empty executor -> its partial (value_w, nil_w,
+         label) per (round, type), the label NIL when it wrote none;
+      exchange: ONE all_gather of the slice totals (K x 3 int64 per rank; RCCL
+         over xGMI, gloo in the CPU tests) -> the ranks before this one;
+      B. every segment from its carry-in (prior, ranks before, segments before)
+         -> per-vote codes identical to tallying the instance as one stream.
+    tally_carried(cfg, offsets int64 [S + 1] on `device`, counts int64 [S, K, 3])
+    runs agnes_tally_carried on the slice.  prior: the instance's (w [K, 2], label
+    [K]) before this call (a stream continued across calls), None = RoundVotes::new.
+    Returns the instance's (w, label) after every rank's votes."""
+    K = 2 * cfg.max_rounds
+    S = max(1, min(n_segments, max(1, n_votes // 4)))
+    off = torch.from_numpy(segment_offsets(n_votes, S).view(np.int64)).to(device)
+    one = abi.Config(cfg.mode, cfg.flags | abi.FLAG_ONE_INSTANCE, cfg.max_rounds, inst_id)
+    counts = torch.zeros((S, K, 3), dtype=torch.int64, device=device)
+    counts[..., 2] = NIL
+    tally_carried(one, off, counts)                                    # pass A
+    ex_w, ex_lab, tot_w, tot_lab = fold_counts(counts[..., :2], counts[..., 2] & 0xFFFFFFFF)
+    mine = torch.cat([tot_w, tot_lab.unsqueeze(-1)], dim=-1)           # [K, 3]
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        t = mine.to(_device_for(group))
+        parts = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(parts, t, group=group)                         # the exchange step
+        ranks = torch.stack(parts).to(device)
+    else:
+        rank, ranks = 0, mine.unsqueeze(0)
+    if prior is not None:
+        pw, pl = prior
+        pl = torch.where(pl == 0, torch.full_like(pl, NIL), pl)  # "no value yet" and label 0 fold alike
+        ranks = torch.cat([torch.cat([pw, pl.unsqueeze(-1)], dim=-1).unsqueeze(0).to(device), ranks])
+        rank += 1
+    r_w, r_lab, fin_w, fin_lab = fold_counts(ranks[..., :2], ranks[..., 2])
+    in_w = ex_w + r_w[rank].unsqueeze(0)
+    in_lab = torch.where(ex_lab != NIL, ex_lab, r_lab[rank].unsqueeze(0).expand_as(ex_lab))
+    in_lab = torch.where(in_lab == NIL, torch.zeros_like(in_lab), in_lab)  # VoteCount::new's label
+    counts = torch.cat([in_w, in_lab.unsqueeze(-1)], dim=-1).contiguous()
+    tally_carried(one, off, counts)                                    # pass B
+    return fin_w, torch.where(fin_lab == NIL, torch.zeros_like(fin_lab), fin_lab)
+
+
 __all__ = ["env", "shard_range", "Shard", "make_shard", "set_of_instances", "max_over_ranks",
-           "sum_over_ranks", "decisions", "gather_decisions", "DECISION_DTYPE"]
+           "sum_over_ranks", "decisions", "gather_decisions", "DECISION_DTYPE", "segment_offsets",
+           "fold_counts", "tally_one_instance"]

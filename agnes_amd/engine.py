@@ -131,6 +131,19 @@ class Engine:
         check(self.lib.agnes_tally(self.ctx, C.byref(cfg), C.byref(b), _ptr(codes), _ptr(states),
                                    _stream_handle(stream)), "agnes_tally")
 
+    def tally_carried(self, cfg: abi.Config, batch: DeviceBatch, codes: torch.Tensor,
+                      counts: torch.Tensor, stream=None):
+        """agnes_tally_carried: counts = int64 tensor [n_instances, 2 * max_rounds, 3]
+        (agnes_vote_count records: value_w, nil_w, value | reserved << 32), in/out."""
+        if codes.dtype != torch.uint8 or codes.numel() < batch.n_votes:
+            raise ValueError("codes must be a uint8 tensor of n_votes")
+        if (counts.dtype != torch.int64 or not counts.is_contiguous()
+                or counts.numel() < batch.n_instances * 2 * cfg.max_rounds * 3):
+            raise ValueError("counts must be a contiguous int64 [n_instances, 2R, 3] tensor")
+        b = batch.c()
+        check(self.lib.agnes_tally_carried(self.ctx, C.byref(cfg), C.byref(b), _ptr(codes), _ptr(counts),
+                                           _stream_handle(stream)), "agnes_tally_carried")
+
     def last_error_count(self) -> int:
         v = C.c_uint64(0)
         check(self.lib.agnes_last_error_count(self.ctx, C.byref(v)), "agnes_last_error_count")

@@ -67,6 +67,11 @@ WORKLOADS = {
                         higher_permille=50),
                power=(abi.POWER_ZIPF, 1, 1_000_000, 1024), mode=abi.MODE_DEDUP,
                flags=abi.FLAG_STATE_MACHINE | abi.FLAG_ROUND_SKIP, max_rounds=5, scaling="weak"),
+    "c5": dict(desc="C5: 1 instance x 1M validators (Zipf power), prevote + precommit: 2e6 votes in one "
+                    "stream, split over ranks and per rank over segments; one all_gather of partial tallies",
+               gen=dict(n_instances=1, n_vals=1_000_000, rounds_min=1, rounds_max=1, nil_permille=200),
+               power=(abi.POWER_ZIPF, 1, 1_000_000, 1), mode=abi.MODE_REFERENCE, flags=0,
+               max_rounds=1, scaling="strong", one_instance=True, segments=1024),
 }
 
 
@@ -134,6 +139,8 @@ def main():
 
     w = WORKLOADS[args.config]
     eng = Engine(local)
+    if w.get("one_instance"):
+        return bench_one_instance(args, w, eng, rank, world)
     shard = adist.make_shard(w["gen"], rank, world, strong=w["scaling"] == "strong")
     p = shard.params
     kind, lo, hi, n_sets = w["power"]
@@ -240,6 +247,102 @@ def main():
                 # the bench codes come from the LAST step; states were reset each step
                 out["cpu_check_equal"] = bool(np.array_equal(g, prefix))
             out["cpu_baseline"] = cb
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_one_instance(args, w, eng, rank, world):
+    """C5: one instance's stream split over ranks (agnes_amd/dist.py
+    tally_one_instance): two carried-tally passes + one all_gather per step."""
+    import dataclasses
+    from agnes_amd.engine import DeviceBatch
+    p = abi.gen_params(seed=0xA6E5, **w["gen"])
+    kind, plo, phi, n_sets = w["power"]
+    power = eng.gen_power(0xA6E5, n_sets, p.n_vals, kind, plo, phi)
+    eng.upload_power(power)
+    stream = torch.cuda.current_stream()
+    whole = eng.gen_batch(p)  # the whole instance on every rank (generation is not timed)
+    n = whole.n_votes
+    lo = (n * rank // world) // 4 * 4
+    hi = n if rank == world - 1 else (n * (rank + 1) // world) // 4 * 4
+    batch = DeviceBatch(whole.instance[lo:hi], whole.round[lo:hi], whole.type[lo:hi],
+                        whole.value[lo:hi], whole.validator[lo:hi],
+                        torch.tensor([0, hi - lo], dtype=torch.int64, device=eng.device), n_votes=hi - lo)
+    codes = torch.empty(max(hi - lo, 1), dtype=torch.uint8, device=eng.device)
+    cfg = abi.config(w["mode"], w["flags"], w["max_rounds"])
+
+    def tc(one, off, counts):
+        eng.tally_carried(one, dataclasses.replace(batch, offsets=off), codes, counts, stream)
+
+    def step():
+        return adist.tally_one_instance(tc, hi - lo, cfg, w["segments"], eng.device, 0, None)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if eng.last_error_count() != 0:
+        raise SystemExit("bench batch has invalid votes")
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    eng.kernel_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ktimes = eng.kernel_times()
+    eng.kernel_timing(False)
+    elapsed = adist.max_over_ranks(elapsed)
+    if world > 1:
+        dist.barrier()
+    if rank == 0:
+        kernels = {}
+        for name, (launches, total) in ktimes.items():
+            avg = total / max(launches, 1)
+            ab = KERNEL_BYTES_PER_VOTE.get(name, 0) * (hi - lo)
+            kernels[name] = {"launches": launches, "avg_ms": avg, "algorithmic_bytes": ab,
+                             "GBps": ab / (avg * 1e-3) / 1e9 if ab and avg > 0 else None}
+        dom = max(kernels, key=lambda k: kernels[k]["avg_ms"] * kernels[k]["launches"])
+        dom_ms = kernels[dom]["avg_ms"]
+        achieved = KERNEL_BYTES_PER_VOTE[dom] * (hi - lo) / (dom_ms * 1e-3) / 1e9
+        out = {
+            "metric": "votes_tallied_per_sec", "value": n * args.steps / elapsed, "unit": "votes/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
+            "scaling": w["scaling"], "vs_baseline": None, "dtype": "int64",
+            "data": "synthetic (counter-based splitmix64 streams, agnes_gen.h; Zipf powers)",
+            "config": {"workload": w["desc"], "config": args.config, "instances": 1,
+                       "validators": p.n_vals, "votes_total": n, "votes_per_gpu_per_step": hi - lo,
+                       "segments_per_gpu": w["segments"], "mode": "REFERENCE", "flags": w["flags"],
+                       "parallelism": f"stream-sliced x{world} (one all_gather per step)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "traffic_source": None,
+                         "kernel": KERNEL_SYMBOLS.get(dom, dom), "kernel_avg_ms": dom_ms,
+                         "bytes_per_vote": KERNEL_BYTES_PER_VOTE[dom],
+                         "algorithmic_bytes": KERNEL_BYTES_PER_VOTE[dom] * (hi - lo),
+                         "note": "two passes per step (partials, exact rescan); latency-bound at 2e6 votes"},
+            "kernels": kernels,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import oracle_lib as ol  # test infrastructure: the CPU baseline leg only
+            h = whole.to_host()
+            hb = ol.HostBatch(h["instance"], h["round"], h["type"], h["value"], h["validator"],
+                              h["offsets"].copy(), None)
+            best = None
+            for _ in range(3):
+                t1 = time.perf_counter()
+                want, _, _ = ol.tally(cfg, hb, power)
+                dt = time.perf_counter() - t1
+                best = dt if best is None else min(best, dt)
+            out["cpu_baseline"] = {"value": n / best, "unit": "votes/s", "cores": 1, "kind": "port",
+                                   "sample": f"the whole instance ({n} votes), oracle/agnes_oracle.c "
+                                             "orc_tally (one instance: one thread), best of 3"}
+            if args.check:
+                out["cpu_check_equal"] = bool(np.array_equal(codes[: hi - lo].cpu().numpy(), want))
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

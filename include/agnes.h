@@ -186,6 +186,10 @@ typedef struct agnes_state {
 #define AGNES_FLAG_ROUND_SKIP 0x1u      /* emit RoundSkip (+1/3) — producer absent in the reference */
 #define AGNES_FLAG_STATE_MACHINE 0x2u   /* apply events to per-instance State (apply_msg :61-69)     */
 #define AGNES_FLAG_DISTINCT_VALUES 0x4u /* compare value labels in prevote() (:241); default: ZST, all equal */
+#define AGNES_FLAG_ONE_INSTANCE 0x8u    /* agnes_tally_carried only: the batch's segments are consecutive
+                                           slices of ONE instance whose votes carry instance id
+                                           agnes_config.reserved (C5: one huge instance split over
+                                           waves and GPUs) */
 
 typedef struct agnes_config {
     uint32_t mode;       /* AGNES_MODE_*                                            */
@@ -275,6 +279,27 @@ int agnes_upload_power(agnes_ctx* ctx, const int64_t* power, uint32_t n_sets, ui
  * get AGNES_CODE_INVALID and are counted by agnes_last_error_count. */
 int agnes_tally(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
                 uint8_t* codes, agnes_state* states, void* stream);
+
+/* VoteCount of one (round, type) bucket (round_votes.rs:15-19): the executor state
+ * a stream carries between calls.  value = the bucket's label, the last non-nil
+ * value written (:50-54; 0 = VoteCount::new).  24-byte device record. */
+typedef struct agnes_vote_count {
+    int64_t value_w;
+    int64_t nil_w;
+    uint32_t value;
+    uint32_t reserved;
+} agnes_vote_count;
+
+/* agnes_tally continuing carried executors: counts (DEVICE, [n_instances][2 *
+ * max_rounds], index round * 2 + type) holds each segment's RoundVotes state
+ * before its first vote and is overwritten with the state after its last.  With
+ * AGNES_FLAG_ONE_INSTANCE every segment is a consecutive slice of one instance
+ * (id cfg->reserved): a segment's counts are then the fold of the slices before it
+ * (weights summed, the latest label) and the codes equal one stream's (C5: one
+ * instance split over waves and GPUs, agnes_amd/dist.py tally_one_instance).
+ * REFERENCE mode without RoundSkip or State machine; runs the i64 kernel. */
+int agnes_tally_carried(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
+                        uint8_t* codes, agnes_vote_count* counts, void* stream);
 
 /* Number of votes coded AGNES_CODE_INVALID by the most recent agnes_tally on
  * this context (synchronises the context's stream). */

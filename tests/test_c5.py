@@ -1,0 +1,222 @@
+"""C5 — one instance split into contiguous slices over waves and GPUs (SURVEY.md
+§8(e): per-slice partial tallies, one exchange step, an exact rescan).
+
+Parity bar: the per-vote codes of the split computation equal the checker's on
+the whole instance tallied as one stream (oracle/agnes_oracle.c orc_tally).  The
+CPU tests drive agnes_amd/dist.py tally_one_instance with the carried-tally
+stand-in (tests/carried_fake.py), including a world_size-2 gloo run; the GPU tests
+drive it on agnes_tally_carried through the C ABI.
+"""
+import dataclasses
+import os
+import socket
+import sys
+import types
+
+import numpy as np
+import pytest
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+sys.path.insert(0, HERE)
+
+from agnes_amd import abi  # noqa: E402
+from agnes_amd import dist as ad  # noqa: E402
+import oracle_lib as ol  # noqa: E402
+from carried_fake import CarriedFake  # noqa: E402
+
+
+def _instance(seed=5, n_vals=300, R=2, nil=250, kind=abi.POWER_ZIPF):
+    """One instance: n_vals validators prevote and precommit in each of R rounds."""
+    p = abi.gen_params(seed=seed, n_instances=1, n_vals=n_vals, rounds_min=R, rounds_max=R,
+                       nil_permille=nil)
+    hb = ol.gen_batch(p)
+    power = ol.gen_power(seed, 1, n_vals, kind, 1, 1000)
+    return hb, power, abi.config(abi.MODE_REFERENCE, 0, R)
+
+
+def _slice(n, rank, world):
+    lo = (n * rank // world) // 4 * 4
+    hi = n if rank == world - 1 else (n * (rank + 1) // world) // 4 * 4
+    return lo, hi
+
+
+def _fake_tc(fake, hb, lo, hi, codes):
+    def tc(one, off, counts):
+        b = types.SimpleNamespace(instance=hb.instance[lo:hi], round=hb.round[lo:hi],
+                                  type=hb.type[lo:hi], value=hb.value[lo:hi],
+                                  validator=hb.validator[lo:hi],
+                                  offsets=off.cpu().numpy().astype(np.int64), instance_set=None)
+        cv = counts.numpy().view(abi.VOTE_COUNT_DTYPE).reshape(counts.shape[0], counts.shape[1])
+        fake.tally_carried(one, b, codes, cv)
+    return tc
+
+
+def test_segment_offsets_partition():
+    for n, s in [(0, 1), (3, 4), (1001, 7), (4096, 64)]:
+        b = ad.segment_offsets(n, s)
+        assert b[0] == 0 and b[-1] == n and len(b) == s + 1
+        assert np.all(np.diff(b.astype(np.int64)) >= 0)
+        assert np.all(b[:-1] % 4 == 0)
+
+
+def test_fold_counts_is_the_sequential_fold():
+    rng = np.random.default_rng(1)
+    S, K = 9, 4
+    w = torch.from_numpy(rng.integers(-1000, 1000, (S, K, 2)))
+    lab = torch.from_numpy(np.where(rng.random((S, K)) < 0.4, abi.NIL,
+                                    rng.integers(0, 7, (S, K))).astype(np.int64))
+    ex_w, ex_lab, tot_w, tot_lab = ad.fold_counts(w, lab)
+    acc_w = np.zeros((K, 2), np.int64)
+    acc_l = np.full(K, abi.NIL, np.int64)
+    for s in range(S):
+        assert np.array_equal(ex_w[s].numpy(), acc_w)
+        assert np.array_equal(ex_lab[s].numpy(), acc_l)
+        acc_w = acc_w + w[s].numpy()
+        acc_l = np.where(lab[s].numpy() != abi.NIL, lab[s].numpy(), acc_l)
+    assert np.array_equal(tot_w.numpy(), acc_w) and np.array_equal(tot_lab.numpy(), acc_l)
+
+
+@pytest.mark.parametrize("segments", [1, 3, 16])
+def test_split_instance_equals_whole_cpu(segments):
+    hb, power, cfg = _instance()
+    want, _, _ = ol.tally(cfg, hb, power)
+    codes = np.zeros(hb.n_votes, np.uint8)
+    ad.tally_one_instance(_fake_tc(CarriedFake(power), hb, 0, hb.n_votes, codes), hb.n_votes, cfg,
+                          segments, torch.device("cpu"))
+    assert np.array_equal(codes, want)
+    assert (want & abi.CODE_EVENT_MASK != 0).any()
+
+
+def test_split_instance_continued_across_calls_cpu():
+    """two calls on consecutive slices, the second continuing from the first's
+    result (prior): a stream continued across calls"""
+    hb, power, cfg = _instance(seed=9)
+    want, _, _ = ol.tally(cfg, hb, power)
+    fake = CarriedFake(power)
+    mid = (hb.n_votes // 2) // 4 * 4
+    c0 = np.zeros(mid, np.uint8)
+    c1 = np.zeros(hb.n_votes - mid, np.uint8)
+    fw, fl = ad.tally_one_instance(_fake_tc(fake, hb, 0, mid, c0), mid, cfg, 4, torch.device("cpu"))
+    ad.tally_one_instance(_fake_tc(fake, hb, mid, hb.n_votes, c1), hb.n_votes - mid, cfg, 4,
+                          torch.device("cpu"), prior=(fw, fl))
+    assert np.array_equal(np.concatenate([c0, c1]), want)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, HERE)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        hb, power, cfg = _instance()
+        lo, hi = _slice(hb.n_votes, rank, world)
+        codes = np.zeros(hi - lo, np.uint8)
+        fw, fl = ad.tally_one_instance(_fake_tc(CarriedFake(power), hb, lo, hi, codes), hi - lo, cfg, 5,
+                                       torch.device("cpu"))
+        q.put((rank, codes.tobytes(), fw.numpy().tobytes(), fl.numpy().tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_split_instance_two_ranks_gloo():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    hb, power, cfg = _instance()
+    want, _, _ = ol.tally(cfg, hb, power)
+    assert b"".join(r[1] for r in res) == want.tobytes()
+    assert res[0][2] == res[1][2] and res[0][3] == res[1][3]  # every rank has the final tally
+    # ... and it is the whole instance's
+    codes = np.zeros(hb.n_votes, np.uint8)
+    fw, fl = ad.tally_one_instance(_fake_tc(CarriedFake(power), hb, 0, hb.n_votes, codes), hb.n_votes,
+                                   cfg, 1, torch.device("cpu"))
+    assert res[0][2] == fw.numpy().tobytes() and res[0][3] == fl.numpy().tobytes()
+
+
+# ------------------------------------------------------------------ GPU (C ABI)
+
+@pytest.fixture(scope="module")
+def eng():
+    from agnes_amd.engine import Engine
+    return Engine(0)
+
+
+def _gpu_tc(eng, db, codes):
+    def tc(one, off, counts):
+        eng.tally_carried(one, dataclasses.replace(db, offsets=off, instance_set=None), codes, counts)
+    return tc
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("segments,n_vals,R,nil", [(1, 3000, 1, 200), (7, 3000, 2, 200),
+                                                   (64, 20000, 1, 200), (300, 20000, 3, 300),
+                                                   (33, 5000, 2, 900)])
+def test_gpu_split_instance(eng, segments, n_vals, R, nil):
+    from agnes_amd.engine import DeviceBatch
+    hb, power, cfg = _instance(seed=11 + segments, n_vals=n_vals, R=R, nil=nil)
+    want, _, _ = ol.tally(cfg, hb, power)
+    eng.upload_power(power)
+    db = DeviceBatch.from_host(hb, eng.device)
+    codes = torch.zeros(hb.n_votes, dtype=torch.uint8, device=eng.device)
+    ad.tally_one_instance(_gpu_tc(eng, db, codes), hb.n_votes, cfg, segments, eng.device)
+    torch.cuda.synchronize()
+    assert np.array_equal(codes.cpu().numpy(), want)
+    assert eng.last_error_count() == 0
+
+
+@pytest.mark.gpu
+def test_gpu_split_instance_continued_across_calls(eng):
+    from agnes_amd.engine import DeviceBatch
+    hb, power, cfg = _instance(seed=21, n_vals=8000, R=2)
+    want, _, _ = ol.tally(cfg, hb, power)
+    eng.upload_power(power)
+    mid = (hb.n_votes * 3 // 5) // 4 * 4
+    out = []
+    prior = None
+    for lo, hi in [(0, mid), (mid, hb.n_votes)]:
+        part = types.SimpleNamespace(instance=hb.instance[lo:hi], round=hb.round[lo:hi],
+                                     type=hb.type[lo:hi], value=hb.value[lo:hi],
+                                     validator=hb.validator[lo:hi],
+                                     offsets=np.array([0, hi - lo], np.uint64))
+        db = DeviceBatch.from_host(part, eng.device)
+        codes = torch.zeros(hi - lo, dtype=torch.uint8, device=eng.device)
+        prior = ad.tally_one_instance(_gpu_tc(eng, db, codes), hi - lo, cfg, 16, eng.device,
+                                      prior=prior)
+        out.append(codes.cpu().numpy())
+    assert np.array_equal(np.concatenate(out), want)
+
+
+@pytest.mark.gpu
+def test_gpu_tally_carried_rejects(eng):
+    """ONE_INSTANCE needs the carried entry point; the carried path is REFERENCE only"""
+    from agnes_amd.engine import DeviceBatch
+    from agnes_amd.lib import AgnesError
+    hb, power, cfg = _instance(seed=3, n_vals=64, R=1)
+    eng.upload_power(power)
+    db = DeviceBatch.from_host(hb, eng.device)
+    codes = torch.zeros(hb.n_votes, dtype=torch.uint8, device=eng.device)
+    with pytest.raises(AgnesError):
+        eng.tally(abi.config(abi.MODE_REFERENCE, abi.FLAG_ONE_INSTANCE, 1), db, codes)
+    counts = torch.zeros((1, 2, 3), dtype=torch.int64, device=eng.device)
+    with pytest.raises(AgnesError):
+        eng.tally_carried(abi.config(abi.MODE_DEDUP, 0, 1), db, codes, counts)
