@@ -141,22 +141,26 @@ def fold_counts(w: torch.Tensor, lab: torch.Tensor):
     the last slice's that wrote a value (round_votes.rs:50-54; NIL = none).
     w int64 [S, K, 2], lab int64 [S, K] -> (exclusive w, exclusive lab, total w
     [K, 2], total lab [K])."""
-    S = w.shape[0]
-    incl = torch.cumsum(w, dim=0)
-    excl = incl - w
-    idx = torch.arange(S, device=w.device, dtype=torch.int64).view(S, 1).expand_as(lab)
-    last = torch.cummax(torch.where(lab != NIL, idx, torch.full_like(idx, -1)), dim=0).values
-    prev = torch.cat([torch.full_like(last[:1], -1), last[:-1]], dim=0)
+    # the scans run along the innermost dimension ([K, S] layouts): torch's
+    # outer-dimension scan kernels are an order of magnitude slower at S ~ 1e3
+    S, K = w.shape[0], w.shape[1]
+    wt = w.reshape(S, 2 * K).t().contiguous()                       # [2K, S]
+    incl_t = torch.cumsum(wt, dim=1)
+    excl = (incl_t - wt).t().reshape(S, K, 2)
+    lt = lab.t().contiguous()                                        # [K, S]
+    idx = torch.arange(S, device=w.device, dtype=torch.int64).view(1, S).expand_as(lt)
+    last = torch.cummax(torch.where(lt != NIL, idx, torch.full_like(idx, -1)), dim=1).values
+    prev = torch.cat([torch.full_like(last[:, :1], -1), last[:, :-1]], dim=1)
 
     def pick(at):
-        g = torch.gather(lab, 0, at.clamp(min=0))
+        g = torch.gather(lt, 1, at.clamp(min=0))
         return torch.where(at >= 0, g, torch.full_like(g, NIL))
 
-    return excl, pick(prev), incl[-1], pick(last)[-1]
+    return excl, pick(prev).t(), incl_t[:, -1].reshape(K, 2), pick(last)[:, -1]
 
 
 def tally_one_instance(tally_carried, n_votes: int, cfg: abi.Config, n_segments: int, device,
-                       inst_id: int = 0, group=None, prior=None):
+                       inst_id: int = 0, group=None, prior=None, offsets=None):
     """C5 driver.  This rank holds a contiguous slice (n_votes votes) of ONE
     instance's stream; ranks hold consecutive slices in rank order.  The slice is
     cut into n_segments segments (one wave each) and tallied twice:
@@ -169,10 +173,16 @@ def tally_one_instance(tally_carried, n_votes: int, cfg: abi.Config, n_segments:
     tally_carried(cfg, offsets int64 [S + 1] on `device`, counts int64 [S, K, 3])
     runs agnes_tally_carried on the slice.  prior: the instance's (w [K, 2], label
     [K]) before this call (a stream continued across calls), None = RoundVotes::new.
+    offsets: segment_offsets(n_votes, n_segments) already on `device` (lets a caller
+    capture the whole step in a HIP graph).
     Returns the instance's (w, label) after every rank's votes."""
     K = 2 * cfg.max_rounds
-    S = max(1, min(n_segments, max(1, n_votes // 4)))
-    off = torch.from_numpy(segment_offsets(n_votes, S).view(np.int64)).to(device)
+    if offsets is None:
+        S = max(1, min(n_segments, max(1, n_votes // 4)))
+        off = torch.from_numpy(segment_offsets(n_votes, S).view(np.int64)).to(device)
+    else:
+        off = offsets
+        S = off.numel() - 1
     one = abi.Config(cfg.mode, cfg.flags | abi.FLAG_ONE_INSTANCE, cfg.max_rounds, inst_id)
     counts = torch.zeros((S, K, 3), dtype=torch.int64, device=device)
     counts[..., 2] = NIL

@@ -272,29 +272,50 @@ def bench_one_instance(args, w, eng, rank, world):
     codes = torch.empty(max(hi - lo, 1), dtype=torch.uint8, device=eng.device)
     cfg = abi.config(w["mode"], w["flags"], w["max_rounds"])
 
-    def tc(one, off, counts):
-        eng.tally_carried(one, dataclasses.replace(batch, offsets=off), codes, counts, stream)
+    segs = max(1, min(w["segments"], max(1, (hi - lo) // 4)))
+    off = torch.from_numpy(adist.segment_offsets(hi - lo, segs).view(np.int64)).to(eng.device)
+
+    def tc(one, o, counts):  # on the current stream: a graph capture's while capturing
+        eng.tally_carried(one, dataclasses.replace(batch, offsets=o), codes, counts)
 
     def step():
-        return adist.tally_one_instance(tc, hi - lo, cfg, w["segments"], eng.device, 0, None)
+        return adist.tally_one_instance(tc, hi - lo, cfg, segs, eng.device, 0, None, offsets=off)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     if eng.last_error_count() != 0:
         raise SystemExit("bench batch has invalid votes")
+    # per-kernel times: one eager step with the engine's event timing
+    eng.kernel_timing(True)
+    step()
+    torch.cuda.synchronize()
+    ktimes = eng.kernel_times()
+    eng.kernel_timing(False)
+    # one GPU: the step is ~20 short launches (two tallies + the folds), so it is
+    # captured once in a HIP graph and replayed; over ranks the all_gather stays eager
+    run = step
+    graph = world == 1 and not os.environ.get("AGNES_NO_GRAPH")
+    if graph:
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            step()
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            step()
+        run = g.replay
+        run()
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
     torch.cuda.synchronize()
-    eng.kernel_timing(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        run()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    ktimes = eng.kernel_times()
-    eng.kernel_timing(False)
     elapsed = adist.max_over_ranks(elapsed)
     if world > 1:
         dist.barrier()
@@ -316,8 +337,9 @@ def bench_one_instance(args, w, eng, rank, world):
             "data": "synthetic (counter-based splitmix64 streams, agnes_gen.h; Zipf powers)",
             "config": {"workload": w["desc"], "config": args.config, "instances": 1,
                        "validators": p.n_vals, "votes_total": n, "votes_per_gpu_per_step": hi - lo,
-                       "segments_per_gpu": w["segments"], "mode": "REFERENCE", "flags": w["flags"],
-                       "parallelism": f"stream-sliced x{world} (one all_gather per step)"},
+                       "segments_per_gpu": segs, "mode": "REFERENCE", "flags": w["flags"],
+                       "parallelism": f"stream-sliced x{world} (one all_gather per step)",
+                       "hip_graph": graph},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None, "traffic_source": None,
                          "kernel": KERNEL_SYMBOLS.get(dom, dom), "kernel_avg_ms": dom_ms,
