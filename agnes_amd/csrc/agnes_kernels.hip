@@ -1187,15 +1187,15 @@ static hipError_t launch_mode(const agnes_tally_args* a, uint32_t lpw, int num_c
          * serial ballot loops (C2 1.39 ms per-instance fused, 1.82 ms stream fused).
          * Development knobs, read per launch (tests switch them):
          *   AGNES_STREAM 0 never stream, 2 the stream kernel with its fused State machine;
-         *   AGNES_APPLY  0 never the apply pass, 2 also after the per-instance kernel. */
+         *   AGNES_APPLY  0 never the apply pass (the fused State machine kernels). */
         const char* d = std::getenv("AGNES_STREAM");
         const int stream_lvl = d && d[0] >= '0' && d[0] <= '2' ? d[0] - '0' : 1;
         const char* p = std::getenv("AGNES_APPLY");
         const int apply_lvl = p && p[0] >= '0' && p[0] <= '2' ? p[0] - '0' : 1;
         const bool stream = MODE == AGNES_MODE_REFERENCE && !SKIP && stream_lvl >= 1;
         const bool fused_stream = SM && stream_lvl == 2;
-        const bool split = SM && !fused_stream && agnes_apply_codes_supported(a) &&
-                           (stream ? apply_lvl >= 1 : apply_lvl == 2);
+        /* per-instance route (DEDUP / RoundSkip) split as well: C4 1.04 vs 1.11 ms fused */
+        const bool split = SM && !fused_stream && agnes_apply_codes_supported(a) && apply_lvl >= 1;
         agnes_tally_args b = *a;
         if (split) b.flags &= ~AGNES_FLAG_STATE_MACHINE;
         /* first-event hints: the stream kernel records them for the apply pass */
