@@ -53,6 +53,8 @@ __device__ __forceinline__ uint32_t bytes_of(uint32_t x) {
     const uint32_t b = (x * 0x00204081u) & 0x01010101u;
     return (b << 8) - b;
 }
+/* 0xFF in the bytes below byte i (i <= 4) */
+__device__ __forceinline__ uint32_t below_bytes(uint32_t i) { return i >= 4u ? 0xFFFFFFFFu : (1u << (8u * i)) - 1u; }
 /* 0xFF in the bytes of x that are zero (exact, no borrow) */
 __device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
     const uint32_t t = (x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
@@ -173,6 +175,98 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
     bool skipped = false;
     /* the positions (relative to lo) whose values the State takes */
     uint32_t lock_at = NOPOS, valid_at = NOPOS, dec_at = NOPOS, dec_round = 0;
+
+    /* Without RoundSkip, branch-free: a window holds at most one P1 (the first
+     * PolkaNil / PolkaValue at eqr in Prevote, :197-198) and one commit (the first
+     * PrecommitValue, :211), so two table lookups per dword — the start step's and
+     * Precommit's — and byte masks decide every vote: start-table messages before
+     * P1 (or the commit), Precommit-table messages between P1 and the commit, the
+     * step messages at the two, nothing after the commit. */
+    auto walk_ns = [&](uint64_t w, uint4 cq, uint4 rq) {
+        const uint32_t c4[4] = {cq.x, cq.y, cq.z, cq.w}, r4[4] = {rq.x, rq.y, rq.z, rq.w};
+        const int32_t rel = (int32_t)((int64_t)w - (int64_t)lo); /* > -16 */
+        const uint32_t a0 = rel < 0 ? (uint32_t)(-rel) : 0u;
+        const uint64_t rem = hi - w;
+        const uint32_t a1 = rem < 16u ? (uint32_t)rem : 16u;
+        const uint32_t allowed = ((1u << a1) - 1u) & ~((1u << a0) - 1u); /* this instance's bytes */
+        const bool eqok = eq8 < 0x100u, pv0 = step == AGNES_STEP_PREVOTE;
+        const uint32_t eqrep = (eq8 & 0xFFu) * 0x01010101u;
+        const uint32_t tshi = eqok ? T1HI : T0HI;
+        const uint32_t tslo = eqok ? t1lo_of(step) : T0LO, tplo = eqok ? t1lo_of(AGNES_STEP_PRECOMMIT) : T0LO;
+        uint32_t os[4], op[4], cvb[4], p1b[4];
+#pragma unroll
+        for (uint32_t d = 0; d < 4u; ++d) {
+            const uint32_t e = c4[d] & 0x07070707u;
+            const uint32_t q = eqok ? zero_bytes(r4[d] ^ eqrep) : 0u;
+            const uint32_t bm = bytes_of((allowed >> (4u * d)) & 0xFu);
+            const uint32_t z = __builtin_amdgcn_perm(T0HI, T0LO, e) & ~q;
+            os[d] = ((__builtin_amdgcn_perm(tshi, tslo, e) & q) | z) & bm;
+            op[d] = ((__builtin_amdgcn_perm(tshi, tplo, e) & q) | z) & bm;
+            cvb[d] = zero_bytes(e ^ 0x05050505u) & bm & 0x01010101u;   /* PrecommitValue, any round */
+            p1b[d] = pv0 ? (os[d] & 0x01010101u & ~cvb[d]) : 0u;       /* PolkaNil / Value at eqr */
+        }
+        auto first = [](const uint32_t (&m)[4]) -> uint32_t {
+            uint32_t f = 16u;
+#pragma unroll
+            for (int d = 3; d >= 0; --d)
+                if (m[d]) f = 4u * (uint32_t)d + ((uint32_t)__builtin_ctz(m[d]) >> 3);
+            return f;
+        };
+        /* 0xFF in the bytes of dword d whose window index lies in [b, e) */
+        auto span = [](uint32_t d, uint32_t b, uint32_t e) -> uint32_t {
+            const uint32_t lo4 = 4u * d;
+            const uint32_t bb = b > lo4 ? (b - lo4 < 4u ? b - lo4 : 4u) : 0u;
+            const uint32_t ee = e > lo4 ? (e - lo4 < 4u ? e - lo4 : 4u) : 0u;
+            return below_bytes(ee) & ~below_bytes(bb);
+        };
+        const uint32_t fc = first(cvb), fp = first(p1b);
+        const bool has_p1 = fp < fc;          /* P1 before the commit (a commit ends the walk) */
+        const uint32_t pre = has_p1 ? fp : fc; /* start-table messages below this byte */
+        uint32_t ow[4], vup[4];
+#pragma unroll
+        for (uint32_t d = 0; d < 4u; ++d) {
+            const uint32_t mid = has_p1 ? span(d, fp + 1u, fc) : 0u;
+            ow[d] = c4[d] | (os[d] & 0xF0F0F0F0u & span(d, 0u, pre)) | (op[d] & 0xF0F0F0F0u & mid);
+            /* set_valid_value (:202): Precommit-table PolkaValues at eqr before the commit */
+            vup[d] = (has_p1 ? op[d] & mid : (step == AGNES_STEP_PRECOMMIT ? os[d] & span(d, 0u, fc) : 0u)) &
+                     0x02020202u;
+        }
+        if (has_p1) {
+            const uint32_t sh = 8u * (fp & 3u);
+            const uint32_t ev = ((fp < 8u ? (fp < 4u ? c4[0] : c4[1]) : (fp < 12u ? c4[2] : c4[3])) >> sh) & 7u;
+            const uint32_t m = ev == AGNES_CODE_POLKA_VALUE ? AGNES_VMSG_PRECOMMIT_VALUE : AGNES_VMSG_PRECOMMIT_NIL;
+#pragma unroll
+            for (uint32_t d = 0; d < 4u; ++d) ow[d] |= d == (fp >> 2) ? m << (sh + AGNES_CODE_MSG_SHIFT) : 0u;
+            if (ev == AGNES_CODE_POLKA_VALUE) lock_at = valid_at = (uint32_t)(rel + (int32_t)fp); /* :198 */
+            step = AGNES_STEP_PRECOMMIT;
+        }
+#pragma unroll
+        for (int d = 3; d >= 0; --d) { /* the last set_valid_value of the window */
+            if (vup[d]) {
+                valid_at = (uint32_t)(rel + (int32_t)(4u * (uint32_t)d + ((31u - (uint32_t)__builtin_clz(vup[d])) >> 3)));
+                break;
+            }
+        }
+        if (fc < 16u) { /* :211 commit */
+            const uint32_t sh = 8u * (fc & 3u);
+#pragma unroll
+            for (uint32_t d = 0; d < 4u; ++d)
+                ow[d] |= d == (fc >> 2) ? AGNES_VMSG_DECISION << (sh + AGNES_CODE_MSG_SHIFT) : 0u;
+            dec_at = (uint32_t)(rel + (int32_t)fc);
+            dec_round = ((fc < 8u ? (fc < 4u ? r4[0] : r4[1]) : (fc < 12u ? r4[2] : r4[3])) >> sh) & 0xFFu;
+            step = AGNES_STEP_COMMIT;
+        }
+        if (((ow[0] ^ c4[0]) | (ow[1] ^ c4[1]) | (ow[2] ^ c4[2]) | (ow[3] ^ c4[3])) && !(a.dbg & 64u)) {
+            if (rel >= 0 && rem >= 16u) {
+                *reinterpret_cast<uint4*>(a.codes + w) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+            } else {
+                for (uint32_t b = 0; b < 16u; ++b) {
+                    const uint32_t x = (ow[b >> 2] >> (8u * (b & 3u))) & 0xFFu;
+                    if (x != ((c4[b >> 2] >> (8u * (b & 3u))) & 0xFFu)) a.codes[w + b] = (uint8_t)x;
+                }
+            }
+        }
+    };
 
     /* one 16-B window at w of this instance (cq, rq: its code and round bytes) */
     auto walk = [&](uint64_t w, uint4 cq, uint4 rq) {
@@ -309,7 +403,10 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
                 tail_fill(a.vb.round, w, NV, rs);
             }
             if (w + 16u > lo && !(a.dbg & 32u)) /* development knob 32: DMA only */
-                walk(w, *reinterpret_cast<const uint4*>(cs), *reinterpret_cast<const uint4*>(rs));
+            {
+                if (SKIP) walk(w, *reinterpret_cast<const uint4*>(cs), *reinterpret_cast<const uint4*>(rs));
+                else walk_ns(w, *reinterpret_cast<const uint4*>(cs), *reinterpret_cast<const uint4*>(rs));
+            }
             if (step == AGNES_STEP_COMMIT) break;
         }
         const uint64_t nb = blk + BLK;
