@@ -9,5 +9,5 @@ tail -1 gpurun_out/smoke.log
 timeout -k 10 300 python -u bench.py > gpurun_out/bench.log 2>&1 || { cat gpurun_out/bench.log; exit 1; }
 grep '^{' gpurun_out/bench.log
 rm -rf gpurun_out/prof
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 20 --warmup 5 > gpurun_out/prof.log 2>&1 || { tail -20 gpurun_out/prof.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 20 --warmup 5 > gpurun_out/prof.log 2>&1 || { tail -20 gpurun_out/prof.log; exit 1; }
 find gpurun_out/prof -name '*kernel_stats.csv' | head -1 | xargs cat | cut -c1-200
