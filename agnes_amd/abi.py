@@ -115,6 +115,10 @@ EVENT_DTYPE = np.dtype([("round", "<i8"), ("pol_round", "<i8"), ("value", "<u4")
 MESSAGE_DTYPE = np.dtype([("round", "<i8"), ("pol_round", "<i8"), ("value", "<u4"),
                           ("kind", "u1"), ("vote_type", "u1"), ("timeout_step", "u1"),
                           ("pad", "u1")])
+# agnes_edge (include/agnes.h): one 16-B record per edge-triggered vote
+EDGE_DTYPE = np.dtype([("vote", "<u8"), ("instance", "<u4"), ("round", "u1"), ("type", "u1"),
+                       ("code", "u1"), ("prev", "u1")])
+assert EDGE_DTYPE.itemsize == 16
 VOTE_COUNT_DTYPE = np.dtype([("value_w", "<i8"), ("nil_w", "<i8"), ("value", "<u4"),
                              ("reserved", "<u4")])  # agnes_vote_count
 assert STATE_DTYPE.itemsize == 64 and EVENT_DTYPE.itemsize == 24 and MESSAGE_DTYPE.itemsize == 24

@@ -35,6 +35,8 @@ struct agnes_ctx {
                                    (split route), then the list counter and
                                    AGNES_QUEUE_WORDS - 1 work-queue counters */
     uint32_t list_cap = 0;
+    uint64_t* d_scan = nullptr; /* edge-offset scan: block totals */
+    uint64_t scan_cap = 0;
 };
 
 namespace {
@@ -205,6 +207,7 @@ void agnes_ctx_destroy(agnes_ctx* c) {
     free_power(c);
     if (c->d_err) (void)hipFree(c->d_err);
     if (c->d_list) (void)hipFree(c->d_list);
+    if (c->d_scan) (void)hipFree(c->d_scan);
     delete c;
 }
 
@@ -328,6 +331,7 @@ int agnes_tally(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b
 }
 
 static_assert(sizeof(agnes_vote_count) == sizeof(agnes_carry_rec), "agnes_vote_count is the carried executor");
+static_assert(sizeof(agnes_edge) == 16, "agnes_edge is one 16-B record");
 
 int agnes_tally_carried(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint8_t* codes,
                         agnes_vote_count* counts, void* stream) {
@@ -354,6 +358,39 @@ int agnes_apply_events(agnes_ctx* c, agnes_state* states, uint32_t n, const uint
     AGNES_TRY(hipSetDevice(c->device));
     c->last_stream = (hipStream_t)stream;
     return status_of(agnes_launch_apply_events(states, n, off, ev, msgs, flags, (hipStream_t)stream));
+}
+
+/* ---------------- edge-triggered summary ---------------- */
+
+static bool edges_args_ok(const agnes_config* cfg, const agnes_vote_batch* b, const uint8_t* codes) {
+    return cfg && b && cfg->max_rounds >= 1u && cfg->max_rounds <= 256u &&
+           (b->n_instances == 0 || (b->offsets && (b->n_votes == 0 || (codes && b->round && b->type))));
+}
+
+int agnes_edge_offsets(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, const uint8_t* codes,
+                       uint64_t* offsets, void* stream) {
+    if (!c || !offsets || !edges_args_ok(cfg, b, codes)) return AGNES_E_INVALID;
+    AGNES_TRY(hipSetDevice(c->device));
+    c->last_stream = (hipStream_t)stream;
+    const uint64_t words = agnes_edges_scratch_words(b->n_instances);
+    if (words > c->scan_cap) {
+        if (c->d_scan) AGNES_TRY(hipFree(c->d_scan));
+        c->d_scan = nullptr;
+        c->scan_cap = 0;
+        AGNES_TRY(hipMalloc(&c->d_scan, words * sizeof(uint64_t)));
+        c->scan_cap = words;
+    }
+    return status_of(agnes_launch_edges(b, codes, cfg->max_rounds, offsets, nullptr, c->d_scan,
+                                        (hipStream_t)stream));
+}
+
+int agnes_edges(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, const uint8_t* codes,
+                const uint64_t* offsets, agnes_edge* out, void* stream) {
+    if (!c || !offsets || !out || !edges_args_ok(cfg, b, codes)) return AGNES_E_INVALID;
+    AGNES_TRY(hipSetDevice(c->device));
+    c->last_stream = (hipStream_t)stream;
+    return status_of(agnes_launch_edges(b, codes, cfg->max_rounds, const_cast<uint64_t*>(offsets), out,
+                                        nullptr, (hipStream_t)stream));
 }
 
 /* ---------------- generator ---------------- */

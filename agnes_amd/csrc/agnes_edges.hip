@@ -1,0 +1,206 @@
+/*
+ * agnes_edges.hip — edge-triggered summary of a coded batch (SURVEY.md §8(f) 1;
+ * include/agnes.h agnes_edge_offsets / agnes_edges).
+ *
+ * VoteExecutor::apply (vote_executor.rs:20-36) is level-triggered: after a
+ * threshold holds, every later vote of the executor repeats the event.  The
+ * summary keeps, per instance, the votes that change their (round, type)
+ * executor's level (code bits 0..3) or that carry a State-machine message (bits
+ * 4..7).  The (round, type) executors of an instance are the HeightVotes the
+ * reference leaves as a stub (consensus_executor.rs:5; vote_executor.rs:9,14).
+ *
+ * Two walks of the codes, one instance per lane (like apply_codes): a count pass
+ * that writes each instance's edge count, an exclusive scan of the counts (three
+ * small kernels), and an emit pass that writes 16-B records at the scanned
+ * offsets — ordered by instance then vote, deterministic.  Each lane keeps its
+ * executors' levels as 4-bit nibbles in LDS, [slot][lane] (slot = key / 8, key =
+ * round * 2 + type), so a wave's 64 lookups hit 64 banks.  HBM bound: 3 B per vote
+ * read per pass (code, round, type) + 16 B per edge written.
+ */
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "agnes_device.h"
+#include "agnes_internal.h"
+
+namespace agnes {
+namespace edges {
+
+struct EdgeArgs {
+    agnes_vote_batch vb;
+    const uint8_t* codes;
+    uint64_t* offs;   /* n_instances + 1 */
+    agnes_edge* out;
+    uint32_t keys;    /* 2 * max_rounds */
+    uint32_t nslots;  /* ceil(keys / 8) nibble words per lane */
+};
+
+template <uint32_t W>
+__device__ __forceinline__ void load_win(const uint8_t* col, uint64_t w, uint64_t NV, uint32_t (&v)[W / 4u]) {
+    if (w + W <= NV) {
+        if constexpr (W == 16u) {
+            const uint4 q = *reinterpret_cast<const uint4*>(col + w);
+            v[0] = q.x;
+            v[1] = q.y;
+            v[2] = q.z;
+            v[3] = q.w;
+        } else {
+            v[0] = *reinterpret_cast<const uint32_t*>(col + w);
+        }
+    } else { /* the batch's last window: its real bytes only */
+#pragma unroll
+        for (uint32_t d = 0; d < W / 4u; ++d) v[d] = 0u;
+        for (uint32_t b = 0; b < W && w + b < NV; ++b) v[b >> 2] |= (uint32_t)col[w + b] << (8u * (b & 3u));
+    }
+}
+
+template <bool EMIT, uint32_t W>
+__global__ __launch_bounds__(64) void edge_walk(EdgeArgs a) {
+    uint32_t* const tab = reinterpret_cast<uint32_t*>(agnes_smem);
+    const uint32_t lane = threadIdx.x;
+    const uint32_t i = blockIdx.x * 64u + lane;
+    if (i >= a.vb.n_instances) return;
+    for (uint32_t s = 0; s < a.nslots; ++s) tab[s * 64u + lane] = 0u; /* VoteCount::new: level 0 */
+    const uint64_t NV = a.vb.n_votes;
+    uint64_t lo = a.vb.offsets[i], hi = a.vb.offsets[i + 1u];
+    lo = lo < NV ? lo : NV;
+    hi = hi < NV ? hi : NV;
+    const uint64_t base = EMIT ? a.offs[i] : 0u;
+    uint64_t cnt = 0;
+    for (uint64_t w = lo & ~(uint64_t)(W - 1u); w < hi; w += W) {
+        uint32_t c[W / 4u], r[W / 4u], t[W / 4u];
+        load_win<W>(a.codes, w, NV, c);
+        load_win<W>(a.vb.round, w, NV, r);
+        load_win<W>(a.vb.type, w, NV, t);
+#pragma unroll
+        for (uint32_t b = 0; b < W; ++b) {
+            const uint64_t j = w + b;
+            const uint32_t sh8 = 8u * (b & 3u);
+            const uint32_t cb = (c[b >> 2] >> sh8) & 0xFFu, rb = (r[b >> 2] >> sh8) & 0xFFu,
+                           tb = (t[b >> 2] >> sh8) & 0xFFu;
+            const uint32_t ev = cb & AGNES_CODE_EVENT_MASK;
+            const uint32_t key = rb * 2u + tb;
+            /* outside the instance, INVALID / REJECTED (never counted), or no executor */
+            if (j < lo || j >= hi || ev == AGNES_CODE_INVALID || ev == AGNES_CODE_REJECTED || tb > 1u ||
+                key >= a.keys)
+                continue;
+            uint32_t* const p = tab + (key >> 3) * 64u + lane;
+            const uint32_t x = *p, sh = 4u * (key & 7u);
+            const uint32_t lvl = (x >> sh) & 0xFu, nl = cb & 0xFu;
+            if (lvl != nl || (cb >> AGNES_CODE_MSG_SHIFT) != 0u) {
+                if (EMIT) {
+                    const uint32_t tail = rb | (tb << 8) | (cb << 16) | (lvl << 24);
+                    *reinterpret_cast<uint4*>(a.out + base + cnt) =
+                        make_uint4((uint32_t)j, (uint32_t)(j >> 32), i, tail);
+                }
+                ++cnt;
+            }
+            if (lvl != nl) *p = x ^ ((lvl ^ nl) << sh);
+        }
+    }
+    if (!EMIT) a.offs[i + 1u] = cnt;
+}
+
+/* ---- exclusive offsets: inclusive scan of offs[1..n] in place, three kernels ---- */
+constexpr uint32_t SCAN_T = 256u, SCAN_PER = 4u, SCAN_BLK = SCAN_T * SCAN_PER;
+
+/* inclusive scan of x[0..n) inside one 256-thread block; the block total returned */
+__device__ uint64_t block_scan(uint64_t (&v)[SCAN_PER], uint64_t* wsum) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+#pragma unroll
+    for (uint32_t k = 1; k < SCAN_PER; ++k) v[k] += v[k - 1u];
+    const uint64_t incl = scan(v[SCAN_PER - 1u]); /* wave inclusive over the threads' sums */
+    if (lane == 63u) wsum[wv] = incl;
+    __syncthreads();
+    uint64_t before = incl - v[SCAN_PER - 1u], total = 0;
+    for (uint32_t q = 0; q < SCAN_T / 64u; ++q) {
+        if (q < wv) before += wsum[q];
+        total += wsum[q];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_PER; ++k) v[k] += before;
+    __syncthreads(); /* wsum reusable */
+    return total;
+}
+
+__global__ __launch_bounds__(SCAN_T) void scan_blocks(uint64_t* x, uint64_t n, uint64_t* part) {
+    __shared__ uint64_t wsum[SCAN_T / 64u];
+    const uint64_t b0 = (uint64_t)blockIdx.x * SCAN_BLK + threadIdx.x * SCAN_PER;
+    uint64_t v[SCAN_PER];
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_PER; ++k) v[k] = b0 + k < n ? x[b0 + k] : 0u;
+    const uint64_t total = block_scan(v, wsum);
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_PER; ++k)
+        if (b0 + k < n) x[b0 + k] = v[k];
+    if (threadIdx.x == 0) part[blockIdx.x] = total;
+}
+
+/* one block: exclusive scan of the block totals in place */
+__global__ __launch_bounds__(SCAN_T) void scan_parts(uint64_t* part, uint64_t nb) {
+    __shared__ uint64_t wsum[SCAN_T / 64u];
+    uint64_t carry = 0;
+    for (uint64_t c0 = 0; c0 < nb; c0 += SCAN_BLK) {
+        const uint64_t b0 = c0 + threadIdx.x * SCAN_PER;
+        uint64_t v[SCAN_PER], in[SCAN_PER];
+#pragma unroll
+        for (uint32_t k = 0; k < SCAN_PER; ++k) in[k] = v[k] = b0 + k < nb ? part[b0 + k] : 0u;
+        const uint64_t total = block_scan(v, wsum);
+#pragma unroll
+        for (uint32_t k = 0; k < SCAN_PER; ++k)
+            if (b0 + k < nb) part[b0 + k] = carry + v[k] - in[k];
+        carry += total;
+    }
+}
+
+__global__ __launch_bounds__(SCAN_T) void scan_add(uint64_t* x, uint64_t n, const uint64_t* part) {
+    const uint64_t add = part[blockIdx.x];
+    const uint64_t b0 = (uint64_t)blockIdx.x * SCAN_BLK + threadIdx.x * SCAN_PER;
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_PER; ++k)
+        if (b0 + k < n) x[b0 + k] += add;
+}
+
+} // namespace edges
+} // namespace agnes
+
+/* ------------------------------------------------------------------ */
+
+uint64_t agnes_edges_scratch_words(uint32_t n_instances) {
+    return ((uint64_t)n_instances + agnes::edges::SCAN_BLK - 1u) / agnes::edges::SCAN_BLK;
+}
+
+hipError_t agnes_launch_edges(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds,
+                              uint64_t* offs, agnes_edge* out, uint64_t* scratch, hipStream_t st) {
+    using namespace agnes::edges;
+    const uint32_t n = vb->n_instances;
+    EdgeArgs a{*vb, codes, offs, out, 2u * max_rounds, (2u * max_rounds + 7u) / 8u};
+    /* 16-B windows when the three columns allow them */
+    const bool w16 = ((reinterpret_cast<uintptr_t>(codes) | reinterpret_cast<uintptr_t>(vb->round) |
+                       reinterpret_cast<uintptr_t>(vb->type)) & 15u) == 0u;
+    const dim3 grid((n + 63u) / 64u), blk(64);
+    const size_t lds = (size_t)a.nslots * 64u * sizeof(uint32_t);
+    if (!out) { /* pass 1: counts, then the exclusive scan */
+        hipError_t e = hipMemsetAsync(offs, 0, sizeof(uint64_t), st);
+        if (e != hipSuccess || n == 0) return e;
+        {
+            AgnesKt kt("edge_count", st);
+            if (w16) hipLaunchKernelGGL((edge_walk<false, 16u>), grid, blk, lds, st, a);
+            else hipLaunchKernelGGL((edge_walk<false, 4u>), grid, blk, lds, st, a);
+        }
+        const uint64_t nb = agnes_edges_scratch_words(n);
+        AgnesKt kt("edge_scan", st);
+        hipLaunchKernelGGL(scan_blocks, dim3((uint32_t)nb), dim3(SCAN_T), 0, st, offs + 1, (uint64_t)n, scratch);
+        if (nb > 1u) {
+            hipLaunchKernelGGL(scan_parts, dim3(1), dim3(SCAN_T), 0, st, scratch, nb);
+            hipLaunchKernelGGL(scan_add, dim3((uint32_t)nb), dim3(SCAN_T), 0, st, offs + 1, (uint64_t)n, scratch);
+        }
+        return hipGetLastError();
+    }
+    if (n == 0) return hipSuccess;
+    AgnesKt kt("edge_emit", st);
+    if (w16) hipLaunchKernelGGL((edge_walk<true, 16u>), grid, blk, lds, st, a);
+    else hipLaunchKernelGGL((edge_walk<true, 4u>), grid, blk, lds, st, a);
+    return hipGetLastError();
+}

@@ -96,6 +96,12 @@ hipError_t agnes_launch_gen(const agnes_gen_params* p, const uint64_t* d_offsets
                             uint32_t* instance, uint8_t* round, uint8_t* type, uint32_t* value,
                             uint32_t* validator, hipStream_t stream);
 
+/* the edge summary (agnes_edges.hip): out == nullptr -> count pass + exclusive scan of
+ * offs (scratch: agnes_edges_scratch_words u64); else the emit pass */
+uint64_t agnes_edges_scratch_words(uint32_t n_instances);
+hipError_t agnes_launch_edges(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds,
+                              uint64_t* offs, agnes_edge* out, uint64_t* scratch, hipStream_t stream);
+
 #define AGNES_WAVES_PER_BLOCK 4
 /* list_count[0] counts the deferred list; list_count[1 .. AGNES_QUEUE_WORDS-1] are the
  * fast kernel's work-queue counters; all zeroed before each launch */

@@ -173,6 +173,24 @@ class Engine:
                                           _ptr(events), _ptr(msgs), flags,
                                           _stream_handle(stream)), "agnes_apply_events")
 
+    def edges(self, cfg: abi.Config, batch: DeviceBatch, codes: torch.Tensor, stream=None):
+        """Edge-triggered summary of coded votes (agnes_edge_offsets + agnes_edges).
+        Returns (offsets int64 [n_instances + 1], records uint8 [n_edges, 16] — view
+        the host copy as abi.EDGE_DTYPE).  Reads the total back (one sync)."""
+        if codes.dtype != torch.uint8 or codes.numel() < batch.n_votes:
+            raise ValueError("codes must be a uint8 tensor of n_votes")
+        b = batch.c()
+        offs = torch.empty(batch.n_instances + 1, dtype=torch.int64, device=self.device)
+        sh = _stream_handle(stream)
+        check(self.lib.agnes_edge_offsets(self.ctx, C.byref(cfg), C.byref(b), _ptr(codes), _ptr(offs), sh),
+              "agnes_edge_offsets")
+        n = int(offs[-1].item())
+        out = torch.empty((max(n, 1), 16), dtype=torch.uint8, device=self.device)
+        if n:
+            check(self.lib.agnes_edges(self.ctx, C.byref(cfg), C.byref(b), _ptr(codes), _ptr(offs),
+                                       _ptr(out), sh), "agnes_edges")
+        return offs, out[:n]
+
     # -- synthetic workloads ------------------------------------------------
     def gen_offsets(self, p: abi.GenParams) -> np.ndarray:
         off = np.zeros(p.n_instances + 1, dtype=np.uint64)

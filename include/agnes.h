@@ -318,6 +318,41 @@ int agnes_apply_events(agnes_ctx* ctx, agnes_state* states, uint32_t n_instances
                        uint32_t flags, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Edge-triggered summary of a coded batch.
+ *
+ * VoteExecutor::apply is level-triggered (vote_executor.rs:20-36): once a
+ * threshold holds, every later vote of the executor repeats its event.  The
+ * summary keeps the votes a consumer acts on.  Per instance, the executor of a
+ * valid vote (event not INVALID / REJECTED) is its (round, type) — the
+ * HeightVotes the reference leaves as a stub (consensus_executor.rs:5,
+ * vote_executor.rs:9,14) — and its LEVEL is the vote's code bits 0..3 (tally
+ * event + RoundSkip), 0 before its first vote (VoteCount::new,
+ * round_votes.rs:36-45).  A vote is an EDGE when its level differs from the
+ * level its executor's previous valid vote left, or when it carries a message
+ * (code bits 4..7).  Records are ordered by instance, then vote index.
+ * ------------------------------------------------------------------------- */
+typedef struct agnes_edge {
+    uint64_t vote;     /* index of the vote in the batch                    */
+    uint32_t instance; /* the vote's segment (instance) index               */
+    uint8_t round;     /* Vote.round                                        */
+    uint8_t type;      /* Vote.typ                                          */
+    uint8_t code;      /* the vote's code byte: new level | message << 4     */
+    uint8_t prev;      /* the executor's level before this vote (bits 0..3) */
+} agnes_edge;
+
+/* Pass 1: offsets (DEVICE, n_instances + 1): exclusive offsets of each instance's
+ * edges, offsets[n_instances] = the total.  codes as agnes_tally left them
+ * (DEVICE); votes with round >= cfg->max_rounds or type > 1 are never edges.
+ * Asynchronous on `stream`. */
+int agnes_edge_offsets(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
+                       const uint8_t* codes, uint64_t* offsets, void* stream);
+/* Pass 2: the records into out (DEVICE, offsets[n_instances] records), instance i's
+ * at [offsets[i], offsets[i+1]).  offsets from agnes_edge_offsets on the same
+ * batch and codes. */
+int agnes_edges(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
+                const uint8_t* codes, const uint64_t* offsets, agnes_edge* out, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Synthetic workload generator (counter-based splitmix64; identical on host
  * and device, see agnes_amd/csrc/agnes_gen.h).  Not part of the hot path.
  * ------------------------------------------------------------------------- */

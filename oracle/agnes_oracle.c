@@ -474,6 +474,50 @@ int orc_apply_events(agnes_state* states, uint32_t n, const uint64_t* off, const
     return AGNES_OK;
 }
 
+/* Edge-triggered summary (include/agnes.h agnes_edge).  The
+ * per-vote codes are VoteExecutor::apply's level-triggered Option<Event>
+ * (vote_executor.rs:20-36) for the vote's (round, type) executor — the
+ * reference's HeightVotes stub (consensus_executor.rs:5, vote_executor.rs:9,14).
+ * An executor starts at level 0 (VoteCount::new, round_votes.rs:36-45); a valid
+ * vote is an edge when its level (code bits 0..3) differs from the level its
+ * executor's previous valid vote left, or when it carries a message (bits 4..7).
+ * offsets[n+1] always written; out (NULL: count only) gets the records. */
+int orc_edges(const agnes_config* cfg, const agnes_vote_batch* b, const uint8_t* codes,
+              uint64_t* offsets, agnes_edge* out) {
+    if (!cfg || !b || !offsets || cfg->max_rounds < 1 || cfg->max_rounds > 256) return AGNES_E_INVALID;
+    const uint32_t keys = 2u * cfg->max_rounds;
+    uint8_t level[512];
+    uint64_t k = 0;
+    offsets[0] = 0;
+    for (uint32_t i = 0; i < b->n_instances; ++i) {
+        memset(level, 0, sizeof level);
+        uint64_t lo = b->offsets[i], hi = b->offsets[i + 1];
+        if (lo > b->n_votes) lo = b->n_votes;
+        if (hi > b->n_votes) hi = b->n_votes;
+        for (uint64_t j = lo; j < hi; ++j) {
+            const uint32_t c = codes[j], ev = c & AGNES_CODE_EVENT_MASK;
+            const uint32_t r = b->round[j], t = b->type[j], key = r * 2u + t;
+            if (ev == AGNES_CODE_INVALID || ev == AGNES_CODE_REJECTED || t > 1u || key >= keys) continue;
+            const uint32_t nl = c & 0xFu, prev = level[key];
+            if (prev != nl || (c >> AGNES_CODE_MSG_SHIFT) != 0u) {
+                if (out) {
+                    agnes_edge* e = &out[k];
+                    e->vote = j;
+                    e->instance = i;
+                    e->round = (uint8_t)r;
+                    e->type = (uint8_t)t;
+                    e->code = (uint8_t)c;
+                    e->prev = (uint8_t)prev;
+                }
+                ++k;
+            }
+            level[key] = (uint8_t)nl;
+        }
+        offsets[i + 1] = k;
+    }
+    return AGNES_OK;
+}
+
 void orc_set_totals(const int64_t* power, uint32_t n_sets, uint32_t n_vals, int64_t* totals) {
     for (uint32_t s = 0; s < n_sets; ++s) {
         int64_t t = 0;

@@ -80,6 +80,11 @@ int orc_tally_mt(const agnes_config* cfg, const agnes_vote_batch* batch, const o
 int orc_apply_events(agnes_state* states, uint32_t n_instances, const uint64_t* ev_offsets,
                      const agnes_event* events, agnes_message* msgs, uint32_t flags);
 
+/* edge-triggered summary of coded votes (agnes_edge_offsets + agnes_edges):
+ * offsets[n_instances + 1]; out NULL = count only */
+int orc_edges(const agnes_config* cfg, const agnes_vote_batch* batch, const uint8_t* codes,
+              uint64_t* offsets, agnes_edge* out);
+
 /* wrapping totals of each set (VoteExecutor::new's total_weight default) */
 void orc_set_totals(const int64_t* power, uint32_t n_sets, uint32_t n_vals, int64_t* totals);
 

@@ -57,6 +57,7 @@ def lib():
         L.orc_tally_mt.argtypes = [C.POINTER(abi.Config), C.POINTER(abi.VoteBatch),
                                    C.POINTER(OrcPower), P, P, C.POINTER(C.c_uint64), C.c_int]
         L.orc_apply_events.argtypes = [P, C.c_uint32, P, P, P, C.c_uint32]
+        L.orc_edges.argtypes = [C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P]
         L.orc_set_totals.argtypes = [P, C.c_uint32, C.c_uint32, P]
         L.orc_gen_instance_votes.argtypes = [C.POINTER(abi.GenParams), C.c_uint32]
         L.orc_gen_instance_votes.restype = C.c_uint64
@@ -169,6 +170,19 @@ def tally(cfg: abi.Config, b: HostBatch, power: Optional[np.ndarray], totals=Non
     if rc != 0:
         raise RuntimeError(f"orc_tally rc={rc}")
     return codes, st, int(nbad.value)
+
+
+def edges(cfg: abi.Config, b: HostBatch, codes: np.ndarray):
+    """orc_edges: (offsets u64 [n+1], records abi.EDGE_DTYPE)."""
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    offs = np.zeros(b.n_instances + 1, dtype=np.uint64)
+    cb = b.c()
+    rc = lib().orc_edges(C.byref(cfg), C.byref(cb), _p(codes), _p(offs), None)
+    assert rc == 0, rc
+    out = np.zeros(int(offs[-1]), dtype=abi.EDGE_DTYPE)
+    rc = lib().orc_edges(C.byref(cfg), C.byref(cb), _p(codes), _p(offs), _p(out) if len(out) else None)
+    assert rc == 0, rc
+    return offs, out
 
 
 def apply_events(states: np.ndarray, ev_offsets: np.ndarray, events: np.ndarray, flags: int = 0):

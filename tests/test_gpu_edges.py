@@ -1,0 +1,125 @@
+"""Edge-triggered summary on the GPU (agnes_edge_offsets + agnes_edges through the C
+ABI) against the checker's orc_edges — bit-exact offsets and records."""
+import numpy as np
+import pytest
+import torch
+
+import oracle_lib as ol
+from agnes_amd import abi
+from agnes_amd.engine import DeviceBatch, states_to_device
+from test_gpu_parity import CONFIGS, _make, _start_states, eng  # noqa: F401  (fixture)
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu_edges(eng, cfg, hb, power, states=None, shift=0):
+    """Tally on the GPU, then summarise; shift > 0 offsets the u8 columns by `shift`
+    bytes (4-B windows instead of 16-B)."""
+    eng.upload_power(power)
+    db = DeviceBatch.from_host(hb, eng.device)
+    n = max(hb.n_votes, 1)
+    codes_buf = torch.zeros(n + 16, dtype=torch.uint8, device=eng.device)
+    codes = codes_buf[shift:shift + n]
+    if shift:
+        for f in ("round", "type"):
+            buf = torch.zeros(n + 16, dtype=torch.uint8, device=eng.device)
+            buf[shift:shift + hb.n_votes] = getattr(db, f)
+            setattr(db, f, buf[shift:shift + n])
+    dst = None if states is None else states_to_device(states, eng.device)
+    eng.tally(cfg, db, codes, dst)
+    offs, recs = eng.edges(cfg, db, codes)
+    torch.cuda.synchronize()
+    g_codes = codes[:hb.n_votes].cpu().numpy()
+    return g_codes, offs.cpu().numpy().view(np.uint64), recs.cpu().numpy().reshape(-1).view(abi.EDGE_DTYPE)
+
+
+def _check(cfg, hb, g_codes, g_offs, g_recs):
+    o_offs, o_recs = ol.edges(cfg, hb, g_codes)
+    assert np.array_equal(g_offs, o_offs)
+    if g_recs.tobytes() != o_recs.tobytes():
+        k = int(np.nonzero(g_recs != o_recs)[0][0])
+        raise AssertionError(f"edge {k}: gpu {g_recs[k]} oracle {o_recs[k]}")
+
+
+@pytest.mark.parametrize("name", ["c2_small", "c4_small", "c4_ref_skip", "phased_dedup",
+                                  "sorted_tiny_sets", "many_rounds", "wide_negative_powers"])
+def test_edges_generated(eng, name):
+    if name not in CONFIGS:
+        pytest.skip(f"{name} not in CONFIGS")
+    p, hb, power, cfg = _make(name)
+    states = _start_states(p.n_instances) if cfg.flags & abi.FLAG_STATE_MACHINE else None
+    g_codes, g_offs, g_recs = _gpu_edges(eng, cfg, hb, power, states)
+    o_codes, _, _ = ol.tally(cfg, hb, power, None, states, threads=8)
+    assert np.array_equal(g_codes, o_codes)
+    _check(cfg, hb, g_codes, g_offs, g_recs)
+    assert 0 < len(g_recs) < hb.n_votes
+
+
+@pytest.mark.parametrize("shift", [4, 8, 12])
+def test_edges_unaligned_columns(eng, shift):
+    p, hb, power, cfg = _make("c4_small")
+    g_codes, g_offs, g_recs = _gpu_edges(eng, cfg, hb, power, None, shift)
+    _check(cfg, hb, g_codes, g_offs, g_recs)
+
+
+def test_edges_ragged_empty_and_invalid(eng):
+    rng = np.random.default_rng(11)
+    lengths = [0, 1, 2, 15, 16, 17, 0, 31, 33, 200, 0, 5]
+    off = np.concatenate([[0], np.cumsum(lengths)]).astype(np.uint64)
+    n = int(off[-1])
+    inst = np.repeat(np.arange(len(lengths)), lengths)
+    hb = ol.batch_from_lists(inst, rng.integers(0, 3, n), rng.integers(0, 2, n),
+                             np.where(rng.random(n) < 0.3, abi.NIL, 1), rng.integers(0, 8, n), off)
+    hb.type[3] = 2           # invalid type
+    hb.round[20] = 7         # >= max_rounds
+    hb.instance[40] += 1     # wrong segment
+    power = ol.gen_power(3, 1, 8, abi.POWER_UNIFORM, 1, 9)
+    cfg = abi.config(abi.MODE_DEDUP, abi.FLAG_ROUND_SKIP | abi.FLAG_STATE_MACHINE, 3)
+    st = abi.new_states(len(lengths), 1, abi.STEP_PREVOTE, 0)
+    g_codes, g_offs, g_recs = _gpu_edges(eng, cfg, hb, power, st)
+    _check(cfg, hb, g_codes, g_offs, g_recs)
+    assert g_offs[1] == 0 and g_offs[7] == g_offs[6]
+
+
+def test_edges_many_instances_scan(eng):
+    """1.1M tiny instances: > 1024 scan blocks, so the block totals take more than one
+    chunk of the single-block pass (multi-level offsets)."""
+    p = abi.gen_params(seed=0x5CA, n_instances=1_100_000, n_vals=2, rounds_min=1, rounds_max=1,
+                       nil_permille=300)
+    hb = ol.gen_batch(p)
+    power = ol.gen_power(0x5CA, 1, 2, abi.POWER_EQUAL, 1, 1)
+    cfg = abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 1)
+    st = abi.new_states(p.n_instances, 1, abi.STEP_PREVOTE, 0)
+    g_codes, g_offs, g_recs = _gpu_edges(eng, cfg, hb, power, st)
+    _check(cfg, hb, g_codes, g_offs, g_recs)
+    assert g_offs[-1] > 1024
+
+
+@pytest.mark.slow
+def test_edges_full_c2_roundtrip(eng):
+    """C2x100 (1M instances, 2e8 votes): offsets monotone, every record's vote inside
+    its instance, and per-instance edge counts equal the checker's on a sample."""
+    p = abi.gen_params(seed=0xA6E5, n_instances=1_000_000, n_vals=100, rounds_min=1, rounds_max=1,
+                       nil_permille=200)
+    eng.upload_power(ol.gen_power(0xA6E5, 1, 100, abi.POWER_UNIFORM, 1, 1000))
+    db = eng.gen_batch(p)
+    cfg = abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 1)
+    codes = torch.zeros(db.n_votes, dtype=torch.uint8, device=eng.device)
+    dst = states_to_device(abi.new_states(p.n_instances, 1, abi.STEP_PREVOTE, 0), eng.device)
+    eng.tally(cfg, db, codes, dst)
+    offs, recs = eng.edges(cfg, db, codes)
+    torch.cuda.synchronize()
+    o = offs.cpu().numpy().view(np.uint64)
+    assert (np.diff(o.astype(np.int64)) >= 0).all() and o[0] == 0
+    r = recs.cpu().numpy().reshape(-1).view(abi.EDGE_DTYPE)
+    inst = r["instance"].astype(np.int64)
+    assert np.array_equal(np.repeat(np.arange(p.n_instances), np.diff(o.astype(np.int64))), inst)
+    vo = db.offsets.cpu().numpy()
+    assert ((r["vote"] >= vo[inst]) & (r["vote"] < vo[inst + 1])).all()
+    # the first 2000 instances through the checker
+    k = 2000
+    sub = ol.gen_batch(abi.gen_params(seed=0xA6E5, n_instances=k, n_vals=100, rounds_min=1,
+                                      rounds_max=1, nil_permille=200))
+    s_offs, s_recs = ol.edges(cfg, sub, codes[:sub.n_votes].cpu().numpy())
+    assert np.array_equal(s_offs, o[:k + 1])
+    assert s_recs.tobytes() == r[:int(o[k])].tobytes()
