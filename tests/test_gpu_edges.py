@@ -13,20 +13,22 @@ pytestmark = pytest.mark.gpu
 
 
 def _gpu_edges(eng, cfg, hb, power, states=None, shift=0):
-    """Tally on the GPU, then summarise; shift > 0 offsets the u8 columns by `shift`
-    bytes (4-B windows instead of 16-B)."""
+    """Tally on the GPU, then summarise; shift > 0 hands the summary copies of the u8
+    columns (codes, round, type) placed `shift` bytes past a 16-B boundary (4-B
+    windows instead of 16-B)."""
     eng.upload_power(power)
     db = DeviceBatch.from_host(hb, eng.device)
     n = max(hb.n_votes, 1)
-    codes_buf = torch.zeros(n + 16, dtype=torch.uint8, device=eng.device)
-    codes = codes_buf[shift:shift + n]
-    if shift:
-        for f in ("round", "type"):
-            buf = torch.zeros(n + 16, dtype=torch.uint8, device=eng.device)
-            buf[shift:shift + hb.n_votes] = getattr(db, f)
-            setattr(db, f, buf[shift:shift + n])
+    codes = torch.zeros(n, dtype=torch.uint8, device=eng.device)
     dst = None if states is None else states_to_device(states, eng.device)
     eng.tally(cfg, db, codes, dst)
+    if shift:
+        def shifted(t):
+            buf = torch.zeros(n + 16, dtype=torch.uint8, device=eng.device)
+            buf[shift:shift + n] = t[:n]
+            return buf[shift:shift + n]
+        db.round, db.type = shifted(db.round), shifted(db.type)
+        codes = shifted(codes)
     offs, recs = eng.edges(cfg, db, codes)
     torch.cuda.synchronize()
     g_codes = codes[:hb.n_votes].cpu().numpy()
@@ -58,7 +60,8 @@ def test_edges_generated(eng, name):
 @pytest.mark.parametrize("shift", [4, 8, 12])
 def test_edges_unaligned_columns(eng, shift):
     p, hb, power, cfg = _make("c4_small")
-    g_codes, g_offs, g_recs = _gpu_edges(eng, cfg, hb, power, None, shift)
+    states = _start_states(p.n_instances) if cfg.flags & abi.FLAG_STATE_MACHINE else None
+    g_codes, g_offs, g_recs = _gpu_edges(eng, cfg, hb, power, states, shift)
     _check(cfg, hb, g_codes, g_offs, g_recs)
 
 
