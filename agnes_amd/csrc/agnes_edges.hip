@@ -14,8 +14,9 @@
  * small kernels), and an emit pass that writes 16-B records at the scanned
  * offsets — ordered by instance then vote, deterministic.  Each lane keeps its
  * executors' levels as 4-bit nibbles in LDS, [slot][lane] (slot = key / 8, key =
- * round * 2 + type), so a wave's 64 lookups hit 64 banks.  HBM bound: 3 B per vote
- * read per pass (code, round, type) + 16 B per edge written.
+ * round * 2 + type), so a wave's 64 lookups hit 64 banks.  Each lane reads 64-B
+ * windows of each column (four 16-B loads of one line in flight together).  HBM
+ * bound: 3 B per vote read per pass (code, round, type) + 16 B per edge written.
  */
 #include <hip/hip_runtime.h>
 
@@ -39,12 +40,15 @@ struct EdgeArgs {
 template <uint32_t W>
 __device__ __forceinline__ void load_win(const uint8_t* col, uint64_t w, uint64_t NV, uint32_t (&v)[W / 4u]) {
     if (w + W <= NV) {
-        if constexpr (W == 16u) {
-            const uint4 q = *reinterpret_cast<const uint4*>(col + w);
-            v[0] = q.x;
-            v[1] = q.y;
-            v[2] = q.z;
-            v[3] = q.w;
+        if constexpr (W >= 16u) { /* W/16 16-B loads of one line, in flight together */
+#pragma unroll
+            for (uint32_t k = 0; k < W / 16u; ++k) {
+                const uint4 q = *reinterpret_cast<const uint4*>(col + w + 16u * k);
+                v[4u * k] = q.x;
+                v[4u * k + 1u] = q.y;
+                v[4u * k + 2u] = q.z;
+                v[4u * k + 3u] = q.w;
+            }
         } else {
             v[0] = *reinterpret_cast<const uint32_t*>(col + w);
         }
@@ -101,6 +105,11 @@ __global__ __launch_bounds__(64) void edge_walk(EdgeArgs a) {
     }
     if (!EMIT) a.offs[i + 1u] = cnt;
 }
+
+/* window of the aligned path: 64 B per column (four 16-B loads of one 128-B line
+ * issued together, so the line is fetched once although the wave's 64 lanes read
+ * 64 different lines) */
+constexpr uint32_t EW = 64u;
 
 /* ---- exclusive offsets: inclusive scan of offs[1..n] in place, three kernels ---- */
 constexpr uint32_t SCAN_T = 256u, SCAN_PER = 4u, SCAN_BLK = SCAN_T * SCAN_PER;
@@ -186,7 +195,7 @@ hipError_t agnes_launch_edges(const agnes_vote_batch* vb, const uint8_t* codes, 
         if (e != hipSuccess || n == 0) return e;
         {
             AgnesKt kt("edge_count", st);
-            if (w16) hipLaunchKernelGGL((edge_walk<false, 16u>), grid, blk, lds, st, a);
+            if (w16) hipLaunchKernelGGL((edge_walk<false, EW>), grid, blk, lds, st, a);
             else hipLaunchKernelGGL((edge_walk<false, 4u>), grid, blk, lds, st, a);
         }
         const uint64_t nb = agnes_edges_scratch_words(n);
@@ -200,7 +209,7 @@ hipError_t agnes_launch_edges(const agnes_vote_batch* vb, const uint8_t* codes, 
     }
     if (n == 0) return hipSuccess;
     AgnesKt kt("edge_emit", st);
-    if (w16) hipLaunchKernelGGL((edge_walk<true, 16u>), grid, blk, lds, st, a);
+    if (w16) hipLaunchKernelGGL((edge_walk<true, EW>), grid, blk, lds, st, a);
     else hipLaunchKernelGGL((edge_walk<true, 4u>), grid, blk, lds, st, a);
     return hipGetLastError();
 }

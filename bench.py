@@ -119,6 +119,30 @@ def cpu_baseline(eng, cfg, batch, power, states0, set_of_instance):
             "codes_prefix": codes}
 
 
+def edge_summary(eng, cfg, batch, codes, reps: int = 5):
+    """The edge-triggered summary (agnes_edge_offsets + agnes_edges, §8(f) 1) of the
+    last step's codes, timed OUTSIDE the bench's timed region (it is not part of
+    `value`).  Algorithmic bytes: each walk reads code + round + type (3 B/vote) and
+    one offset pair per instance; the count walk writes 8 B per instance, the emit
+    walk 16 B per edge."""
+    eng.edges(cfg, batch, codes)
+    torch.cuda.synchronize()
+    eng.kernel_timing(True)
+    for _ in range(reps):
+        offs, recs = eng.edges(cfg, batch, codes)
+    torch.cuda.synchronize()
+    kt = eng.kernel_times()
+    eng.kernel_timing(False)
+    nv, ni, ne = batch.n_votes, batch.n_instances, recs.shape[0]
+    ab = {"edge_count": 3 * nv + 24 * ni, "edge_scan": 16 * ni, "edge_emit": 3 * nv + 16 * ni + 16 * ne}
+    res = {"edges": int(ne), "edges_per_vote": ne / max(nv, 1)}
+    for name, (launches, total) in kt.items():
+        avg = total / max(launches, 1)
+        res[name] = {"avg_ms": avg, "algorithmic_bytes": ab.get(name),
+                     "GBps": ab[name] / (avg * 1e-3) / 1e9 if name in ab and avg > 0 else None}
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -239,6 +263,7 @@ def main():
                               "frac": step_achieved / HBM_PEAK_GBS, "kernel_ms": step_kernel_ms},
             "kernels": kernels,
         }
+        out["edge_summary"] = edge_summary(eng, cfg, batch, codes)
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(eng, cfg, batch, power, st0_host, set_of)
             prefix = cb.pop("codes_prefix")
