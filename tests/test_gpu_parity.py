@@ -415,6 +415,22 @@ def test_stream_mixed_domains(eng):
     assert_same(g, o)
 
 
+@pytest.mark.parametrize("route", ["split", "fast_split", "fused"])
+@pytest.mark.parametrize("mode,flags", [
+    (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE),
+    (abi.MODE_DEDUP, abi.FLAG_STATE_MACHINE | abi.FLAG_ROUND_SKIP)])
+def test_deferred_instances_and_set_fallback(eng, monkeypatch, route, mode, flags):
+    """Instances whose sums may reach 2^31 (len * maxpow) deferred by the u32 kernels
+    to the i64 LIST kernel, mixed with fast ones, with the State machine; no
+    instance_set, so the set of instance i is i % n_sets."""
+    _route(monkeypatch, route)
+    hb = _ragged_batch(91, 6000, 13, 3, [8, 40, 200, 1200])
+    power = ol.gen_power(91, 3, 13, abi.POWER_UNIFORM, 1 << 20, 1 << 21)
+    hb.instance_set = None
+    g, o = run_both(eng, abi.config(mode, flags, 3), hb, power, None, _start_states(hb.n_instances))
+    assert_same(g, o)
+
+
 def test_epoch_table_recycling(eng, monkeypatch):
     """DEDUP/RoundSkip tables tag entries with per-instance epochs; with few
     epoch bits the tables are cleared every 3 instances (chunks cut there)."""
