@@ -393,6 +393,40 @@ int agnes_edges(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b
                                         nullptr, (hipStream_t)stream));
 }
 
+/* ---------------- DEDUP for a split instance ---------------- */
+
+static int dedup_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint64_t base,
+                      uint64_t* first, uint8_t* type_out, void* stream) {
+    if (!c || !cfg_ok(cfg) || !b || !first) return AGNES_E_INVALID;
+    if (b->n_votes && (!b->instance || !b->round || !b->type || !b->validator)) return AGNES_E_INVALID;
+    if (c->n_vals == 0) return AGNES_E_INVALID; /* no power table: no validator range */
+    AGNES_TRY(hipSetDevice(c->device));
+    c->last_stream = (hipStream_t)stream;
+    if (b->instance_set) return AGNES_E_UNSUPPORTED; /* one instance: its set is reserved % n_sets */
+    const uint32_t set = cfg->reserved % (c->n_sets ? c->n_sets : 1u);
+    return status_of(agnes_launch_dedup(b, cfg->reserved, cfg->max_rounds, c->n_vals, set < c->n_sets, base,
+                                        first, type_out, (hipStream_t)stream));
+}
+
+int agnes_dedup_first(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint64_t base,
+                      uint64_t* first, void* stream) {
+    return dedup_impl(c, cfg, b, base, first, nullptr, stream);
+}
+
+int agnes_dedup_mask(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint64_t base,
+                     const uint64_t* first, uint8_t* type_out, void* stream) {
+    if (!type_out && b && b->n_votes) return AGNES_E_INVALID;
+    if (b && b->n_votes == 0) return AGNES_OK;
+    return dedup_impl(c, cfg, b, base, const_cast<uint64_t*>(first), type_out, stream);
+}
+
+int agnes_dedup_reject(agnes_ctx* c, const uint8_t* type_masked, uint64_t n, uint8_t* codes, void* stream) {
+    if (!c || (n && (!type_masked || !codes))) return AGNES_E_INVALID;
+    AGNES_TRY(hipSetDevice(c->device));
+    c->last_stream = (hipStream_t)stream;
+    return status_of(agnes_launch_dedup_reject(type_masked, n, codes, (hipStream_t)stream));
+}
+
 /* ---------------- generator ---------------- */
 
 uint64_t agnes_gen_instance_votes(const agnes_gen_params* p, uint32_t i) {

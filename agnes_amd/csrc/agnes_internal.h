@@ -102,6 +102,13 @@ uint64_t agnes_edges_scratch_words(uint32_t n_instances);
 hipError_t agnes_launch_edges(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds,
                               uint64_t* offs, agnes_edge* out, uint64_t* scratch, hipStream_t stream);
 
+/* DEDUP for a split instance (agnes_dedup.hip): type_out == nullptr -> the first-seen
+ * pass into first[], else the mask pass; reject rewrites the masked votes' codes */
+hipError_t agnes_launch_dedup(const agnes_vote_batch* vb, uint32_t inst_id, uint32_t max_rounds,
+                              uint32_t n_vals, bool set_ok, uint64_t base, uint64_t* first,
+                              uint8_t* type_out, hipStream_t stream);
+hipError_t agnes_launch_dedup_reject(const uint8_t* type_masked, uint64_t n, uint8_t* codes, hipStream_t stream);
+
 #define AGNES_WAVES_PER_BLOCK 4
 /* list_count[0] counts the deferred list; list_count[1 .. AGNES_QUEUE_WORDS-1] are the
  * fast kernel's work-queue counters; all zeroed before each launch */

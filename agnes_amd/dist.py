@@ -211,6 +211,41 @@ def tally_one_instance(tally_carried, n_votes: int, cfg: abi.Config, n_segments:
     return fin_w, torch.where(fin_lab == NIL, torch.zeros_like(fin_lab), fin_lab)
 
 
+INT64_MAX = (1 << 63) - 1
+
+
+def tally_one_instance_dedup(tally_carried, dedup_first, dedup_mask, dedup_reject, n_votes: int,
+                             n_vals: int, cfg: abi.Config, n_segments: int, device, base: int = 0,
+                             inst_id: int = 0, group=None):
+    """C5 in DEDUP mode ("DEDUP mode adds an all-reduce(min) on
+    first_index").  A vote's slice cannot see whether an earlier slice (or rank)
+    already counted its (round, type, validator), so the first vote of every key is
+    found before the tally:
+      dedup_first(base, first)  this rank's slice lowers first[key] to its global
+                                vote indices (agnes_dedup_first; base = the index of
+                                the slice's first vote in the whole stream);
+      exchange: ONE all_reduce(MIN) of first (8 B per key: 16 MB at 1M validators,
+                                one round) over RCCL, gloo in the CPU tests;
+      dedup_mask(base, first)   the slice's type column with the later duplicates
+                                masked (agnes_dedup_mask); tally_carried must read
+                                THAT column: a masked vote counts as nothing;
+      tally_one_instance        the REFERENCE split tally of the masked stream;
+      dedup_reject()            the masked votes' codes -> REJECTED.
+    The codes equal tallying the whole instance as one DEDUP stream.  A stream
+    continued across calls would also carry `first`; not offered here."""
+    first = torch.full((2 * cfg.max_rounds * n_vals,), INT64_MAX, dtype=torch.int64, device=device)
+    dedup_first(base, first)
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        t = first.to(_device_for(group))
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)         # the DEDUP exchange step
+        first = t.to(device)
+    dedup_mask(base, first)
+    ref = abi.Config(abi.MODE_REFERENCE, cfg.flags, cfg.max_rounds, cfg.reserved)
+    out = tally_one_instance(tally_carried, n_votes, ref, n_segments, device, inst_id, group)
+    dedup_reject()
+    return out
+
+
 __all__ = ["env", "shard_range", "Shard", "make_shard", "set_of_instances", "max_over_ranks",
            "sum_over_ranks", "decisions", "gather_decisions", "DECISION_DTYPE", "segment_offsets",
-           "fold_counts", "tally_one_instance"]
+           "fold_counts", "tally_one_instance", "tally_one_instance_dedup", "INT64_MAX"]

@@ -144,6 +144,27 @@ class Engine:
         check(self.lib.agnes_tally_carried(self.ctx, C.byref(cfg), C.byref(b), _ptr(codes), _ptr(counts),
                                            _stream_handle(stream)), "agnes_tally_carried")
 
+    # -- DEDUP for one instance split over slices (C5) --------------------------
+    def dedup_first(self, cfg: abi.Config, batch: DeviceBatch, base: int, first: torch.Tensor, stream=None):
+        """agnes_dedup_first: first = int64 [2 * max_rounds * n_vals], INT64_MAX-initialised."""
+        if first.dtype != torch.int64 or first.numel() < 2 * cfg.max_rounds * self.n_vals:
+            raise ValueError("first must be an int64 [2 * max_rounds * n_vals] tensor")
+        b = batch.c()
+        check(self.lib.agnes_dedup_first(self.ctx, C.byref(cfg), C.byref(b), base, _ptr(first),
+                                         _stream_handle(stream)), "agnes_dedup_first")
+
+    def dedup_mask(self, cfg: abi.Config, batch: DeviceBatch, base: int, first: torch.Tensor,
+                   type_out: torch.Tensor, stream=None):
+        if type_out.dtype != torch.uint8 or type_out.numel() < batch.n_votes:
+            raise ValueError("type_out must be a uint8 tensor of n_votes")
+        b = batch.c()
+        check(self.lib.agnes_dedup_mask(self.ctx, C.byref(cfg), C.byref(b), base, _ptr(first), _ptr(type_out),
+                                        _stream_handle(stream)), "agnes_dedup_mask")
+
+    def dedup_reject(self, type_masked: torch.Tensor, codes: torch.Tensor, n_votes: int, stream=None):
+        check(self.lib.agnes_dedup_reject(self.ctx, _ptr(type_masked), n_votes, _ptr(codes),
+                                          _stream_handle(stream)), "agnes_dedup_reject")
+
     def last_error_count(self) -> int:
         v = C.c_uint64(0)
         check(self.lib.agnes_last_error_count(self.ctx, C.byref(v)), "agnes_last_error_count")

@@ -301,6 +301,33 @@ typedef struct agnes_vote_count {
 int agnes_tally_carried(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
                         uint8_t* codes, agnes_vote_count* counts, void* stream);
 
+/* DEDUP for one instance split over slices (C5; agnes_amd/dist.py
+ * tally_one_instance_dedup).  The carried tally is REFERENCE only, so the first
+ * vote of each (round, type, validator) is found up front:
+ *   agnes_dedup_first  lowers first[(round * 2 + type) * n_vals + validator] (DEVICE,
+ *                      u64 [2 * max_rounds * n_vals], caller-initialised to
+ *                      INT64_MAX) to base + j for every valid vote j of the batch,
+ *                      base = the index of the batch's first vote in the whole
+ *                      stream; the caller then min-combines `first` over the ranks;
+ *   agnes_dedup_mask   writes type_out (DEVICE, n_votes): the batch's type column
+ *                      with every valid vote that is not its key's first set to
+ *                      AGNES_TYPE_MASKED — tallied with it, such a vote counts as
+ *                      nothing (round_votes.rs:48-56 never runs for it);
+ *   agnes_dedup_reject after the carried tally: the codes of the masked votes
+ *                      INVALID -> AGNES_CODE_REJECTED (the DEDUP codes of the
+ *                      whole instance; agnes_last_error_count still counts them).
+ * Validity is the tally's: instance id == cfg->reserved, round < max_rounds,
+ * type <= 1, validator < n_vals (set reserved % n_sets; batch->instance_set must be
+ * NULL, else AGNES_E_UNSUPPORTED).
+ * Asynchronous on `stream`. */
+#define AGNES_TYPE_MASKED 0xFEu
+int agnes_dedup_first(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch, uint64_t base,
+                      uint64_t* first, void* stream);
+int agnes_dedup_mask(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch, uint64_t base,
+                     const uint64_t* first, uint8_t* type_out, void* stream);
+int agnes_dedup_reject(agnes_ctx* ctx, const uint8_t* type_masked, uint64_t n_votes, uint8_t* codes,
+                       void* stream);
+
 /* Number of votes coded AGNES_CODE_INVALID by the most recent agnes_tally on
  * this context (synchronises the context's stream). */
 int agnes_last_error_count(agnes_ctx* ctx, uint64_t* out);

@@ -70,3 +70,40 @@ class CarriedFake:
             counts[k]["value_w"] = vw
             counts[k]["nil_w"] = vn
             counts[k]["value"] = lab
+
+
+class DedupFake:
+    """CPU stand-in for agnes_dedup_first / _mask / _reject (include/agnes.h): the
+    first vote of each (round, type, validator) of one instance found across
+    slices, the later ones masked out of the tally and coded REJECTED."""
+
+    MASKED = 0xFE
+
+    def __init__(self, n_sets: int, n_vals: int):
+        self.n_sets, self.n_vals = n_sets, n_vals
+
+    def _keys(self, cfg, b):
+        r = np.asarray(b.round, np.int64)
+        t = np.asarray(b.type, np.int64)
+        x = np.asarray(b.validator, np.int64)
+        ok = ((np.asarray(b.instance, np.int64) == cfg.reserved) & (r < cfg.max_rounds) & (t <= 1)
+              & (x < self.n_vals) & (cfg.reserved % self.n_sets < self.n_sets))
+        return ok, (r * 2 + t) * self.n_vals + x
+
+    def first(self, cfg, b, base: int, first: np.ndarray):
+        ok, key = self._keys(cfg, b)
+        idx = base + np.arange(len(key), dtype=np.int64)
+        np.minimum.at(first, key[ok], idx[ok])
+
+    def mask(self, cfg, b, base: int, first: np.ndarray) -> np.ndarray:
+        ok, key = self._keys(cfg, b)
+        t = np.asarray(b.type, np.uint8).copy()
+        idx = base + np.arange(len(key), dtype=np.int64)
+        dup = ok.copy()
+        dup[ok] = first[key[ok]] != idx[ok]
+        t[~ok & (t == self.MASKED)] = 0xFF
+        t[dup] = self.MASKED
+        return t
+
+    def reject(self, type_masked: np.ndarray, codes: np.ndarray):
+        codes[type_masked == self.MASKED] = abi.CODE_REJECTED

@@ -25,7 +25,7 @@ sys.path.insert(0, HERE)
 from agnes_amd import abi  # noqa: E402
 from agnes_amd import dist as ad  # noqa: E402
 import oracle_lib as ol  # noqa: E402
-from carried_fake import CarriedFake  # noqa: E402
+from carried_fake import CarriedFake, DedupFake  # noqa: E402
 
 
 def _instance(seed=5, n_vals=300, R=2, nil=250, kind=abi.POWER_ZIPF):
@@ -153,6 +153,81 @@ def test_split_instance_two_ranks_gloo():
     assert res[0][2] == fw.numpy().tobytes() and res[0][3] == fl.numpy().tobytes()
 
 
+# --------------------------------------------------- DEDUP across slices (CPU)
+
+def _dedup_instance(seed=5, n_vals=300, R=2, nil=250):
+    """One instance with 15 % exact duplicates and 15 % equivocations (DEDUP mode)."""
+    p = abi.gen_params(seed=seed, n_instances=1, n_vals=n_vals, rounds_min=R, rounds_max=R,
+                       nil_permille=nil, dup_permille=150, equiv_permille=150)
+    hb = ol.gen_batch(p)
+    power = ol.gen_power(seed, 1, n_vals, abi.POWER_ZIPF, 1, 1000)
+    return hb, power, abi.config(abi.MODE_DEDUP, 0, R)
+
+
+def _cpu_dedup_slice(hb, power, cfg, lo, hi, segments):
+    """This rank's slice [lo, hi) through tally_one_instance_dedup on the CPU stand-ins."""
+    dd = DedupFake(*power.shape)
+    sl = types.SimpleNamespace(instance=hb.instance[lo:hi], round=hb.round[lo:hi], type=hb.type[lo:hi],
+                               validator=hb.validator[lo:hi])
+    view = types.SimpleNamespace(instance=hb.instance, round=hb.round, type=hb.type.copy(),
+                                 value=hb.value, validator=hb.validator)
+    codes = np.zeros(hi - lo, np.uint8)
+
+    def mask(base, f):
+        view.type[lo:hi] = dd.mask(cfg, sl, base, f.numpy())
+
+    fw, fl = ad.tally_one_instance_dedup(
+        _fake_tc(CarriedFake(power), view, lo, hi, codes),
+        lambda base, f: dd.first(cfg, sl, base, f.numpy()), mask,
+        lambda: dd.reject(view.type[lo:hi], codes), hi - lo, power.shape[1], cfg, segments,
+        torch.device("cpu"), base=lo)
+    return codes, fw, fl
+
+
+@pytest.mark.parametrize("segments", [1, 3, 16])
+def test_split_instance_dedup_equals_whole_cpu(segments):
+    hb, power, cfg = _dedup_instance()
+    want, _, _ = ol.tally(cfg, hb, power)
+    assert (want == abi.CODE_REJECTED).sum() > hb.n_votes // 10  # the stream has duplicates
+    codes, _, _ = _cpu_dedup_slice(hb, power, cfg, 0, hb.n_votes, segments)
+    assert np.array_equal(codes, want)
+
+
+def _dedup_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, HERE)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        hb, power, cfg = _dedup_instance(seed=8)
+        lo, hi = _slice(hb.n_votes, rank, world)
+        codes, fw, fl = _cpu_dedup_slice(hb, power, cfg, lo, hi, 3)
+        q.put((rank, codes.tobytes(), fw.numpy().tobytes(), fl.numpy().tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_split_instance_dedup_two_ranks_gloo():
+    """all_reduce(MIN) of the first-seen table + all_gather of the partial tallies:
+    the ranks' codes concatenate to the whole instance's DEDUP codes"""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dedup_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    hb, power, cfg = _dedup_instance(seed=8)
+    want, _, _ = ol.tally(cfg, hb, power)
+    assert b"".join(r[1] for r in res) == want.tobytes()
+    assert res[0][2] == res[1][2] and res[0][3] == res[1][3]
+
+
 # ------------------------------------------------------------------ GPU (C ABI)
 
 @pytest.fixture(scope="module")
@@ -220,3 +295,74 @@ def test_gpu_tally_carried_rejects(eng):
     counts = torch.zeros((1, 2, 3), dtype=torch.int64, device=eng.device)
     with pytest.raises(AgnesError):
         eng.tally_carried(abi.config(abi.MODE_DEDUP, 0, 1), db, codes, counts)
+
+
+def _gpu_dedup_run(eng, hb, power, cfg, segments):
+    from agnes_amd.engine import DeviceBatch
+    eng.upload_power(power)
+    db = DeviceBatch.from_host(hb, eng.device)
+    n = hb.n_votes
+    tmask = torch.empty(n, dtype=torch.uint8, device=eng.device)
+    dbm = dataclasses.replace(db, type=tmask)
+    codes = torch.zeros(n, dtype=torch.uint8, device=eng.device)
+    ad.tally_one_instance_dedup(_gpu_tc(eng, dbm, codes),
+                                lambda base, f: eng.dedup_first(cfg, db, base, f),
+                                lambda base, f: eng.dedup_mask(cfg, db, base, f, tmask),
+                                lambda: eng.dedup_reject(tmask, codes, n),
+                                n, power.shape[1], cfg, segments, eng.device)
+    torch.cuda.synchronize()
+    return codes.cpu().numpy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("segments,n_vals,R", [(1, 3000, 1), (16, 5000, 2), (300, 20000, 2),
+                                               (64, 100000, 1)])
+def test_gpu_split_instance_dedup(eng, segments, n_vals, R):
+    hb, power, cfg = _dedup_instance(seed=31 + segments, n_vals=n_vals, R=R)
+    want, _, _ = ol.tally(cfg, hb, power)
+    got = _gpu_dedup_run(eng, hb, power, cfg, segments)
+    assert np.array_equal(got, want)
+    assert (got == abi.CODE_REJECTED).any()
+
+
+@pytest.mark.gpu
+def test_gpu_dedup_slices_with_bases(eng):
+    """Two slices with their global bases, first-seen tables min-combined (the
+    all_reduce), give the whole stream's mask — and invalid votes are never masked."""
+    from agnes_amd.engine import DeviceBatch
+    hb, power, cfg = _dedup_instance(seed=13, n_vals=4000, R=2)
+    hb.type[7] = 5
+    hb.type[11] = 0xFE          # an invalid vote whose type byte is the mask value
+    hb.validator[19] = 10 ** 6  # out of range
+    eng.upload_power(power)
+    n, K = hb.n_votes, 2 * cfg.max_rounds * power.shape[1]
+    mid = (n // 3) // 4 * 4
+
+    def part(lo, hi):
+        return DeviceBatch.from_host(types.SimpleNamespace(
+            instance=hb.instance[lo:hi], round=hb.round[lo:hi], type=hb.type[lo:hi], value=hb.value[lo:hi],
+            validator=hb.validator[lo:hi], offsets=np.array([0, hi - lo], np.uint64)), eng.device)
+
+    whole, a, b = part(0, n), part(0, mid), part(mid, n)
+    fw = torch.full((K,), ad.INT64_MAX, dtype=torch.int64, device=eng.device)
+    fa, fb = fw.clone(), fw.clone()
+    eng.dedup_first(cfg, whole, 0, fw)
+    eng.dedup_first(cfg, a, 0, fa)
+    eng.dedup_first(cfg, b, mid, fb)
+    fab = torch.minimum(fa, fb)
+    assert torch.equal(fab, fw)
+    tw = torch.empty(n, dtype=torch.uint8, device=eng.device)
+    ta = torch.empty(mid, dtype=torch.uint8, device=eng.device)
+    tb = torch.empty(n - mid, dtype=torch.uint8, device=eng.device)
+    eng.dedup_mask(cfg, whole, 0, fw, tw)
+    eng.dedup_mask(cfg, a, 0, fab, ta)
+    eng.dedup_mask(cfg, b, mid, fab, tb)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat([ta, tb]), tw)
+    t = tw.cpu().numpy()
+    assert t[7] == 5 and t[11] == 0xFF and t[19] == hb.type[19]
+    dd = DedupFake(*power.shape)
+    f = np.full(K, ad.INT64_MAX, np.int64)
+    dd.first(cfg, hb, 0, f)
+    assert np.array_equal(fw.cpu().numpy(), f)
+    assert np.array_equal(t, dd.mask(cfg, hb, 0, f))
