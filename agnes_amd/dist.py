@@ -216,7 +216,7 @@ INT64_MAX = (1 << 63) - 1
 
 def tally_one_instance_dedup(tally_carried, dedup_first, dedup_mask, dedup_reject, n_votes: int,
                              n_vals: int, cfg: abi.Config, n_segments: int, device, base: int = 0,
-                             inst_id: int = 0, group=None):
+                             inst_id: int = 0, group=None, offsets=None):
     """C5 in DEDUP mode ("DEDUP mode adds an all-reduce(min) on
     first_index").  A vote's slice cannot see whether an earlier slice (or rank)
     already counted its (round, type, validator), so the first vote of every key is
@@ -231,7 +231,8 @@ def tally_one_instance_dedup(tally_carried, dedup_first, dedup_mask, dedup_rejec
                                 THAT column: a masked vote counts as nothing;
       tally_one_instance        the REFERENCE split tally of the masked stream;
       dedup_reject()            the masked votes' codes -> REJECTED.
-    The codes equal tallying the whole instance as one DEDUP stream.  A stream
+    The codes equal tallying the whole instance as one DEDUP stream (offsets: as
+    tally_one_instance's, for a HIP-graph capture).  A stream
     continued across calls would also carry `first`; not offered here."""
     first = torch.full((2 * cfg.max_rounds * n_vals,), INT64_MAX, dtype=torch.int64, device=device)
     dedup_first(base, first)
@@ -241,7 +242,8 @@ def tally_one_instance_dedup(tally_carried, dedup_first, dedup_mask, dedup_rejec
         first = t.to(device)
     dedup_mask(base, first)
     ref = abi.Config(abi.MODE_REFERENCE, cfg.flags, cfg.max_rounds, cfg.reserved)
-    out = tally_one_instance(tally_carried, n_votes, ref, n_segments, device, inst_id, group)
+    out = tally_one_instance(tally_carried, n_votes, ref, n_segments, device, inst_id, group,
+                             offsets=offsets)
     dedup_reject()
     return out
 

@@ -38,6 +38,8 @@ KERNEL_BYTES_PER_VOTE = {
     "tally_fast": 15,
     "tally_wide": 15,
     "apply_codes": 2,    # code + round u8 in (messages written back sparsely)
+    "dedup_first": 10,   # C5 DEDUP: instance, validator u32 + round, type u8 in (+ 8 B atomic per key)
+    "dedup_mask": 11,    # the same in, the masked type u8 out
 }
 KERNEL_SYMBOLS = {
     "tally_stream": "agnes::stream::tally_stream<false, *>",
@@ -72,6 +74,13 @@ WORKLOADS = {
                gen=dict(n_instances=1, n_vals=1_000_000, rounds_min=1, rounds_max=1, nil_permille=200),
                power=(abi.POWER_ZIPF, 1, 1_000_000, 1), mode=abi.MODE_REFERENCE, flags=0,
                max_rounds=1, scaling="strong", one_instance=True, segments=1024),
+    "c5d": dict(desc="C5 in DEDUP mode: 1 instance x 1M validators (Zipf power), 10% duplicates + 10% "
+                     "equivocations; one all_reduce(MIN) of first-seen indices + one all_gather of "
+                     "partial tallies",
+                gen=dict(n_instances=1, n_vals=1_000_000, rounds_min=1, rounds_max=1, nil_permille=200,
+                         dup_permille=100, equiv_permille=100),
+                power=(abi.POWER_ZIPF, 1, 1_000_000, 1), mode=abi.MODE_DEDUP, flags=0,
+                max_rounds=1, scaling="strong", one_instance=True, segments=1024),
 }
 
 
@@ -296,6 +305,11 @@ def bench_one_instance(args, w, eng, rank, world):
                         torch.tensor([0, hi - lo], dtype=torch.int64, device=eng.device), n_votes=hi - lo)
     codes = torch.empty(max(hi - lo, 1), dtype=torch.uint8, device=eng.device)
     cfg = abi.config(w["mode"], w["flags"], w["max_rounds"])
+    dedup = w["mode"] == abi.MODE_DEDUP
+    src = batch
+    if dedup:  # the carried tally reads the type column with the later duplicates masked
+        tmask = torch.empty(max(hi - lo, 1), dtype=torch.uint8, device=eng.device)
+        batch = dataclasses.replace(batch, type=tmask)
 
     segs = max(1, min(w["segments"], max(1, (hi - lo) // 4)))
     off = torch.from_numpy(adist.segment_offsets(hi - lo, segs).view(np.int64)).to(eng.device)
@@ -304,12 +318,19 @@ def bench_one_instance(args, w, eng, rank, world):
         eng.tally_carried(one, dataclasses.replace(batch, offsets=o), codes, counts)
 
     def step():
+        if dedup:
+            return adist.tally_one_instance_dedup(
+                tc, lambda base, f: eng.dedup_first(cfg, src, base, f),
+                lambda base, f: eng.dedup_mask(cfg, src, base, f, tmask),
+                lambda: eng.dedup_reject(tmask, codes, hi - lo), hi - lo, p.n_vals, cfg, segs,
+                eng.device, base=lo, offsets=off)
         return adist.tally_one_instance(tc, hi - lo, cfg, segs, eng.device, 0, None, offsets=off)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if eng.last_error_count() != 0:
+    # (DEDUP: the masked duplicates are counted as invalid by the carried tally)
+    if not dedup and eng.last_error_count() != 0:
         raise SystemExit("bench batch has invalid votes")
     # per-kernel times: one eager step with the engine's event timing
     eng.kernel_timing(True)
@@ -362,8 +383,10 @@ def bench_one_instance(args, w, eng, rank, world):
             "data": "synthetic (counter-based splitmix64 streams, agnes_gen.h; Zipf powers)",
             "config": {"workload": w["desc"], "config": args.config, "instances": 1,
                        "validators": p.n_vals, "votes_total": n, "votes_per_gpu_per_step": hi - lo,
-                       "segments_per_gpu": segs, "mode": "REFERENCE", "flags": w["flags"],
-                       "parallelism": f"stream-sliced x{world} (one all_gather per step)",
+                       "segments_per_gpu": segs, "mode": "DEDUP" if dedup else "REFERENCE",
+                       "flags": w["flags"],
+                       "parallelism": f"stream-sliced x{world} (" + ("one all_reduce(MIN) + " if dedup else "")
+                                      + "one all_gather per step)",
                        "hip_graph": graph},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None, "traffic_source": None,
