@@ -3,18 +3,19 @@
  * include/agnes.h agnes_edge_offsets / agnes_edges).
  *
  * VoteExecutor::apply (vote_executor.rs:20-36) is level-triggered: after a
- * threshold holds, every later vote of the executor repeats the event.  The
- * summary keeps, per instance, the votes that change their (round, type)
- * executor's level (code bits 0..3) or that carry a State-machine message (bits
- * 4..7).  The (round, type) executors of an instance are the HeightVotes the
+ * threshold holds, every later vote of the executor repeats the event, and
+ * State::apply repeats its Timeout messages the same way (state_machine.rs:196,
+ * 208).  The summary keeps, per instance, the votes that change their (round,
+ * type) executor's level (code bits 0..3) or carry a message (bits 4..7) other
+ * than the executor's last one.  The (round, type) executors of an instance are the HeightVotes the
  * reference leaves as a stub (consensus_executor.rs:5; vote_executor.rs:9,14).
  *
  * Two walks of the codes, one instance per lane (like apply_codes): a count pass
  * that writes each instance's edge count, an exclusive scan of the counts (three
  * small kernels), and an emit pass that writes 16-B records at the scanned
- * offsets — ordered by instance then vote, deterministic.  Each lane keeps its
- * executors' levels as 4-bit nibbles in LDS, [slot][lane] (slot = key / 8, key =
- * round * 2 + type), so a wave's 64 lookups hit 64 banks.  Each lane reads 64-B
+ * offsets — ordered by instance then vote, deterministic.  Each lane keeps one
+ * byte per executor (level | last message << 4) in LDS, [slot][lane] (slot = key /
+ * 4, key = round * 2 + type), so a wave's 64 lookups hit 64 banks.  Each lane reads 64-B
  * windows of each column (four 16-B loads of one line in flight together).  HBM
  * bound: 3 B per vote read per pass (code, round, type) + 16 B per edge written.
  */
@@ -34,7 +35,7 @@ struct EdgeArgs {
     uint64_t* offs;   /* n_instances + 1 */
     agnes_edge* out;
     uint32_t keys;    /* 2 * max_rounds */
-    uint32_t nslots;  /* ceil(keys / 8) nibble words per lane */
+    uint32_t nslots;  /* ceil(keys / 4) byte words per lane */
 };
 
 template <uint32_t W>
@@ -89,18 +90,20 @@ __global__ __launch_bounds__(64) void edge_walk(EdgeArgs a) {
             if (j < lo || j >= hi || ev == AGNES_CODE_INVALID || ev == AGNES_CODE_REJECTED || tb > 1u ||
                 key >= a.keys)
                 continue;
-            uint32_t* const p = tab + (key >> 3) * 64u + lane;
-            const uint32_t x = *p, sh = 4u * (key & 7u);
-            const uint32_t lvl = (x >> sh) & 0xFu, nl = cb & 0xFu;
-            if (lvl != nl || (cb >> AGNES_CODE_MSG_SHIFT) != 0u) {
+            /* the executor's byte: level (bits 0..3) | last message (bits 4..7) */
+            uint32_t* const p = tab + (key >> 2) * 64u + lane;
+            const uint32_t x = *p, sh = 8u * (key & 3u);
+            const uint32_t old = (x >> sh) & 0xFFu, msg = cb >> AGNES_CODE_MSG_SHIFT;
+            const uint32_t nb = (cb & 0xFu) | (msg ? msg << AGNES_CODE_MSG_SHIFT : old & 0xF0u);
+            if (nb != old) {
                 if (EMIT) {
-                    const uint32_t tail = rb | (tb << 8) | (cb << 16) | (lvl << 24);
+                    const uint32_t tail = rb | (tb << 8) | (cb << 16) | (old << 24);
                     *reinterpret_cast<uint4*>(a.out + base + cnt) =
                         make_uint4((uint32_t)j, (uint32_t)(j >> 32), i, tail);
                 }
                 ++cnt;
+                *p = x ^ ((old ^ nb) << sh);
             }
-            if (lvl != nl) *p = x ^ ((lvl ^ nl) << sh);
         }
     }
     if (!EMIT) a.offs[i + 1u] = cnt;
@@ -184,7 +187,7 @@ hipError_t agnes_launch_edges(const agnes_vote_batch* vb, const uint8_t* codes, 
                               uint64_t* offs, agnes_edge* out, uint64_t* scratch, hipStream_t st) {
     using namespace agnes::edges;
     const uint32_t n = vb->n_instances;
-    EdgeArgs a{*vb, codes, offs, out, 2u * max_rounds, (2u * max_rounds + 7u) / 8u};
+    EdgeArgs a{*vb, codes, offs, out, 2u * max_rounds, (2u * max_rounds + 3u) / 4u};
     /* 16-B windows when the three columns allow them */
     const bool w16 = ((reinterpret_cast<uintptr_t>(codes) | reinterpret_cast<uintptr_t>(vb->round) |
                        reinterpret_cast<uintptr_t>(vb->type)) & 15u) == 0u;

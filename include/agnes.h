@@ -356,7 +356,9 @@ int agnes_apply_events(agnes_ctx* ctx, agnes_state* states, uint32_t n_instances
  * event + RoundSkip), 0 before its first vote (VoteCount::new,
  * round_votes.rs:36-45).  A vote is an EDGE when its level differs from the
  * level its executor's previous valid vote left, or when it carries a message
- * (code bits 4..7).  Records are ordered by instance, then vote index.
+ * (code bits 4..7) other than the last message of its executor (State::apply
+ * repeats Timeouts the same way, state_machine.rs:196,208).  Records are ordered
+ * by instance, then vote index.
  * ------------------------------------------------------------------------- */
 typedef struct agnes_edge {
     uint64_t vote;     /* index of the vote in the batch                    */
@@ -364,7 +366,7 @@ typedef struct agnes_edge {
     uint8_t round;     /* Vote.round                                        */
     uint8_t type;      /* Vote.typ                                          */
     uint8_t code;      /* the vote's code byte: new level | message << 4     */
-    uint8_t prev;      /* the executor's level before this vote (bits 0..3) */
+    uint8_t prev;      /* the executor before this vote: level | last message << 4 */
 } agnes_edge;
 
 /* Pass 1: offsets (DEVICE, n_instances + 1): exclusive offsets of each instance's

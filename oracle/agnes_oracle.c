@@ -477,10 +477,12 @@ int orc_apply_events(agnes_state* states, uint32_t n, const uint64_t* off, const
 /* Edge-triggered summary (include/agnes.h agnes_edge).  The
  * per-vote codes are VoteExecutor::apply's level-triggered Option<Event>
  * (vote_executor.rs:20-36) for the vote's (round, type) executor — the
- * reference's HeightVotes stub (consensus_executor.rs:5, vote_executor.rs:9,14).
- * An executor starts at level 0 (VoteCount::new, round_votes.rs:36-45); a valid
- * vote is an edge when its level (code bits 0..3) differs from the level its
- * executor's previous valid vote left, or when it carries a message (bits 4..7).
+ * reference's HeightVotes stub (consensus_executor.rs:5, vote_executor.rs:9,14) —
+ * and the message State::apply produced for it (state_machine.rs:196-211, whose
+ * Timeout arms repeat too).  An executor starts at level 0 with no message
+ * (VoteCount::new, round_votes.rs:36-45); a valid vote is an edge when its level
+ * (code bits 0..3) differs from the level its executor's previous valid vote
+ * left, or when it carries a message (bits 4..7) other than the executor's last.
  * offsets[n+1] always written; out (NULL: count only) gets the records. */
 int orc_edges(const agnes_config* cfg, const agnes_vote_batch* b, const uint8_t* codes,
               uint64_t* offsets, agnes_edge* out) {
@@ -498,8 +500,9 @@ int orc_edges(const agnes_config* cfg, const agnes_vote_batch* b, const uint8_t*
             const uint32_t c = codes[j], ev = c & AGNES_CODE_EVENT_MASK;
             const uint32_t r = b->round[j], t = b->type[j], key = r * 2u + t;
             if (ev == AGNES_CODE_INVALID || ev == AGNES_CODE_REJECTED || t > 1u || key >= keys) continue;
-            const uint32_t nl = c & 0xFu, prev = level[key];
-            if (prev != nl || (c >> AGNES_CODE_MSG_SHIFT) != 0u) {
+            const uint32_t prev = level[key], msg = c >> AGNES_CODE_MSG_SHIFT;
+            const uint32_t nl = (c & 0xFu) | (msg ? (msg << AGNES_CODE_MSG_SHIFT) : (prev & 0xF0u));
+            if (prev != nl) {
                 if (out) {
                     agnes_edge* e = &out[k];
                     e->vote = j;

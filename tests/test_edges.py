@@ -16,9 +16,10 @@ CODE_INVALID, CODE_REJECTED = 6, 7
 
 
 def py_edges(cfg, hb, codes):
-    """Pure-Python restatement of the edge rule (agnes.h): level = code bits 0..3 of
-    the vote's (round, type) executor, 0 initially; edge on a level change or a
-    message nibble; INVALID / REJECTED votes and keys >= 2*max_rounds skipped."""
+    """Pure-Python restatement of the edge rule (agnes.h): per (round, type) executor
+    its level (code bits 0..3, 0 initially) and its last message; edge on a level
+    change or a message other than the last; INVALID / REJECTED votes and keys >=
+    2*max_rounds skipped.  `prev` = level | last message << 4 before the vote."""
     out, offs = [], [0]
     for i in range(hb.n_instances):
         level = {}
@@ -28,10 +29,12 @@ def py_edges(cfg, hb, codes):
             r, t = int(hb.round[j]), int(hb.type[j])
             if ev in (CODE_INVALID, CODE_REJECTED) or t > 1 or r >= cfg.max_rounds:
                 continue
-            prev = level.get((r, t), 0)
-            if prev != (c & 15) or (c >> 4):
-                out.append((j, i, r, t, c, prev))
-            level[(r, t)] = c & 15
+            lv, lm = level.get((r, t), (0, 0))
+            m = c >> 4
+            nlm = m if m else lm
+            if (c & 15) != lv or nlm != lm:
+                out.append((j, i, r, t, c, lv | (lm << 4)))
+            level[(r, t)] = (c & 15, nlm)
         offs.append(len(out))
     return np.array(offs, dtype=np.uint64), np.array(out, dtype=abi.EDGE_DTYPE)
 
@@ -151,3 +154,18 @@ def test_empty_and_ragged_instances():
     offs, recs = ol.edges(cfg, hb, codes)
     assert list(offs) == [0, 0, 2, 2, 3]  # rounds 0 and 1 are separate executors
     assert [int(e["instance"]) for e in recs] == [1, 1, 3]
+
+
+def test_repeated_timeout_message_is_one_edge():
+    # prevote v, nil, v, nil in Prevote step: PolkaAny twice, and State::apply
+    # schedules timeout_prevote on each (state_machine.rs:196 repeats) — one edge.
+    power = np.ones((1, 4), dtype=np.int64)
+    cfg = abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 1)
+    NIL = abi.NIL
+    hb = ol.batch_from_lists([0] * 4, [0] * 4, [0] * 4, [1, NIL, 1, NIL], [0, 1, 2, 3], [0, 4])
+    st = abi.new_states(1, 1, abi.STEP_PREVOTE, 0)
+    codes, _, _ = ol.tally(cfg, hb, power, None, st)
+    assert [int(c) >> 4 for c in codes[2:]] == [abi.VMSG_TIMEOUT_PREVOTE] * 2
+    offs, recs = ol.edges(cfg, hb, codes)
+    assert list(offs) == [0, 1] and int(recs[0]["vote"]) == 2
+    assert int(recs[0]["prev"]) == 0
