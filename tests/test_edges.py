@@ -169,3 +169,27 @@ def test_repeated_timeout_message_is_one_edge():
     offs, recs = ol.edges(cfg, hb, codes)
     assert list(offs) == [0, 1] and int(recs[0]["vote"]) == 2
     assert int(recs[0]["prev"]) == 0
+
+
+def test_edges_arbitrary_code_streams_hypothesis():
+    """Any code bytes (events, RoundSkip, messages, invalid / rejected), rounds and
+    types: the checker's orc_edges equals the Python restatement."""
+    from hypothesis import given, settings, strategies as st
+
+    @settings(max_examples=150, deadline=None)
+    @given(st.lists(st.integers(0, 12), min_size=1, max_size=6), st.integers(1, 4), st.data())
+    def run(lengths, R, data):
+        off = np.concatenate([[0], np.cumsum(lengths)]).astype(np.uint64)
+        n = int(off[-1])
+        codes = np.array(data.draw(st.lists(st.integers(0, 255), min_size=n, max_size=n)), np.uint8)
+        rnd = data.draw(st.lists(st.integers(0, R), min_size=n, max_size=n))
+        typ = data.draw(st.lists(st.integers(0, 2), min_size=n, max_size=n))
+        inst = np.repeat(np.arange(len(lengths)), lengths)
+        hb = ol.batch_from_lists(inst, rnd, typ, [0] * n, [0] * n, off)
+        cfg = abi.config(abi.MODE_REFERENCE, 0, R)
+        offs, recs = ol.edges(cfg, hb, codes)
+        poffs, precs = py_edges(cfg, hb, codes)
+        assert np.array_equal(offs, poffs)
+        assert recs.tobytes() == precs.tobytes()
+
+    run()

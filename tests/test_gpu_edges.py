@@ -126,3 +126,36 @@ def test_edges_full_c2_roundtrip(eng):
     s_offs, s_recs = ol.edges(cfg, sub, codes[:sub.n_votes].cpu().numpy())
     assert np.array_equal(s_offs, o[:k + 1])
     assert s_recs.tobytes() == r[:int(o[k])].tobytes()
+
+
+@pytest.mark.parametrize("R", [1, 4, 200])
+def test_edges_arbitrary_code_bytes(eng, R):
+    """Every code byte (events, RoundSkip, messages, INVALID / REJECTED), rounds up
+    to R (some beyond) and types 0..2 straight into agnes_edges, both window paths
+    (R = 200: executors beyond the first LDS words)."""
+    rng = np.random.default_rng(R)
+    lengths = rng.integers(0, 300, 20000)
+    off = np.concatenate([[0], np.cumsum(lengths)]).astype(np.uint64)
+    n = int(off[-1])
+    inst = np.repeat(np.arange(len(lengths)), lengths)
+    rnd = rng.integers(0, R + 1, n)
+    hb = ol.batch_from_lists(inst, rnd, rng.integers(0, 3, n), np.zeros(n), np.zeros(n), off)
+    codes = rng.integers(0, 256, n).astype(np.uint8)
+    codes[rng.random(n) < 0.7] &= 0x0F  # mostly message-free, so levels repeat
+    cfg = abi.config(abi.MODE_REFERENCE, 0, R)
+    db = DeviceBatch.from_host(hb, eng.device)
+    for shift in (0, 4):
+        dc = torch.zeros(n + 16, dtype=torch.uint8, device=eng.device)
+        dc[shift:shift + n] = torch.from_numpy(codes).to(eng.device)
+        d = db
+        if shift:
+            def shifted(t):
+                buf = torch.zeros(n + 16, dtype=torch.uint8, device=eng.device)
+                buf[shift:shift + n] = t[:n]
+                return buf[shift:shift + n]
+            d = DeviceBatch(db.instance, shifted(db.round), shifted(db.type), db.value, db.validator,
+                            db.offsets, n_votes=n)
+        offs, recs = eng.edges(cfg, d, dc[shift:shift + n])
+        torch.cuda.synchronize()
+        _check(cfg, hb, codes, offs.cpu().numpy().view(np.uint64),
+               recs.cpu().numpy().reshape(-1).view(abi.EDGE_DTYPE))
