@@ -8,7 +8,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 NIL = 0xFFFFFFFF
 
 OK, E_INVALID, E_UNSUPPORTED, E_DEVICE, E_NOMEM, E_NODEVICE = 0, -1, -2, -3, -4, -5
@@ -33,6 +33,17 @@ CODE_EVENT_MASK, CODE_SKIP, CODE_MSG_SHIFT = 0x07, 0x08, 4
 MODE_REFERENCE, MODE_DEDUP = 0, 1
 FLAG_ROUND_SKIP, FLAG_STATE_MACHINE, FLAG_DISTINCT_VALUES = 0x1, 0x2, 0x4
 FLAG_ONE_INSTANCE = 0x8  # agnes_tally_carried: segments are slices of one instance (id cfg.reserved)
+# route override (agnes.h AGNES_ROUTE_*): diagnostics / route-equivalence tests
+ROUTE_SHIFT, ROUTE_AUTO, ROUTE_INSTANCE, ROUTE_SPLIT, ROUTE_WIDE = 8, 0, 1, 2, 3
+EPOCH_BITS_SHIFT = 16
+
+
+def FLAG_ROUTE(r: int) -> int:
+    return (r & 3) << ROUTE_SHIFT
+
+
+def FLAG_EPOCH_BITS(b: int) -> int:
+    return (b & 0x1F) << EPOCH_BITS_SHIFT
 
 ORDER_SHUFFLED, ORDER_PHASED, ORDER_SORTED = 0, 1, 2
 POWER_UNIFORM, POWER_ZIPF, POWER_EQUAL = 0, 1, 2

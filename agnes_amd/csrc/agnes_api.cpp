@@ -31,9 +31,8 @@ struct agnes_ctx {
     unsigned long long* d_err = nullptr;
     hipStream_t last_stream = nullptr;
     bool all_fast = false;     /* every set inside the u32 fast domain */
-    uint32_t* d_list = nullptr; /* [list_cap] deferred instances, [list_cap] first-event hints
-                                   (split route), then the list counter and
-                                   AGNES_QUEUE_WORDS - 1 work-queue counters */
+    uint32_t* d_list = nullptr; /* [list_cap] deferred instances, [list_cap] walk list, then
+                                   AGNES_QUEUE_WORDS counters (agnes_internal.h) */
     uint32_t list_cap = 0;
     uint64_t* d_scan = nullptr; /* edge-offset scan: block totals */
     uint64_t scan_cap = 0;
@@ -88,8 +87,9 @@ agnes_set_info set_info(const int64_t* pw, uint32_t n_vals, int64_t total) {
 
 bool cfg_ok(const agnes_config* cfg) {
     return cfg && cfg->max_rounds >= 1 && cfg->max_rounds <= 256 && cfg->mode <= AGNES_MODE_DEDUP &&
-           (cfg->flags & ~(AGNES_FLAG_ROUND_SKIP | AGNES_FLAG_STATE_MACHINE |
-                           AGNES_FLAG_DISTINCT_VALUES | AGNES_FLAG_ONE_INSTANCE)) == 0;
+           (cfg->flags & ~(AGNES_FLAG_ROUND_SKIP | AGNES_FLAG_STATE_MACHINE | AGNES_FLAG_DISTINCT_VALUES |
+                           AGNES_FLAG_ONE_INSTANCE | (AGNES_ROUTE_MASK << AGNES_ROUTE_SHIFT) |
+                           AGNES_FLAG_EPOCH_BITS(0x1F))) == 0;
 }
 
 /* ---- scalar mirror: one process-wide context ---- */
@@ -257,8 +257,8 @@ int64_t agnes_lds_bytes_per_wave(const agnes_config* cfg, uint32_t n_vals) {
 }
 
 static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b,
-                      uint8_t* codes, agnes_state* states, agnes_carry_rec* carry,
-                      const agnes_set_info* sets, uint32_t n_sets, bool sets_fast,
+                      uint8_t* codes, const agnes_state* states_in, agnes_state* states,
+                      agnes_carry_rec* carry, const agnes_set_info* sets, uint32_t n_sets, bool sets_fast,
                       hipStream_t st) {
     if (!c || !cfg_ok(cfg) || !b || !b->offsets) return AGNES_E_INVALID;
     if (b->n_votes && (!codes || !b->instance || !b->round || !b->type || !b->value ||
@@ -275,7 +275,7 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     AGNES_TRY(hipSetDevice(c->device));
     const bool wide_all = b->weight != nullptr || carry != nullptr || !sets_fast;
     if (!wide_all && (!c->d_list || c->list_cap < b->n_instances)) {
-        /* [list_cap] deferred instances | [list_cap] first-event hints | counters */
+        /* [list_cap] deferred instances | [list_cap] walk list | counters */
         AGNES_TRY(hipStreamSynchronize(st));
         if (c->d_list) (void)hipFree(c->d_list);
         c->d_list = nullptr;
@@ -298,27 +298,37 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     a.one_id = cfg->reserved;
     a.codes = codes;
     a.states = (cfg->flags & AGNES_FLAG_STATE_MACHINE) ? states : nullptr;
+    a.states_in = nullptr;
+    if (a.states && states_in && states_in != states) {
+        /* the sweep route reads the input States itself; the other routes work in place */
+        const uint32_t route = (cfg->flags >> AGNES_ROUTE_SHIFT) & AGNES_ROUTE_MASK;
+        const bool sweep = !wide_all && route == AGNES_ROUTE_AUTO && cfg->mode == AGNES_MODE_REFERENCE &&
+                           !(cfg->flags & AGNES_FLAG_ROUND_SKIP) && cfg->max_rounds <= 15u;
+        if (sweep) {
+            a.states_in = states_in;
+        } else if (b->n_instances) {
+            AGNES_TRY(hipMemcpyAsync(states, states_in, (size_t)b->n_instances * sizeof(agnes_state),
+                                     hipMemcpyDeviceToDevice, st));
+        }
+    }
     a.carry = carry;
     a.n_invalid = c->d_err;
     a.list = c->d_list;
+    a.walk = c->d_list ? c->d_list + (size_t)c->list_cap : nullptr;
     a.list_count = c->d_list ? c->d_list + 2 * (size_t)c->list_cap : nullptr;
-    a.hint = c->d_list ? c->d_list + c->list_cap : nullptr; /* used by the split route only */
     /* DEDUP / RoundSkip tables tag entries with (instance epoch, local vote index):
      * the local index of any vote is < n_votes, so it needs bit_length(n_votes - 1) bits */
     if (cfg->mode == AGNES_MODE_DEDUP || (cfg->flags & AGNES_FLAG_ROUND_SKIP)) {
         if (b->n_votes > (1ull << 31)) return AGNES_E_UNSUPPORTED;
         uint32_t lb = 1;
         while (lb < 31 && (1ull << lb) < b->n_votes) ++lb;
-        /* test hook: spend fewer bits on epochs to exercise table recycling */
-        if (const char* d = std::getenv("AGNES_DEBUG_EPOCH_SHIFT")) {
-            const int v = std::atoi(d);
-            if (v > (int)lb && v <= 31) lb = (uint32_t)v;
-        }
+        /* AGNES_FLAG_EPOCH_BITS: spend more bits on the index (fewer epochs per fill) */
+        const uint32_t want = (cfg->flags >> AGNES_EPOCH_BITS_SHIFT) & 0x1Fu;
+        if (want > lb && want <= 31u) lb = want;
         a.epoch_shift = lb;
     } else {
         a.epoch_shift = 31;
     }
-    if (const char* d = std::getenv("AGNES_DEBUG_SKIP")) a.dbg = (uint32_t)std::atoi(d);
     c->last_stream = st;
     return status_of(agnes_launch_tally(&a, cfg->mode, c->num_cus, wide_all, st));
 }
@@ -326,7 +336,14 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
 int agnes_tally(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint8_t* codes,
                 agnes_state* states, void* stream) {
     if (!c || !cfg || (cfg->flags & AGNES_FLAG_ONE_INSTANCE)) return AGNES_E_INVALID; /* needs counts */
-    return tally_impl(c, cfg, b, codes, states, nullptr, c->d_sets, c->n_sets, c->all_fast,
+    return tally_impl(c, cfg, b, codes, nullptr, states, nullptr, c->d_sets, c->n_sets, c->all_fast,
+                      (hipStream_t)stream);
+}
+
+int agnes_tally_states(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint8_t* codes,
+                       const agnes_state* states_in, agnes_state* states_out, void* stream) {
+    if (!c || !cfg || (cfg->flags & AGNES_FLAG_ONE_INSTANCE)) return AGNES_E_INVALID;
+    return tally_impl(c, cfg, b, codes, states_in, states_out, nullptr, c->d_sets, c->n_sets, c->all_fast,
                       (hipStream_t)stream);
 }
 
@@ -338,7 +355,7 @@ int agnes_tally_carried(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_
     if (!c || !cfg || !b || (b->n_instances && !counts)) return AGNES_E_INVALID;
     if (cfg->mode != AGNES_MODE_REFERENCE || (cfg->flags & (AGNES_FLAG_ROUND_SKIP | AGNES_FLAG_STATE_MACHINE)))
         return AGNES_E_UNSUPPORTED;
-    return tally_impl(c, cfg, b, codes, nullptr, reinterpret_cast<agnes_carry_rec*>(counts), c->d_sets,
+    return tally_impl(c, cfg, b, codes, nullptr, nullptr, reinterpret_cast<agnes_carry_rec*>(counts), c->d_sets,
                       c->n_sets, c->all_fast, (hipStream_t)stream);
 }
 
@@ -518,7 +535,7 @@ int sx_add(ScalarExec* x, uint32_t slot, uint32_t as_type, uint32_t value, int64
     const uint32_t saved_nv = c->n_vals;
     c->n_vals = 0; /* no power table: the validator index is unused */
     agnes_carry_rec* carry = (agnes_carry_rec*)(x->dev + SX_CARRY) + slot;
-    rc = tally_impl(c, &cfg, &b, x->dev + SX_CODE, nullptr, carry,
+    rc = tally_impl(c, &cfg, &b, x->dev + SX_CODE, nullptr, nullptr, carry,
                     (const agnes_set_info*)(x->dev + SX_SET), 1u, false, nullptr);
     c->n_vals = saved_nv;
     if (rc != AGNES_OK) return rc;

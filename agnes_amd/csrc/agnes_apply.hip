@@ -86,7 +86,6 @@ __device__ __forceinline__ uint32_t t1lo_of(uint32_t step) {
  * value counted into its (round, type) bucket before it, 0 if none (VoteCount::new
  * label; one value slot, last writer wins: round_votes.rs:36-54) */
 __device__ uint32_t label_of(const agnes_tally_args& a, uint64_t lo, uint64_t j) {
-    if (a.dbg & 16u) return 0u; /* development knob 16: no label reads */
     const uint32_t v = a.vb.value[j];
     if (v != AGNES_NIL) return v;
     const uint32_t r = a.vb.round[j], t = a.vb.type[j];
@@ -147,17 +146,13 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
     if (i >= n) return;
     /* every per-instance input at once (one latency, not a chain) */
     uint4* const sp = reinterpret_cast<uint4*>(a.states + i);
-    const uint32_t hint = a.hint ? a.hint[i] : 0u;
     uint64_t lo = a.vb.offsets[i], hi = a.vb.offsets[i + 1u];
     const uint4 s0 = sp[0], s1 = sp[1], s2 = sp[2], s3 = sp[3];
-    /* the stream tally's first-event hint: no event (or deferred to the LIST kernel):
-     * nothing to apply; else the walk starts there — earlier votes have no event */
-    if (hint == AGNES_NOHINT) return;
     const uint64_t NV = a.vb.n_votes;
     lo = lo < NV ? lo : NV;
     hi = hi < NV ? hi : NV;
     if (hi <= lo) return;
-    if (!a.hint) { /* the same u32-domain test as the tally kernels: the rest is the LIST kernel's */
+    { /* the same u32-domain test as the tally kernels: the rest is the LIST kernel's */
         const uint32_t set = a.vb.instance_set ? a.vb.instance_set[i] : (ns ? i % ns : 0u);
         if (set < ns) {
             const agnes_set_info si = a.sets[set];
@@ -256,7 +251,7 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
             dec_round = ((fc < 8u ? (fc < 4u ? r4[0] : r4[1]) : (fc < 12u ? r4[2] : r4[3])) >> sh) & 0xFFu;
             step = AGNES_STEP_COMMIT;
         }
-        if (((ow[0] ^ c4[0]) | (ow[1] ^ c4[1]) | (ow[2] ^ c4[2]) | (ow[3] ^ c4[3])) && !(a.dbg & 64u)) {
+        if (((ow[0] ^ c4[0]) | (ow[1] ^ c4[1]) | (ow[2] ^ c4[2]) | (ow[3] ^ c4[3])) ) {
             if (rel >= 0 && rem >= 16u) {
                 *reinterpret_cast<uint4*>(a.codes + w) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
             } else {
@@ -377,8 +372,7 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
     const uint32_t lane = threadIdx.x & 63u;
     unsigned char* const wbase = agnes_smem + rfl(threadIdx.x >> 6) * LDS_PER_WAVE; /* wave-uniform: m0 */
     const uint64_t wmax = (NV & ~15ull) - 16u; /* the last window fully inside [0, NV) */
-    /* single-buffered: with the hint a walk is one or two blocks, and 8 KB per wave
-     * keeps 20 waves per CU resident to cover the latency instead */
+    /* single-buffered: 8 KB per wave keeps 20 waves per CU resident to cover the latency */
     auto issue = [&](uint64_t blk) {
 #pragma unroll
         for (uint32_t k = 0; k < 4u; ++k) {
@@ -388,7 +382,7 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
             fast::glds16(a.vb.round + ws, wbase + (4u + k) * 1024u);
         }
     };
-    uint64_t blk = (lo + hint) & ~(uint64_t)(BLK - 1u);
+    uint64_t blk = lo & ~(uint64_t)(BLK - 1u);
     issue(blk);
     for (;;) {
         fast::dma_wait();
@@ -402,8 +396,7 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
                 tail_fill(a.codes, w, NV, cs);
                 tail_fill(a.vb.round, w, NV, rs);
             }
-            if (w + 16u > lo && !(a.dbg & 32u)) /* development knob 32: DMA only */
-            {
+            if (w + 16u > lo) {
                 if (SKIP) walk(w, *reinterpret_cast<const uint4*>(cs), *reinterpret_cast<const uint4*>(rs));
                 else walk_ns(w, *reinterpret_cast<const uint4*>(cs), *reinterpret_cast<const uint4*>(rs));
             }

@@ -17,7 +17,7 @@ constexpr uint32_t VPL = 4;
 constexpr uint32_t CHUNK = 64u * VPL;
 constexpr uint32_t SL = 16u; /* State dword k lives in lane SL + k of a State VGPR */
 constexpr uint32_t BQ = 4u;  /* instances per work-queue batch (agnes_fast.hip)   */
-constexpr uint32_t QN = AGNES_QUEUE_WORDS - 1u; /* work-queue counters (at most)  */
+constexpr uint32_t QN = AGNES_QUEUE_N;          /* work-queue counters (at most)  */
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 #ifndef AGNES_FAST_NT
 #define AGNES_FAST_NT 0 /* cache policy of the streamed vote/code traffic (2 = nt: slower here, the
@@ -46,6 +46,21 @@ __device__ __forceinline__ void glds16(const void* g, unsigned char* l) {
 __device__ __forceinline__ void glds4(const void* g, unsigned char* l) {
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(lds_addr(l))
+                 : "memory");
+}
+/* non-temporal forms (the streamed vote columns are read once: keep them out of L2) */
+__device__ __forceinline__ void glds16nt(const void* g, unsigned char* l) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(lds_addr(l))
+                 : "memory");
+}
+__device__ __forceinline__ void glds4nt(const void* g, unsigned char* l) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off nt\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "v"(g), "s"(lds_addr(l))
                  : "memory");

@@ -29,7 +29,6 @@
  * nil vote (a PrecommitValue, or a PolkaValue after a round skip) looks its
  * payload up backwards in the instance's stream.
  */
-#include <cstdlib>
 
 #include "agnes_fast.h"
 
@@ -333,12 +332,6 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
             /* first-vote tables: atomic max of (epoch << lb | LMASK - local index), so
              * the earliest vote of the instance wins (DEDUP: per (round, type,
              * validator); RoundSkip: per (round, validator)) */
-            if (a.dbg & 1u) { /* development knob (AGNES_DEBUG_SKIP=1): memory traffic only */
-                dc_code = (x.value[0] ^ x.key[1] ^ w[2] ^ w[3] ^ x.r4) & 0x07070707u;
-                dc_pos = x.pos;
-                dc_at = c;
-                continue;
-            }
             uint32_t acc = x.ok, sfirst = 0;
             if (TABLES) {
                 const uint32_t loc0 = (uint32_t)(c - I.beg) + p0;
@@ -729,16 +722,8 @@ static hipError_t launch_fast_k(const agnes_tally_args* a, int num_cus, hipStrea
         const int order[3] = {3, 2, 1};
         for (int v : order)
             if (k[v] > 0 && k[v] >= base) { best = v; break; }
-        if (const char* d = std::getenv("AGNES_FAST_VARIANT")) { /* development knob */
-            const int v = std::atoi(d);
-            if (v >= 0 && v < 4 && k[v] > 0) best = v;
-        }
         o->v = best;
         o->per_cu = k[best] > 0 ? k[best] : 1;
-        if (const char* d = std::getenv("AGNES_BLOCKS_PER_CU")) { /* development knob */
-            const int v = std::atoi(d);
-            if (v > 0 && v < o->per_cu) o->per_cu = v;
-        }
     }
     agnes_tally_args b = *a;
     b.set_cache = 0;

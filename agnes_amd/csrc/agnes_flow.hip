@@ -1,0 +1,861 @@
+/*
+ * agnes_flow.hip — the hot path for REFERENCE batches without RoundSkip (BASELINE
+ * C2/C3): ingest -> weight gather -> ordered tally -> quorum -> event ->
+ * State::apply, ONE pass over the votes (consensus_executor.rs:61-69).
+ *
+ * A work queue hands out batches of up to FB consecutive instances.  A batch whose
+ * offsets are multiples of 4 and whose instances are in the flow domain (u32 power
+ * set, maxpow < 4096, len * maxpow < 2^30) is walked as ONE vote stream in 512-vote
+ * chunks: lane l holds votes 8l .. 8l+7, as two 4-vote UNITS (A, B).  Instance
+ * starts are multiples of 4, so a unit never straddles an instance; a lane can
+ * (the instance of its unit B started inside the lane: a SPLIT lane).  Any other
+ * batch goes to the walk list (agnes_sweep.hip) with its States copied through.
+ *
+ * Per chunk (VALU per vote is what bounds the kernel, so the per-vote work is
+ * lane-serial with transient masks and every wave-level step is shared by 512
+ * votes):
+ *   K1   validation (bit tests per unit, SWAR on the round/type bytes), weight
+ *        gather from the power table (block LDS copy when it fits, else L2);
+ *   K2   per round present: one lane-serial prefix of the four buckets of the
+ *        round's RoundVotes (prevote / precommit x value / nil, round_votes.rs:
+ *        48-56), packed as 16-bit fields of one 64-bit accumulator (a vote adds
+ *        w << (32 * precommit + 16 * nil): one shift and one add); four DPP wave
+ *        scans of the lanes' last-segment totals; a segment's running sum is
+ *        scan - base + carry;
+ *   K3   per vote is_quorum on its own type's sums (round_votes.rs:31-33) with
+ *        precedence Value > Nil > Any > Init (:58-66) as a level 0..3, and
+ *        to_event (vote_executor.rs:26-36) as one byte lookup by (type, level);
+ *   K4   State::apply for the vote events (state_machine.rs:196-211).  Without
+ *        RoundSkip the step moves only at P1 (the first PolkaNil / PolkaValue at
+ *        State.round while in Prevote, :197-198) and at C (the first
+ *        PrecommitValue, any round, :211).  Every unit lowers its instance's P1 and
+ *        C positions by an LDS atomic min, reads them back, and derives every
+ *        message from the vote's position relative to them: TimeoutPrevote before
+ *        P1 in Prevote (:196), TimeoutPrecommit before C (:208), the precommit at
+ *        P1, the Decision at C.  valid (:198, :202) is the last PolkaValue at
+ *        State.round at or after P1 (or from the start, entering in Precommit)
+ *        before C: an LDS atomic max of (position, value) over the non-nil ones
+ *        (in this domain a nil PolkaValue's label is the last non-nil one's,
+ *        round_votes.rs:50-54, and P1 / C are crossed by non-nil votes).
+ */
+#include "agnes_fast.h"
+
+namespace agnes {
+namespace flow {
+using namespace agnes::fast;
+
+constexpr uint32_t LV = 8u, CH = 64u * LV; /* votes per lane, per chunk */
+/* DMA slot: each column of the chunk as a contiguous image */
+constexpr uint32_t F_INST = 0, F_VALUE = 2048, F_VAL = 4096, F_ROUND = 6144, F_TYPE = 6656, F_BYTES = 7168;
+constexpr uint32_t FB = 16u;    /* instances per batch (header offsets in lanes 0..FB) */
+constexpr uint32_t HI = 32u;    /* header lanes HI + k: per-instance data of instance k */
+constexpr uint32_t SMALLB = 4u; /* batch size of the work queue's tail                  */
+/* instance record, 12 words: quorum threshold, power-row base, validators of its set
+ * (0: no such set); the State machine's view: the roles its step keeps (one byte per
+ * vote, 0 without the State machine), State.round in every byte, 0xFF bytes when it
+ * enters in Precommit (valid from the start); the P1 and C positions (stream-relative,
+ * ~0: none); locked value, decision value, decision round | F_LOCK << 8, step.  The
+ * valid candidates, (position + 1) << 32 | value, are kept beside (vtab). */
+constexpr uint32_t R_Q2 = 0, R_PBASE = 1, R_NV = 2, R_SMASK = 3, R_EQ = 4, R_VALL = 5, R_P1 = 6, R_C = 7,
+                   R_LOCK = 8, R_DEC = 9, R_DF = 10, R_STEP = 11, RECW = 12;
+constexpr uint32_t F_LOCK = 0x100u;
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+/* K4 roles of a vote event (byte lookup by v_perm, index = event code 0..7) */
+constexpr uint32_t X_P1 = 0x01u, X_C = 0x02u, X_TP = 0x04u, X_TC = 0x08u, X_PV = 0x10u;
+constexpr uint32_t XT_LO = (0u) | (X_TP << 8) | (X_P1 << 16) | ((X_P1 | X_PV) << 24); /* None, PolkaAny, PolkaNil, PolkaValue */
+constexpr uint32_t XT_HI = (X_TC) | (X_C << 8);                                      /* PrecommitAny, PrecommitValue */
+/* roles kept per step (byte lookup by step 0..7): NewRound / Propose: TimeoutPrecommit
+ * and commit only (:208, :211); Prevote: all; Precommit: no P1 / TimeoutPrevote; Commit: none (:205) */
+constexpr uint32_t SM_LO = (X_C | X_TC) | ((X_C | X_TC) << 8) | (0x1Fu << 16) | ((X_C | X_TC | X_PV) << 24);
+constexpr uint32_t SM_HI = 0u;
+/* to_event by index type * 4 + level (Init, Any, Nil, Value): vote_executor.rs:26-36 */
+constexpr uint32_t EV_LO = AGNES_CODE_NONE | (AGNES_CODE_POLKA_ANY << 8) | (AGNES_CODE_POLKA_NIL << 16) |
+                           (AGNES_CODE_POLKA_VALUE << 24);
+constexpr uint32_t EV_HI = AGNES_CODE_NONE | (AGNES_CODE_PRECOMMIT_ANY << 8) | (AGNES_CODE_NONE << 16) |
+                           (AGNES_CODE_PRECOMMIT_VALUE << 24);
+
+__host__ __device__ inline uint32_t carry_bytes(uint32_t R) { return (uint32_t)align16(32ull * R); }
+/* per-wave LDS: DMA slot | carried executors (2 copies x (vw[2R], vn[2R]) u32) |
+ * instance records | (State machine) valid candidates, two batches' staged States */
+__host__ __device__ inline uint32_t lds_bytes(bool sm, uint32_t R) {
+    return F_BYTES + carry_bytes(R) + FB * RECW * 4u + (sm ? FB * 8u + 2u * FB * 64u : 0u);
+}
+
+__device__ __forceinline__ uint32_t zero_marks(uint32_t x) { /* 0x80 in the bytes of x that are zero */
+    const uint32_t t = (x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+    return ((t | x) & 0x80808080u) ^ 0x80808080u;
+}
+__device__ __forceinline__ uint32_t mark_bytes(uint32_t m) { /* 0x80 marks -> 0xFF bytes (no multiply) */
+    return (m << 1) - (m >> 7);
+}
+__device__ __forceinline__ uint32_t rep4(uint32_t b) { /* byte 0 of b in every byte */
+    return __builtin_amdgcn_perm(0u, b, 0u);
+}
+__device__ __forceinline__ uint32_t below_bytes(int32_t i) { /* 0xFF in the bytes below byte i, i clamped to 0..4 */
+    return i <= 0 ? 0u : (i >= 4 ? 0xFFFFFFFFu : (1u << (8u * (uint32_t)i)) - 1u);
+}
+__device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ uint32_t wave_or(uint32_t x) { /* every lane active */
+    x |= dpp<0x111, 0xf>(x);
+    x |= dpp<0x112, 0xf>(x);
+    x |= dpp<0x114, 0xf>(x);
+    x |= dpp<0x118, 0xf>(x);
+    x |= dpp<0x142, 0xa>(x);
+    x |= dpp<0x143, 0xc>(x);
+    return rdl(x, 63u);
+}
+/* saddr forms: address = uniform 64-bit base + 32-bit lane offset; the vote
+ * columns are read once (non-temporal) */
+__device__ __forceinline__ void sdma16(const void* base, uint32_t voff, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(base), "s"(lds)
+                 : "memory");
+}
+__device__ __forceinline__ void sdma4(const void* base, uint32_t voff, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2 nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(base), "s"(lds)
+                 : "memory");
+}
+__device__ __forceinline__ void sstore4(void* base, uint32_t voff, uint32_t d) {
+    asm volatile("global_store_dword %0, %1, %2" ::"v"(voff), "v"(d), "s"(base) : "memory");
+}
+__device__ __forceinline__ void sstore8(void* base, uint32_t voff, uint32_t d0, uint32_t d1) {
+    asm volatile("global_store_dwordx2 %0, %1, %2" ::"v"(voff), "v"(u64of(d0, d1)), "s"(base) : "memory");
+}
+
+/* a batch: instances [s0, e0).  Its header is built in three stages, each one
+ * chunk apart so that its loads land behind the chunk DMA's wait: (1) offsets
+ * (lanes 0..m, clamped to n_votes) and sets (lanes HI + k) requested; (2) lengths
+ * and the checks on the offsets, the sets' constants requested; (3) the quorum
+ * thresholds and whether the batch is one flow stream. */
+struct Hdr {
+    uint32_t s0, e0;
+    uint32_t olo, ohi;  /* lanes 0..m: offset; lane HI + k: set (in olo)        */
+    uint32_t q2, mp;    /* lane HI + k: set q2, maxpow; after stage 3 q2 = threshold */
+    uint32_t fa, ln;    /* lane HI + k: set fast flag (2: no such set), length   */
+    uint32_t stage;     /* 1, 2, 3 (ready)                                       */
+    uint32_t stream;    /* stage 2: the offsets pass; stage 3: walked by this kernel */
+};
+
+template <bool PC, bool SM, bool R1>
+__global__ __launch_bounds__(256) void flow(agnes_tally_args a, uint32_t lds_per_wave) {
+    const uint32_t lane = lane_id();
+    const uint32_t wave = rfl(threadIdx.x >> 6);
+    const uint32_t R = R1 ? 1u : a.max_rounds, nv = a.n_vals, ns = a.n_sets, n = a.vb.n_instances;
+    const uint64_t NV = a.vb.n_votes;
+    const uint32_t o32 = 32u * lane, o16 = 16u * lane, o8 = 8u * lane, o4 = 4u * lane;
+
+    /* block-shared u32 power table (launcher-staged only when it costs no occupancy) */
+    if (PC) {
+        uint32_t* pc = reinterpret_cast<uint32_t*>(agnes_smem);
+        const uint32_t np = ns * nv;
+        for (uint32_t k = threadIdx.x; k < np; k += blockDim.x) pc[k] = a.power32[k];
+        __syncthreads();
+    }
+    unsigned char* const base = agnes_smem + a.power_cache + wave * lds_per_wave;
+    unsigned char* const slot = base;
+    const uint32_t slotl = lds_addr(slot);
+    uint32_t* const crow = reinterpret_cast<uint32_t*>(base + F_BYTES);
+    const uint32_t cw = 4u * R; /* one carry copy: vw[2R] then vn[2R] */
+    uint32_t* const itab = reinterpret_cast<uint32_t*>(base + F_BYTES + carry_bytes(R));
+    unsigned long long* const vtab = reinterpret_cast<unsigned long long*>(base + F_BYTES + carry_bytes(R) + FB * RECW * 4u);
+    unsigned char* const sb = base + F_BYTES + carry_bytes(R) + FB * RECW * 4u + FB * 8u;
+    const agnes_state* const st_in = a.states_in ? a.states_in : a.states;
+    uint32_t cpar = 0;
+    uint64_t pf_at = ~0ull;
+    uint32_t bad = 0;
+    /* r < R <=> ((r & 0x7F) + 128 - R) < 128 and r < 128 (R <= 15) */
+    const uint32_t RK = (128u - R) * 0x01010101u;
+
+    /* ---- work queue: batches of FB, then SMALLB ones for the tail ---- */
+    const uint32_t qn = gridDim.x < QN ? gridDim.x : QN;
+    const uint32_t qk = blockIdx.x % qn;
+    uint32_t* const ctr = a.list_count + 1u + qk;
+    const uint64_t NB = (uint64_t)(n / FB) * 7u / 8u;
+    auto range_of = [&](uint32_t t, uint32_t& s0, uint32_t& e0) {
+        const uint64_t b = (uint64_t)t * qn + qk;
+        const uint64_t s = b < NB ? b * FB : NB * FB + (b - NB) * SMALLB;
+        const uint64_t e = s + (b < NB ? FB : SMALLB);
+        s0 = s < n ? (uint32_t)s : n;
+        e0 = e < n ? (uint32_t)e : n;
+    };
+    auto hdr1 = [&](Hdr& h) { /* stage 1: offsets and sets requested */
+        const uint32_t m = h.e0 - h.s0;
+        uint32_t lo = 0, hi = 0;
+        if (m > 0u && lane <= m) {
+            const uint64_t o = a.vb.offsets[h.s0 + lane];
+            const uint64_t oc = o < NV ? o : NV;
+            lo = (uint32_t)oc;
+            hi = (uint32_t)(oc >> 32);
+        } else if (lane >= HI && lane < HI + m) {
+            const uint32_t k = h.s0 + lane - HI;
+            lo = a.vb.instance_set ? a.vb.instance_set[k] : (ns ? k % ns : 0u);
+        }
+        h.olo = lo;
+        h.ohi = hi;
+        h.stage = 1;
+        h.stream = 0;
+    };
+    auto hdr2 = [&](Hdr& h) { /* stage 2: lengths, offset checks; set constants requested */
+        const uint32_t m = h.e0 - h.s0;
+        const bool il = lane >= HI && lane < HI + m;
+        const uint32_t k = il ? lane - HI : 0u;
+        const uint64_t ob = u64of(shfl(h.olo, k), shfl(h.ohi, k));
+        const uint64_t oe = u64of(shfl(h.olo, k + 1u), shfl(h.ohi, k + 1u));
+        const uint64_t len = oe > ob ? oe - ob : 0ull;
+        h.ln = len < (1ull << 31) ? (uint32_t)len : (1u << 31);
+        uint32_t q2 = 0, mp = 0, fa = 2;
+        if (il && h.olo < ns) {
+            const agnes_set_info* const si = a.sets + h.olo;
+            q2 = si->q2;
+            mp = si->maxpow;
+            fa = si->fast;
+        }
+        h.q2 = q2;
+        h.mp = mp;
+        h.fa = fa;
+        const uint64_t Ol = u64of(h.olo, h.ohi);
+        const uint64_t On = u64of(shfl(h.olo, lane + 1u), shfl(h.ohi, lane + 1u));
+        const bool badl = (lane <= m && (h.olo & 3u) != 0u) || (lane < m && On < Ol);
+        const uint64_t O0 = u64of(rdl(h.olo, 0u), rdl(h.ohi, 0u)), Om = u64of(rdl(h.olo, m), rdl(h.ohi, m));
+        h.stream = m > 0u && !ballot(badl) && Om - O0 < (1ull << 30);
+        h.stage = 2;
+    };
+    auto hdr3 = [&](Hdr& h) { /* stage 3: quorum thresholds; a flow stream or the walk list */
+        const uint32_t m = h.e0 - h.s0;
+        const bool il = lane >= HI && lane < HI + m;
+        bool fl = true;
+        uint32_t q2 = 0;
+        if (il) {
+            const uint64_t len = h.ln;
+            if (h.fa != 2u) {
+                const uint64_t wmax = len * (uint64_t)h.mp; /* no sum of the instance exceeds it */
+                /* u32 sums, per-lane bucket prefixes < 2^15 (8 votes x maxpow), signed thresholds */
+                fl = h.fa != 0u && len < (1ull << 30) && wmax < (1ull << 30) && h.mp < 4096u;
+                const uint64_t qq = (uint64_t)h.q2 < wmax ? (uint64_t)h.q2 : wmax;
+                q2 = (uint32_t)(qq < 0x7FFFFFFFull ? qq : 0x7FFFFFFFull);
+            } else {
+                fl = len < (1ull << 30); /* no such set: every vote INVALID */
+            }
+        }
+        h.q2 = q2;
+        h.stream = h.stream && !ballot(!fl);
+        h.stage = 3;
+    };
+    uint32_t spar = 0; /* States staging buffer of the current batch */
+    auto dma_states = [&](const Hdr& h, uint32_t par) { /* the batch's States into LDS (64 B each) */
+        const uint32_t m = h.e0 - h.s0;
+        if (!SM || m == 0u) return;
+        glds16(reinterpret_cast<const unsigned char*>(st_in + h.s0) + 16u * (lane < 4u * m ? lane : 0u),
+               sb + par * (FB * 64u));
+    };
+    auto dma_chunk = [&](uint64_t c) { /* the chunk's columns into the slot */
+        /* at the columns' end a lane past n_votes reads the chunk's first group instead
+         * (its votes lie past the stream: never active) */
+        uint32_t va = o16, vb = o16, ba = o4, bb = o4;
+        if (c + CH > NV) {
+            const uint64_t lim = NV - c;
+            const bool ia = 4u * lane + 4u <= lim, ib = 256u + 4u * lane + 4u <= lim;
+            va = ia ? o16 : 0u;
+            vb = ib ? o16 : 0u;
+            ba = ia ? o4 : 0u;
+            bb = ib ? o4 : 0u;
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): the slot's LDS reads are done */
+        sdma16(a.vb.instance + c, va, slotl + F_INST);
+        sdma16(a.vb.instance + c + 256u, vb, slotl + F_INST + 1024u);
+        sdma16(a.vb.value + c, va, slotl + F_VALUE);
+        sdma16(a.vb.value + c + 256u, vb, slotl + F_VALUE + 1024u);
+        sdma16(a.vb.validator + c, va, slotl + F_VAL);
+        sdma16(a.vb.validator + c + 256u, vb, slotl + F_VAL + 1024u);
+        sdma4(a.vb.round + c, ba, slotl + F_ROUND);
+        sdma4(a.vb.round + c + 256u, bb, slotl + F_ROUND + 256u);
+        sdma4(a.vb.type + c, ba, slotl + F_TYPE);
+        sdma4(a.vb.type + c + 256u, bb, slotl + F_TYPE + 256u);
+    };
+
+    /* deferred code stores: issued behind the next chunk's gather and DMA (vmcnt
+     * retires in issue order) */
+    uint64_t dc_at = ~0ull;
+    uint32_t dc0 = 0, dc1 = 0, dc_act = 0; /* dc_act: 2 both units, 1 unit A only */
+    auto flush = [&]() {
+        if (dc_at != ~0ull) {
+            if (dc_act == 2u) sstore8(a.codes + dc_at, o8, dc0, dc1);
+            else if (dc_act == 1u) sstore4(a.codes + dc_at, o8, dc0);
+            dc_at = ~0ull;
+        }
+    };
+
+    Hdr H, N;
+    uint32_t tq = 0; /* lane 0: slot of the batch after N (atomic in flight) */
+    {
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(ctr, 2u);
+        t = rdl(t, 0u);
+        range_of(t, H.s0, H.e0);
+        range_of(t + 1u, N.s0, N.e0);
+        if (lane == 0) tq = atomicAdd(ctr, 1u);
+    }
+    if (H.s0 >= H.e0) return;
+    hdr1(H);
+    hdr2(H);
+    hdr3(H);
+    dma_states(H, spar);
+    hdr1(N);
+
+    for (;;) { /* batches: H current, N next */
+        const uint32_t m = H.e0 - H.s0;
+        unsigned char* const sbh = sb + spar * (FB * 64u);
+        bool smf = SM; /* the State views are not yet set up from the staged States */
+        if (!H.stream) { /* not one flow stream: the walk list (agnes_sweep.hip) */
+            uint32_t w0 = 0;
+            if (lane == 0) w0 = atomicAdd(a.list_count + AGNES_WALK_COUNT, m);
+            w0 = rdl(w0, 0u);
+            if (lane < m) a.walk[w0 + lane] = H.s0 + lane;
+        } else {
+            { /* instance records */
+                const uint32_t q2k = shfl(H.q2, HI + lane);
+                const uint32_t setk = shfl(H.olo, HI + lane);
+                if (lane < m) {
+                    uint32_t* const rk = itab + RECW * lane;
+                    rk[R_Q2] = q2k;
+                    rk[R_PBASE] = setk < ns ? setk * nv : 0u;
+                    rk[R_NV] = setk < ns ? nv : 0u;
+                    rk[R_SMASK] = 0u; /* no State machine: no role */
+                    rk[R_P1] = NONE;
+                    rk[R_C] = NONE;
+                    rk[R_DF] = 0u;
+                    if (SM) vtab[lane] = 0ull;
+                }
+            }
+            /* the stream: instance starts relative to its first vote */
+            const uint64_t S0 = u64of(rdl(H.olo, 0u), rdl(H.ohi, 0u));
+            const uint32_t s0lo = (uint32_t)S0;
+            const uint32_t Lend = rdl(H.olo, m) - s0lo;
+            const uint32_t rl = H.olo - s0lo;
+            const uint32_t rn = shfl(rl, lane + 1u);
+            const uint64_t NE = ballot(lane < m && rn > rl);
+            const uint32_t relv = lane <= m ? rl : 0x7FFFFFFFu;
+            const uint64_t mm64 = (1ull << m) - 1ull;
+
+            for (uint32_t rc = 0; rc < Lend; rc += CH) {
+                const uint64_t c = S0 + rc;
+                if (pf_at != c) dma_chunk(c); /* not prefetched: a wave's first chunk */
+                dma_wait(); /* this chunk's DMA (and a new batch's States) have landed */
+                if (SM && smf) { /* the State machine's view of each instance (state_machine.rs:184) */
+                    if (lane < m) {
+                        const uint32_t* const sp = reinterpret_cast<const uint32_t*>(sbh + 64u * lane);
+                        const int64_t rnd = (int64_t)u64of(sp[2], sp[3]);
+                        const uint32_t step = sp[13] & 0xFFu;
+                        uint32_t smask = __builtin_amdgcn_perm(SM_HI, SM_LO, rep4(step < 7u ? step : 7u));
+                        if (rnd < 0 || rnd > 255) smask &= X_C * 0x01010101u; /* no vote round equals State.round */
+                        uint32_t* const rk = itab + RECW * lane;
+                        rk[R_SMASK] = smask;
+                        rk[R_EQ] = rep4((uint32_t)rnd);
+                        rk[R_VALL] = step == AGNES_STEP_PRECOMMIT ? 0xFFFFFFFFu : 0u;
+                        rk[R_STEP] = step;
+                    }
+                    smf = false;
+                }
+                /* the next batch's header, one stage per chunk; its States behind it */
+                if (N.s0 < N.e0) {
+                    if (N.stage == 1u) {
+                        hdr2(N);
+                    } else if (N.stage == 2u) {
+                        hdr3(N);
+                        if (N.stream) dma_states(N, spar ^ 1u);
+                    }
+                }
+
+                /* ---- segments: the instances the chunk straddles, at unit granularity ---- */
+                const uint32_t tj = relv - rc; /* instance start relative to the chunk */
+                const uint32_t k0 = 63u - (uint32_t)__builtin_clzll(ballot((int32_t)tj <= 0) & mm64);
+                uint64_t bk = ballot(tj - 1u < CH - 1u) & NE; /* non-empty, starting inside */
+                const bool multi = bk != 0ull;
+                const bool cont0 = ((ballot((int32_t)tj < 0) >> k0) & 1ull) != 0ull;
+                const uint32_t left = Lend - rc;
+                const bool lastc = left > CH && !ballot(tj == CH);
+                const uint32_t hi_r = left < CH ? left : CH;
+                const bool actA = o8 < hi_r, actB = o8 + 4u < hi_r;
+                uint32_t kA = k0, kB = k0, sA = 0, klast = k0, slast = 0;
+                bool split = false;
+                if (multi) {
+                    uint64_t SA = 0, SBm = 0;
+                    uint32_t segw = k0, D = 0;
+                    while (bk) {
+                        const uint32_t k = (uint32_t)__builtin_ctzll(bk);
+                        bk &= bk - 1ull;
+                        ++D;
+                        const uint32_t u = rdl(tj, k) >> 2; /* its first unit */
+                        const uint32_t L = u >> 1;
+                        if (u & 1u) SBm |= 1ull << L;
+                        else SA |= 1ull << L;
+                        segw = lane == D ? (k | (L << 8)) : segw;
+                        klast = k;
+                        slast = L;
+                    }
+                    /* segments started at or before my unit A, and whether unit B starts one */
+                    const uint32_t dA = mbcnt64(SA) + (uint32_t)((SA >> lane) & 1ull) + mbcnt64(SBm);
+                    split = ((SBm >> lane) & 1ull) != 0ull;
+                    const uint32_t wA = shfl(segw, dA), wB = shfl(segw, dA + (split ? 1u : 0u));
+                    kA = wA & 0xFFu;
+                    sA = wA >> 8;
+                    kB = wB & 0xFFu;
+                }
+                const uint4 recA = *reinterpret_cast<const uint4*>(itab + RECW * kA); /* q2, pbase, nv, smw */
+                const uint4 recB = multi ? *reinterpret_cast<const uint4*>(itab + RECW * kB) : recA;
+
+                /* ---- K1: votes of the chunk + validation + weight gather ---- */
+                uint32_t value[LV], val[LV], r8[2], t8[2];
+                uint32_t nb0 = 0, nb1 = 0; /* 0x10 in the bytes of nil votes */
+                bool all_ok;
+                uint32_t okb0, okb1; /* byte masks of the votes that checked in (exact path) */
+                {
+                    uint32_t inst[LV];
+                    {
+                        const uint4 i0 = *reinterpret_cast<const uint4*>(slot + F_INST + o32);
+                        const uint4 i1 = *reinterpret_cast<const uint4*>(slot + F_INST + o32 + 16u);
+                        const uint4 v0 = *reinterpret_cast<const uint4*>(slot + F_VALUE + o32);
+                        const uint4 v1 = *reinterpret_cast<const uint4*>(slot + F_VALUE + o32 + 16u);
+                        const uint4 d0 = *reinterpret_cast<const uint4*>(slot + F_VAL + o32);
+                        const uint4 d1 = *reinterpret_cast<const uint4*>(slot + F_VAL + o32 + 16u);
+                        const uint2 rr = *reinterpret_cast<const uint2*>(slot + F_ROUND + o8);
+                        const uint2 tt = *reinterpret_cast<const uint2*>(slot + F_TYPE + o8);
+                        inst[0] = i0.x; inst[1] = i0.y; inst[2] = i0.z; inst[3] = i0.w;
+                        inst[4] = i1.x; inst[5] = i1.y; inst[6] = i1.z; inst[7] = i1.w;
+                        value[0] = v0.x; value[1] = v0.y; value[2] = v0.z; value[3] = v0.w;
+                        value[4] = v1.x; value[5] = v1.y; value[6] = v1.z; value[7] = v1.w;
+                        val[0] = d0.x; val[1] = d0.y; val[2] = d0.z; val[3] = d0.w;
+                        val[4] = d1.x; val[5] = d1.y; val[6] = d1.z; val[7] = d1.w;
+                        r8[0] = rr.x; r8[1] = rr.y;
+                        t8[0] = tt.x; t8[1] = tt.y;
+                    }
+#pragma unroll
+                    for (uint32_t s = 0; s < 4u; ++s) {
+                        nb0 |= value[s] == AGNES_NIL ? 0x10u << (8u * s) : 0u;
+                        nb1 |= value[4u + s] == AGNES_NIL ? 0x10u << (8u * s) : 0u;
+                    }
+                    /* the boundary's checks: round < R, type in {0, 1}, the vote names its
+                     * instance, validator in the set */
+                    const uint32_t idA = H.s0 + kA, idB = H.s0 + kB;
+                    const uint32_t bad0 = R == 1u ? (t8[0] & 0xFEFEFEFEu) | r8[0]
+                                                  : (t8[0] & 0xFEFEFEFEu) | ((r8[0] | ((r8[0] & 0x7F7F7F7Fu) + RK)) & 0x80808080u);
+                    const uint32_t bad1 = R == 1u ? (t8[1] & 0xFEFEFEFEu) | r8[1]
+                                                  : (t8[1] & 0xFEFEFEFEu) | ((r8[1] | ((r8[1] & 0x7F7F7F7Fu) + RK)) & 0x80808080u);
+                    const uint32_t mA = max(max(val[0], val[1]), max(val[2], val[3]));
+                    const uint32_t mB = max(max(val[4], val[5]), max(val[6], val[7]));
+                    const bool okA = bad0 == 0u && mA < recA.z && inst[0] == idA && inst[1] == idA && inst[2] == idA &&
+                                     inst[3] == idA;
+                    const bool okB = bad1 == 0u && mB < recB.z && inst[4] == idB && inst[5] == idB && inst[6] == idB &&
+                                     inst[7] == idB;
+                    all_ok = !ballot((actA && !okA) || (actB && !okB));
+                    okb0 = actA ? 0xFFFFFFFFu : 0u;
+                    okb1 = actB ? 0xFFFFFFFFu : 0u;
+                    if (!all_ok) { /* the exact per-vote checks */
+                        uint32_t o0 = 0, o1 = 0;
+#pragma unroll
+                        for (uint32_t s = 0; s < 4u; ++s) {
+                            const bool g0 = ((bad0 >> (8u * s)) & 0xFFu) == 0u && inst[s] == idA && val[s] < recA.z;
+                            const bool g1 = ((bad1 >> (8u * s)) & 0xFFu) == 0u && inst[4u + s] == idB && val[4u + s] < recB.z;
+                            o0 |= g0 ? 0xFFu << (8u * s) : 0u;
+                            o1 |= g1 ? 0xFFu << (8u * s) : 0u;
+                        }
+                        const uint32_t p0m = okb0, p1m = okb1;
+                        okb0 &= o0;
+                        okb1 &= o1;
+                        bad += (uint32_t)(__builtin_popcount(p0m & ~okb0) + __builtin_popcount(p1m & ~okb1)) >> 3;
+                    }
+                }
+                uint32_t w[LV];
+                {
+                    /* K1: w = power[set][validator] (consensus_executor.rs:62-63 ->
+                     * validators.rs:7); a vote that checked out weighs 0 */
+                    const uint32_t pbA = recA.y, pbB = recB.y;
+                    if (all_ok && hi_r == CH) {
+#pragma unroll
+                        for (uint32_t s = 0; s < LV; ++s) {
+                            const uint32_t idx = (s < 4u ? pbA : pbB) + val[s];
+                            w[s] = PC ? reinterpret_cast<const uint32_t*>(agnes_smem)[idx] : a.power32[idx];
+                        }
+                    } else {
+#pragma unroll
+                        for (uint32_t s = 0; s < LV; ++s) {
+                            const bool o = (((s < 4u ? okb0 : okb1) >> (8u * (s & 3u))) & 1u) != 0u;
+                            const uint32_t idx = o ? (s < 4u ? pbA : pbB) + val[s] : 0u;
+                            const uint32_t x = PC ? reinterpret_cast<const uint32_t*>(agnes_smem)[idx] : a.power32[idx];
+                            w[s] = o ? x : 0u;
+                        }
+                    }
+                }
+                /* a gather from HBM retires before the DMA below is issued: a wait on it
+                 * behind the DMA would wait for the DMA too (in-order vmcnt) */
+                if (!PC) asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]),
+                                      "v"(w[6]), "v"(w[7]));
+                { /* the next chunk by LDS-DMA (this stream's, or the next batch's first) */
+                    uint64_t nc = ~0ull;
+                    if (rc + CH < Lend) nc = c + CH;
+                    else if (N.s0 < N.e0 && N.stage == 3u && N.stream) nc = u64of(rdl(N.olo, 0u), rdl(N.ohi, 0u));
+                    if (nc != ~0ull) {
+                        dma_chunk(nc);
+                        pf_at = nc;
+                    } else {
+                        pf_at = ~0ull;
+                    }
+                }
+                flush(); /* the previous chunk's codes */
+
+                /* ---- K2 + K3: one pass per round present ---- */
+                uint32_t* const A = crow + cpar * cw;
+                uint32_t* const B = crow + (cpar ^ 1u) * cw;
+                if (lastc) { /* row B: the executors the last segment carries into the next chunk */
+                    const bool keep = !multi && cont0;
+                    for (uint32_t k = lane; k < cw; k += 64u) B[k] = keep ? A[k] : 0u;
+                    __builtin_amdgcn_wave_barrier();
+                }
+                const bool cA = cont0 && kA == k0;   /* unit A continues the previous chunk's instance */
+                const bool cL = cont0 && klast == k0; /* so does the last segment */
+                /* per-vote bucket shifts as bytes, no per-vote masks: type * 32 (the
+                 * precommit half of the accumulator) | nil * 16 */
+                const uint32_t ts0c = (t8[0] & 0x01010101u) << 5, ts1c = (t8[1] & 0x01010101u) << 5;
+                const uint32_t sh0c = ts0c | nb0, sh1c = ts1c | nb1;
+                uint32_t rset = 1u;
+                if (R > 1u) { /* the rounds present among the votes that checked in */
+                    uint32_t rb = 0;
+#pragma unroll
+                    for (uint32_t s = 0; s < LV; ++s) {
+                        const uint32_t ok = ((s < 4u ? okb0 : okb1) >> (8u * (s & 3u))) & 1u;
+                        rb |= ok << ((r8[s >> 2] >> (8u * (s & 3u))) & 15u);
+                    }
+                    rset = wave_or(rb);
+                }
+                uint32_t lv0 = 0, lv1 = 0; /* levels 0..3, byte s & 3 of unit s >> 2 */
+                while (rset) {
+                    const uint32_t r = (uint32_t)__builtin_ctz(rset);
+                    rset &= rset - 1u;
+                    uint32_t sh0 = sh0c, sh1 = sh1c, ts0 = ts0c, ts1 = ts1c;
+                    if (!R1) asm volatile("" : "+v"(sh0), "+v"(sh1), "+v"(ts0), "+v"(ts1)); /* extracts stay per pass */
+                    /* 0xFF in the bytes of this round's votes */
+                    const uint32_t rm0 = R > 1u ? mark_bytes(zero_marks(r8[0] ^ (r * 0x01010101u))) : 0xFFFFFFFFu;
+                    const uint32_t rm1 = R > 1u ? mark_bytes(zero_marks(r8[1] ^ (r * 0x01010101u))) : 0xFFFFFFFFu;
+                    /* lane-serial prefix of the round's four buckets, 16-bit fields:
+                     * prevote value | prevote nil << 16 | precommit value << 32 | precommit nil << 48;
+                     * Dw: the vote's own type's half after it */
+                    uint64_t P = 0, P3 = 0;
+                    uint32_t Dw[LV];
+#pragma unroll
+                    for (uint32_t s = 0; s < LV; ++s) {
+                        const uint32_t bs = 8u * (s & 3u);
+                        uint32_t ws = w[s];
+                        if (R > 1u) ws &= (uint32_t)__builtin_amdgcn_sbfe((int32_t)(s < 4u ? rm0 : rm1), bs, 8u);
+                        P += (uint64_t)ws << __builtin_amdgcn_ubfe(s < 4u ? sh0 : sh1, bs, 8u);
+                        if (s == 3u) P3 = P;
+                        Dw[s] = (uint32_t)(P >> __builtin_amdgcn_ubfe(s < 4u ? ts0 : ts1, bs, 8u));
+                    }
+                    /* the lane's last segment (unit B alone when it starts an instance) */
+                    const uint64_t T = split ? P - P3 : P;
+                    const uint32_t Tvp = (uint32_t)T & 0xFFFFu, Tnp = (uint32_t)T >> 16;
+                    const uint32_t Tvc = (uint32_t)(T >> 32) & 0xFFFFu, Tnc = (uint32_t)(T >> 48);
+                    const uint32_t Ivp = scan(Tvp), Inp = scan(Tnp), Ivc = scan(Tvc), Inc = scan(Tnc);
+                    const uint32_t Evp = Ivp - Tvp, Enp = Inp - Tnp, Evc = Ivc - Tvc, Enc = Inc - Tnc;
+                    /* carried executors of the instance continuing from the previous chunk
+                     * (keys 2r prevote, 2r + 1 precommit; uniform LDS reads) */
+                    const uint32_t K = 2u * r;
+                    uint32_t cvp = 0, cnp = 0, cvc = 0, cnc = 0;
+                    if (cont0) {
+                        cvp = A[K];
+                        cvc = A[K + 1u];
+                        cnp = A[2u * R + K];
+                        cnc = A[2u * R + K + 1u];
+                    }
+                    /* unit A's running sums before the lane: scan - (scan at its instance's
+                     * first lane) + carry */
+                    uint32_t bvp = Evp, bnp = Enp, bvc = Evc, bnc = Enc;
+                    if (multi) { /* every lane runs the shuffles */
+                        const uint32_t xvp = shfl(Evp, sA), xnp = shfl(Enp, sA), xvc = shfl(Evc, sA), xnc = shfl(Enc, sA);
+                        bvp -= xvp;
+                        bnp -= xnp;
+                        bvc -= xvc;
+                        bnc -= xnc;
+                    }
+                    if (cA) {
+                        bvp += cvp;
+                        bnp += cnp;
+                        bvc += cvc;
+                        bnc += cnc;
+                    }
+                    /* thresholds on the lane prefix (sum > q2 <=> prefix > q2 - base), the
+                     * prevote one in the low half and the precommit one in the high half of a
+                     * u64, so the vote's own is one shift by its type byte */
+                    const uint32_t qA = recA.x;
+                    uint64_t TVa = u64of(qA - bvp, qA - bvc), TNa = u64of(qA - bnp, qA - bnc);
+                    uint64_t TAa = u64of(qA - bvp - bnp, qA - bvc - bnc);
+                    /* unit B: unit A's thresholds, or (split) its own instance from 0: the lane
+                     * prefix there includes unit A's part, P3 */
+                    uint64_t TVb = TVa, TNb = TNa, TAb = TAa;
+                    if (multi && split) {
+                        const uint32_t qB = recB.x;
+                        const uint32_t p3vp = (uint32_t)P3 & 0xFFFFu, p3np = (uint32_t)P3 >> 16;
+                        const uint32_t p3vc = (uint32_t)(P3 >> 32) & 0xFFFFu, p3nc = (uint32_t)(P3 >> 48);
+                        TVb = u64of(qB + p3vp, qB + p3vc);
+                        TNb = u64of(qB + p3np, qB + p3nc);
+                        TAb = u64of(qB + p3vp + p3np, qB + p3vc + p3nc);
+                    }
+                    /* per vote: is_quorum on its own type's sums, precedence as a level */
+                    uint32_t l0 = 0, l1 = 0;
+#pragma unroll
+                    for (uint32_t s = 0; s < LV; ++s) {
+                        const uint32_t bs = 8u * (s & 3u);
+                        const uint32_t tsh = __builtin_amdgcn_ubfe(s < 4u ? ts0 : ts1, bs, 8u);
+                        const int32_t tv = (int32_t)(uint32_t)((s < 4u ? TVa : TVb) >> tsh);
+                        const int32_t tn = (int32_t)(uint32_t)((s < 4u ? TNa : TNb) >> tsh);
+                        const int32_t ta = (int32_t)(uint32_t)((s < 4u ? TAa : TAb) >> tsh);
+                        const int32_t sv = (int32_t)(Dw[s] & 0xFFFFu), sn = (int32_t)(Dw[s] >> 16);
+                        uint32_t l = sv + sn > ta ? 1u : 0u;
+                        l = sn > tn ? 2u : l;
+                        l = sv > tv ? 3u : l;
+                        if (s < 4u) l0 |= l << bs;
+                        else l1 |= l << bs;
+                    }
+                    lv0 |= l0 & rm0;
+                    lv1 |= l1 & rm1;
+                    if (lastc) { /* the last segment's executors after the chunk (lane 0 writes) */
+                        const uint32_t nvp = rdl(Ivp, 63u) - rdl(Evp, slast) + (cL ? cvp : 0u);
+                        const uint32_t nnp = rdl(Inp, 63u) - rdl(Enp, slast) + (cL ? cnp : 0u);
+                        const uint32_t nvc = rdl(Ivc, 63u) - rdl(Evc, slast) + (cL ? cvc : 0u);
+                        const uint32_t nnc = rdl(Inc, 63u) - rdl(Enc, slast) + (cL ? cnc : 0u);
+                        if (lane == 0u) {
+                            B[K] = nvp;
+                            B[K + 1u] = nvc;
+                            B[2u * R + K] = nnp;
+                            B[2u * R + K + 1u] = nnc;
+                        }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
+                if (lastc) cpar ^= 1u;
+                /* to_event by (type, level); INVALID for a vote that checked out */
+                uint32_t c0 = __builtin_amdgcn_perm(EV_HI, EV_LO, lv0 | (ts0c >> 3));
+                uint32_t c1 = __builtin_amdgcn_perm(EV_HI, EV_LO, lv1 | (ts1c >> 3));
+                if (!all_ok) {
+                    c0 = (c0 & okb0) | ((actA ? ~okb0 : 0u) & (AGNES_CODE_INVALID * 0x01010101u));
+                    c1 = (c1 & okb1) | ((actB ? ~okb1 : 0u) & (AGNES_CODE_INVALID * 0x01010101u));
+                }
+
+                /* ---- K4: State::apply(v.round, event) in stream order ---- */
+                if (SM) {
+                    uint32_t* const rA = itab + RECW * kA;
+                    uint32_t* const rB = itab + RECW * kB;
+                    const uint2 eA = *reinterpret_cast<const uint2*>(rA + R_EQ); /* State.round bytes, valid-from-start */
+                    const uint2 eB = *reinterpret_cast<const uint2*>(rB + R_EQ);
+                    /* the roles of a unit's votes its step keeps; all but the commit one only at
+                     * State.round (state_machine.rs:184-211) */
+                    auto roles = [&](uint32_t smask, uint32_t eq, uint32_t r4, uint32_t c4, bool act) -> uint32_t {
+                        const uint32_t eqb = mark_bytes(zero_marks(r4 ^ eq));
+                        const uint32_t x = __builtin_amdgcn_perm(XT_HI, XT_LO, c4 & 0x07070707u) & smask &
+                                           (eqb | (X_C * 0x01010101u));
+                        return act ? x : 0u;
+                    };
+                    const uint32_t x0 = roles(recA.w, eA.x, r8[0], c0, actA), x1 = roles(recB.w, eB.x, r8[1], c1, actB);
+                    if (ballot((x0 | x1) != 0u)) {
+                        const uint32_t pos0 = rc + o8, pos1 = pos0 + 4u; /* stream-relative */
+                        /* the first commit and P1 candidate of each instance: atomic min */
+                        {
+                            const uint32_t cb0 = x0 & (X_C * 0x01010101u), cb1 = x1 & (X_C * 0x01010101u);
+                            const uint32_t pb0 = x0 & (X_P1 * 0x01010101u), pb1 = x1 & (X_P1 * 0x01010101u);
+                            if (cb0) atomicMin(rA + R_C, pos0 + ((uint32_t)__builtin_ctz(cb0) >> 3));
+                            if (pb0) atomicMin(rA + R_P1, pos0 + ((uint32_t)__builtin_ctz(pb0) >> 3));
+                            if (cb1) atomicMin(rB + R_C, pos1 + ((uint32_t)__builtin_ctz(cb1) >> 3));
+                            if (pb1) atomicMin(rB + R_P1, pos1 + ((uint32_t)__builtin_ctz(pb1) >> 3));
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                        const uint2 pcA = *reinterpret_cast<const uint2*>(rA + R_P1);
+                        const uint2 pcB = *reinterpret_cast<const uint2*>(rB + R_P1);
+                        /* messages of one unit (4 votes at pos), branch-free; lo_bytes(d) = 0xFF
+                         * in the bytes below d, d clamped to 0..4 */
+                        auto lo_bytes = [](int32_t d) -> uint32_t {
+                            const uint32_t k = (uint32_t)min(max(d, 0), 4);
+                            return (uint32_t)((0xFFFFFFFFull << (8u * k)) >> 32);
+                        };
+                        auto unit = [&](uint32_t x, uint32_t pos, uint2 pc, uint32_t vall, uint32_t nnb, uint32_t& atP,
+                                        uint32_t& atC, uint32_t& vc) -> uint32_t {
+                            const uint32_t p1 = pc.x, cc = pc.y;
+                            /* (a P1 after the commit never happens: then the Prevote step ends at C) */
+                            const bool p1ok = p1 < cc;
+                            const int32_t dC = cc == NONE ? 4 : (int32_t)(cc - pos);
+                            const int32_t dP = p1ok ? (int32_t)(p1 - pos) : dC;
+                            const uint32_t alive = lo_bytes(dC), pre = lo_bytes(dP);
+                            atP = p1ok ? lo_bytes(dP + 1) ^ pre : 0u; /* the P1 vote's byte */
+                            atC = lo_bytes(dC + 1) ^ alive; /* the commit vote's byte */
+                            /* TimeoutPrevote before P1 (:196), TimeoutPrecommit before C (:208);
+                             * precommit(r, v) / (r, None) at P1 (:197-198); Decision at C (:211) */
+                            uint32_t msg = (x & ((pre & (X_TP * 0x01010101u)) | (alive & (X_TC * 0x01010101u)))) << 2;
+                            msg |= atP & ((AGNES_VMSG_PRECOMMIT_NIL << AGNES_CODE_MSG_SHIFT) * 0x01010101u +
+                                          (x & (X_PV * 0x01010101u)));
+                            msg |= atC & ((AGNES_VMSG_DECISION << AGNES_CODE_MSG_SHIFT) * 0x01010101u);
+                            /* valid: non-nil PolkaValues at State.round from P1 on (or from the
+                             * start, entering in Precommit), before C (:198, :202) */
+                            vc = x & alive & (~pre | vall) & nnb & (X_PV * 0x01010101u);
+                            return msg;
+                        };
+                        uint32_t aP0, aC0, v0, aP1, aC1, v1;
+                        c0 |= unit(x0, pos0, pcA, eA.y, ~mark_bytes(nb0 << 3), aP0, aC0, v0);
+                        c1 |= unit(x1, pos1, pcB, eB.y, ~mark_bytes(nb1 << 3), aP1, aC1, v1);
+                        const uint32_t lk0 = aP0 & (x0 << 3) & 0x80808080u, lk1 = aP1 & (x1 << 3) & 0x80808080u;
+                        if (ballot((lk0 | lk1 | aC0 | aC1 | v0 | v1) != 0u)) { /* the few lanes with a State write */
+                            auto vat = [&](uint32_t h, uint32_t b) { /* value of vote b of unit h */
+                                const uint32_t* const v = value + 4u * h;
+                                return b == 0u ? v[0] : (b == 1u ? v[1] : (b == 2u ? v[2] : v[3]));
+                            };
+                            if (lk0) { rA[R_LOCK] = vat(0u, (uint32_t)__builtin_ctz(lk0) >> 3); rA[R_DF] |= F_LOCK; }
+                            if (lk1) { rB[R_LOCK] = vat(1u, (uint32_t)__builtin_ctz(lk1) >> 3); rB[R_DF] |= F_LOCK; }
+                            if (aC0) {
+                                const uint32_t b = (uint32_t)__builtin_ctz(aC0) >> 3;
+                                rA[R_DEC] = vat(0u, b);
+                                rA[R_DF] = (rA[R_DF] & F_LOCK) | ((r8[0] >> (8u * b)) & 0xFFu);
+                            }
+                            if (aC1) {
+                                const uint32_t b = (uint32_t)__builtin_ctz(aC1) >> 3;
+                                rB[R_DEC] = vat(1u, b);
+                                rB[R_DF] = (rB[R_DF] & F_LOCK) | ((r8[1] >> (8u * b)) & 0xFFu);
+                            }
+                            if (v0) {
+                                const uint32_t b = (31u - (uint32_t)__builtin_clz(v0)) >> 3;
+                                atomicMax(vtab + kA, ((unsigned long long)(pos0 + b + 1u) << 32) | vat(0u, b));
+                            }
+                            if (v1) {
+                                const uint32_t b = (31u - (uint32_t)__builtin_clz(v1)) >> 3;
+                                atomicMax(vtab + kB, ((unsigned long long)(pos1 + b + 1u) << 32) | vat(1u, b));
+                            }
+                        }
+                    }
+                }
+
+                /* codes (deferred) */
+                dc0 = c0;
+                dc1 = c1;
+                dc_act = actB ? 2u : (actA ? 1u : 0u);
+                dc_at = c;
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        /* batch end: the records into the staged States, the States out, then the next batch */
+        if (SM && m) {
+            if (smf) dma_wait(); /* no chunk ran: the staged States are still in flight */
+        }
+        if (SM && m && H.stream) { /* (a walk-list batch's States are the walk kernel's) */
+            if (!smf && lane < m) {
+                const uint32_t* const rk = itab + RECW * lane;
+                uint32_t* const sp = reinterpret_cast<uint32_t*>(sbh + 64u * lane);
+                const uint32_t p1 = rk[R_P1], cc = rk[R_C], df = rk[R_DF];
+                const uint64_t vd = vtab[lane];
+                const uint32_t step = cc != NONE ? (uint32_t)AGNES_STEP_COMMIT
+                                                 : (p1 < cc ? (uint32_t)AGNES_STEP_PRECOMMIT : rk[R_STEP]);
+                uint32_t fl = (sp[13] & ~0xFFu) | step;
+                if ((df & F_LOCK) && p1 < cc) { sp[4] = sp[2]; sp[5] = sp[3]; sp[10] = rk[R_LOCK]; fl |= 1u << 8; }
+                if (vd) { sp[6] = sp[2]; sp[7] = sp[3]; sp[11] = (uint32_t)vd; fl |= 1u << 16; }
+                if (cc != NONE) { sp[8] = df & 0xFFu; sp[9] = 0u; sp[12] = rk[R_DEC]; fl |= 1u << 24; }
+                sp[13] = fl;
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (lane < 4u * m) {
+                const uint4 v = *reinterpret_cast<const uint4*>(sbh + o16);
+                reinterpret_cast<uint4*>(a.states + H.s0)[lane] = v;
+            }
+        }
+        if (N.s0 >= N.e0) break;
+        if (N.stage < 3u) { /* a short batch: the rest of the header now */
+            if (N.stage == 1u) hdr2(N);
+            hdr3(N);
+            if (N.stream) dma_states(N, spar ^ 1u);
+        }
+        H = N;
+        spar ^= 1u;
+        range_of(rdl(tq, 0u), N.s0, N.e0); /* the batch after, grabbed one batch ago */
+        if (lane == 0) tq = atomicAdd(ctr, 1u);
+        hdr1(N);
+    }
+    flush();
+    const uint32_t nb = rdl(scan(bad), 63u);
+    if (lane == 0 && nb) atomicAdd(a.n_invalid, (unsigned long long)nb);
+}
+
+} // namespace flow
+} // namespace agnes
+
+/* ------------------------------------------------------------------ */
+/* launcher                                                            */
+
+template <bool SM, bool R1>
+static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStream_t st) {
+    const uint32_t n = a->vb.n_instances;
+    if (n == 0) return hipSuccess;
+    using agnes::flow::flow;
+    const void* fns[2] = {reinterpret_cast<const void*>(&flow<false, SM, R1>),
+                          reinterpret_cast<const void*>(&flow<true, SM, R1>)};
+    const uint32_t lpw = agnes::flow::lds_bytes(SM, a->max_rounds);
+    const uint64_t wave_lds = (uint64_t)lpw * AGNES_WAVES_PER_BLOCK;
+    const uint64_t pcb = agnes::align16(4ull * a->n_sets * a->n_vals);
+    /* blocks per CU from the occupancy query; the LDS power table only where it
+     * costs no occupancy.  Cached per (kernel, LDS shape). */
+    struct Occ { const void* fn; uint64_t wave_lds, pcb; int per_cu; bool pc; };
+    static thread_local Occ occ[8];
+    static thread_local unsigned occ_next = 0;
+    Occ* o = nullptr;
+    for (auto& c : occ)
+        if (c.per_cu && c.fn == fns[0] && c.wave_lds == wave_lds && c.pcb == pcb) o = &c;
+    if (!o) {
+        auto per_cu = [&](const void* fn, uint64_t lds) -> int {
+            if (lds > 160u * 1024u) return 0;
+            if (lds > 48u * 1024u &&
+                hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+                return 0;
+            int k = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&k, fn, 256, (size_t)lds) != hipSuccess) k = 0;
+            return k;
+        };
+        const int k0 = per_cu(fns[0], wave_lds);
+        const int k1 = pcb <= 32u * 1024u ? per_cu(fns[1], wave_lds + pcb) : 0;
+        o = &occ[occ_next++ % 8];
+        *o = Occ{fns[0], wave_lds, pcb, k0 > 0 ? k0 : 1, false};
+        if (k1 > 0 && k1 >= k0) {
+            o->per_cu = k1;
+            o->pc = true;
+        }
+    }
+    agnes_tally_args b = *a;
+    b.set_cache = 0;
+    b.power_cache = o->pc ? (uint32_t)pcb : 0u;
+    const uint64_t lds = wave_lds + b.power_cache;
+    const void* fn = fns[o->pc ? 1 : 0];
+    if (lds > 48u * 1024u) {
+        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    const uint64_t ncu = (uint64_t)(num_cus > 0 ? num_cus : 256);
+    uint64_t blocks = ((uint64_t)n + 4u * AGNES_WAVES_PER_BLOCK - 1u) / (4u * AGNES_WAVES_PER_BLOCK);
+    const uint64_t cap = ncu * (uint64_t)o->per_cu;
+    if (blocks > cap) blocks = cap;
+    if (blocks == 0) blocks = 1;
+    if (o->pc) hipLaunchKernelGGL((flow<true, SM, R1>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
+    else hipLaunchKernelGGL((flow<false, SM, R1>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
+    return hipGetLastError();
+}
+
+bool agnes_flow_supported(const agnes_tally_args* a) {
+    /* rounds 0..14 in the byte checks; the per-wave LDS fits 16 waves per CU */
+    return a->max_rounds <= 15u && agnes::flow::lds_bytes(true, a->max_rounds) * 16u <= 160u * 1024u;
+}
+
+hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t st) {
+    const bool sm = (a->flags & AGNES_FLAG_STATE_MACHINE) != 0 && a->states != nullptr;
+    if (a->max_rounds == 1u) return sm ? launch_flow_k<true, true>(a, num_cus, st) : launch_flow_k<false, true>(a, num_cus, st);
+    return sm ? launch_flow_k<true, false>(a, num_cus, st) : launch_flow_k<false, false>(a, num_cus, st);
+}

@@ -41,23 +41,20 @@ typedef struct agnes_tally_args {
     uint32_t max_rounds;
     uint32_t flags;
     uint8_t* codes;
-    agnes_state* states;
+    agnes_state* states;          /* out (and in, when states_in is null) */
+    const agnes_state* states_in; /* optional: the States before the call (the sweep route reads them here) */
     agnes_carry_rec* carry; /* optional [n_instances][2*max_rounds], in/out */
     unsigned long long* n_invalid;
     uint32_t* list;       /* deferred instances (fast kernel -> wide kernel), n_instances */
+    uint32_t* walk;       /* sweep: instances of batches that are not one vote stream, n_instances */
     uint32_t* list_count;
     uint32_t epoch_shift; /* bits of a vote's index inside its instance (DEDUP/SKIP tables) */
-    uint32_t dbg;         /* development knob (AGNES_DEBUG_SKIP): phases to skip; 0 in production */
     uint32_t set_cache;   /* bytes of block LDS caching the set constants (0: read them from HBM);
                              set by the launcher only when it costs no occupancy */
     uint32_t power_cache; /* bytes of block LDS holding the u32 power table (0: gather from HBM) */
     uint32_t one_inst;    /* AGNES_FLAG_ONE_INSTANCE: every segment is a slice of instance one_id */
     uint32_t one_id;
-    uint32_t* hint;       /* [n_instances] split route: position of the instance's first vote with
-                             an event (relative to its first vote), AGNES_NOHINT if none or if the
-                             instance was deferred to the LIST kernel; nullptr: not recorded */
 } agnes_tally_args;
-#define AGNES_NOHINT 0xFFFFFFFFu
 
 /* agnes_kernel_timing: HIP events around each launch while enabled (agnes_api.cpp) */
 extern "C" void agnes_kt_mark(const char* name, hipStream_t st, bool begin);
@@ -81,9 +78,13 @@ hipError_t agnes_launch_tally(const agnes_tally_args* a, uint32_t mode, int num_
  * below 2^31, the rest appended to a->list for the i64 LIST kernel */
 hipError_t agnes_launch_tally_fast(const agnes_tally_args* a, uint32_t mode, int num_cus,
                                    hipStream_t stream);
-/* the stream kernel (agnes_stream.hip): REFERENCE mode without RoundSkip, batches of
- * consecutive instances walked as one vote stream; same deferral protocol */
-hipError_t agnes_launch_tally_stream(const agnes_tally_args* a, int num_cus, hipStream_t stream);
+/* the fused sweep kernel (agnes_sweep.hip): REFERENCE mode without RoundSkip, tally
+ * and State machine in one pass; same deferral protocol */
+bool agnes_sweep_supported(const agnes_tally_args* a);
+hipError_t agnes_launch_sweep(const agnes_tally_args* a, int num_cus, hipStream_t stream);
+/* the 8-votes-per-lane flow kernel (agnes_flow.hip) for the sweep route's streams */
+bool agnes_flow_supported(const agnes_tally_args* a);
+hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t stream);
 /* the batched State::apply pass over the codes a tally kernel left (agnes_apply.hip):
  * one instance per lane, skipping the instances deferred to the LIST kernel */
 bool agnes_apply_codes_supported(const agnes_tally_args* a);
@@ -110,9 +111,14 @@ hipError_t agnes_launch_dedup(const agnes_vote_batch* vb, uint32_t inst_id, uint
 hipError_t agnes_launch_dedup_reject(const uint8_t* type_masked, uint64_t n, uint8_t* codes, hipStream_t stream);
 
 #define AGNES_WAVES_PER_BLOCK 4
-/* list_count[0] counts the deferred list; list_count[1 .. AGNES_QUEUE_WORDS-1] are the
- * fast kernel's work-queue counters; all zeroed before each launch */
-#define AGNES_QUEUE_WORDS 257
+/* list_count[0] counts the deferred (i64 LIST) list; list_count[1 .. AGNES_QUEUE_N] are
+ * the u32 kernels' work-queue counters; list_count[AGNES_WALK_COUNT] counts the sweep's
+ * walk list and list_count[AGNES_WALK_QUEUE] is the walk kernel's queue counter; all
+ * zeroed before each launch */
+#define AGNES_QUEUE_N 256
+#define AGNES_WALK_COUNT (AGNES_QUEUE_N + 1)
+#define AGNES_WALK_QUEUE (AGNES_QUEUE_N + 2)
+#define AGNES_QUEUE_WORDS (AGNES_QUEUE_N + 4)
 #define AGNES_MAX_LDS_PER_WAVE (36 * 1024)
 
 #endif

@@ -32,8 +32,6 @@
  *
  * No MFMA: the path is HBM-bound integer work.
  */
-#include <cstdlib>
-
 #include "agnes_device.h"
 #include "agnes_gen.h"
 #include "agnes_internal.h"
@@ -1170,7 +1168,7 @@ static hipError_t launch_k(const agnes_tally_args* a, uint32_t lpw, int num_cus,
 template <uint32_t MODE, bool SKIP, bool SM>
 static hipError_t launch_mode(const agnes_tally_args* a, uint32_t lpw, int num_cus, bool wide_all,
                               hipStream_t st) {
-    if (wide_all) {
+    if (wide_all || ((a->flags >> AGNES_ROUTE_SHIFT) & AGNES_ROUTE_MASK) == AGNES_ROUTE_WIDE) {
         AgnesKt kt("tally_wide", st);
         return launch_k<true, MODE, SKIP, SM, false>(a, lpw, num_cus, st);
     }
@@ -1180,39 +1178,29 @@ static hipError_t launch_mode(const agnes_tally_args* a, uint32_t lpw, int num_c
         e = hipMemsetAsync(a->list_count, 0, AGNES_QUEUE_WORDS * sizeof(uint32_t), st);
     }
     if (e == hipSuccess) {
-        /* REFERENCE without RoundSkip: instance-straddling stream chunks (C2 tally
-         * 0.74 vs 0.88 ms per-instance).  With the State machine the tally kernel
-         * leaves codes only and the one-instance-per-lane apply pass (agnes_apply.hip)
-         * follows: the fused State machine costs the tally kernels registers and
-         * serial ballot loops (C2 1.39 ms per-instance fused, 1.82 ms stream fused).
-         * Development knobs, read per launch (tests switch them):
-         *   AGNES_STREAM 0 never stream, 2 the stream kernel with its fused State machine;
-         *   AGNES_APPLY  0 never the apply pass (the fused State machine kernels). */
-        const char* d = std::getenv("AGNES_STREAM");
-        const int stream_lvl = d && d[0] >= '0' && d[0] <= '2' ? d[0] - '0' : 1;
-        const char* p = std::getenv("AGNES_APPLY");
-        const int apply_lvl = p && p[0] >= '0' && p[0] <= '2' ? p[0] - '0' : 1;
-        const bool stream = MODE == AGNES_MODE_REFERENCE && !SKIP && stream_lvl >= 1;
-        const bool fused_stream = SM && stream_lvl == 2;
-        /* per-instance route (DEDUP / RoundSkip) split as well: C4 1.04 vs 1.11 ms fused */
-        const bool split = SM && !fused_stream && agnes_apply_codes_supported(a) && apply_lvl >= 1;
-        agnes_tally_args b = *a;
-        if (split) b.flags &= ~AGNES_FLAG_STATE_MACHINE;
-        /* first-event hints: the stream kernel records them for the apply pass */
-        const bool hints = split && stream && a->hint != nullptr;
-        if (!hints) b.hint = nullptr;
-        if (stream && (!SM || fused_stream || split)) {
-            AgnesKt kt("tally_stream", st);
-            e = agnes_launch_tally_stream(&b, num_cus, st);
+        /* REFERENCE without RoundSkip: the fused sweep (tally + State machine in one
+         * pass over the votes, agnes_sweep.hip).  DEDUP / RoundSkip: the per-instance
+         * kernel, with the State machine either fused or in the one-instance-per-lane
+         * apply pass (agnes_apply.hip).  AGNES_ROUTE_* in cfg->flags overrides the
+         * choice (diagnostics and the route-equivalence tests; results are identical). */
+        const uint32_t route = (a->flags >> AGNES_ROUTE_SHIFT) & AGNES_ROUTE_MASK;
+        const bool sweep = route == AGNES_ROUTE_AUTO && MODE == AGNES_MODE_REFERENCE && !SKIP &&
+                           agnes_sweep_supported(a);
+        if (sweep) {
+            e = agnes_launch_sweep(a, num_cus, st); /* the stream and walk kernels */
         } else {
-            AgnesKt kt("tally_fast", st);
-            e = agnes_launch_tally_fast(&b, MODE, num_cus, st);
-        }
-        if (e == hipSuccess && split) {
-            AgnesKt kt("apply_codes", st);
-            agnes_tally_args ap = *a;
-            ap.hint = hints ? a->hint : nullptr;
-            e = agnes_launch_apply_codes(&ap, st);
+            /* per-instance route: split (C4 1.04 vs 1.11 ms fused) unless forced fused */
+            const bool split = SM && route != AGNES_ROUTE_INSTANCE && agnes_apply_codes_supported(a);
+            agnes_tally_args b = *a;
+            if (split) b.flags &= ~AGNES_FLAG_STATE_MACHINE;
+            {
+                AgnesKt kt("tally_fast", st);
+                e = agnes_launch_tally_fast(&b, MODE, num_cus, st);
+            }
+            if (e == hipSuccess && split) {
+                AgnesKt kt("apply_codes", st);
+                e = agnes_launch_apply_codes(a, st);
+            }
         }
     }
     if (e == hipSuccess) {

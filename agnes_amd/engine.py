@@ -131,6 +131,18 @@ class Engine:
         check(self.lib.agnes_tally(self.ctx, C.byref(cfg), C.byref(b), _ptr(codes), _ptr(states),
                                    _stream_handle(stream)), "agnes_tally")
 
+    def tally_states(self, cfg: abi.Config, batch: DeviceBatch, codes: torch.Tensor,
+                     states_in: torch.Tensor, states_out: torch.Tensor, stream=None):
+        """agnes_tally_states: the States read from states_in, written to states_out."""
+        if codes.dtype != torch.uint8 or codes.numel() < batch.n_votes:
+            raise ValueError("codes must be a uint8 tensor of n_votes")
+        for t in (states_in, states_out):
+            if t.numel() < 64 * batch.n_instances:
+                raise ValueError("states must hold n_instances 64-byte records")
+        b = batch.c()
+        check(self.lib.agnes_tally_states(self.ctx, C.byref(cfg), C.byref(b), _ptr(codes), _ptr(states_in),
+                                          _ptr(states_out), _stream_handle(stream)), "agnes_tally_states")
+
     def tally_carried(self, cfg: abi.Config, batch: DeviceBatch, codes: torch.Tensor,
                       counts: torch.Tensor, stream=None):
         """agnes_tally_carried: counts = int64 tensor [n_instances, 2 * max_rounds, 3]

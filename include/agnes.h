@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AGNES_ABI_VERSION 1u
+#define AGNES_ABI_VERSION 2u
 
 /* ---------------------------------------------------------------------------
  * Status codes (reference never fails, state_machine.rs:212; these report
@@ -191,6 +191,28 @@ typedef struct agnes_state {
                                            agnes_config.reserved (C5: one huge instance split over
                                            waves and GPUs) */
 
+/* Route override, bits 8..9 of agnes_config.flags (diagnostics and the
+ * route-equivalence tests: every route gives identical codes and States).
+ *   AUTO      the engine's choice: the fused sweep for REFERENCE without RoundSkip,
+ *             the per-instance kernel + apply pass otherwise, the i64 kernel for
+ *             instances outside the u32 domain
+ *   INSTANCE  the per-instance u32 kernel with the State machine fused
+ *   SPLIT     the per-instance u32 kernel, then the one-instance-per-lane apply pass
+ *   WIDE      the i64 kernel for every instance */
+#define AGNES_ROUTE_SHIFT 8
+#define AGNES_ROUTE_MASK 0x3u
+#define AGNES_ROUTE_AUTO 0u
+#define AGNES_ROUTE_INSTANCE 1u
+#define AGNES_ROUTE_SPLIT 2u
+#define AGNES_ROUTE_WIDE 3u
+#define AGNES_FLAG_ROUTE(r) ((uint32_t)(r) << AGNES_ROUTE_SHIFT)
+/* Bits 16..20 of agnes_config.flags: minimum bits the DEDUP / RoundSkip first-vote
+ * tables spend on a vote's index inside its instance (0 = just enough for the
+ * batch).  More index bits leave fewer epochs per table fill, so the tables are
+ * recycled more often (testing the recycling; results are identical). */
+#define AGNES_EPOCH_BITS_SHIFT 16
+#define AGNES_FLAG_EPOCH_BITS(b) (((uint32_t)(b) & 0x1Fu) << AGNES_EPOCH_BITS_SHIFT)
+
 typedef struct agnes_config {
     uint32_t mode;       /* AGNES_MODE_*                                            */
     uint32_t flags;      /* AGNES_FLAG_*                                            */
@@ -279,6 +301,13 @@ int agnes_upload_power(agnes_ctx* ctx, const int64_t* power, uint32_t n_sets, ui
  * get AGNES_CODE_INVALID and are counted by agnes_last_error_count. */
 int agnes_tally(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
                 uint8_t* codes, agnes_state* states, void* stream);
+/* agnes_tally with the States read from states_in and written to states_out
+ * (State::apply takes self by value and returns the new State,
+ * state_machine.rs:174: a batch of heights can start from one template of
+ * States::new without copying it first).  states_in == NULL or == states_out:
+ * in place, as agnes_tally.  The two arrays must not overlap otherwise. */
+int agnes_tally_states(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
+                       uint8_t* codes, const agnes_state* states_in, agnes_state* states_out, void* stream);
 
 /* VoteCount of one (round, type) bucket (round_votes.rs:15-19): the executor state
  * a stream carries between calls.  value = the bucket's label, the last non-nil

@@ -23,6 +23,16 @@ GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 REF = json.load(open(os.path.join(GOLD, "reference_tests.json")))
 REGRESS = json.load(open(os.path.join(GOLD, "regress_small.json")))
 EV_BY_NAME = {n: i for i, n in enumerate(abi.EVENT_NAMES)}
+# every route the launcher can take (agnes_kernels.hip launch_mode), forced by the
+# cfg route field: the engine's choice (the fused sweep for REFERENCE without
+# RoundSkip), the per-instance kernel with the State machine fused, the same
+# followed by the apply pass, the i64 kernel for every instance
+ROUTES = {
+    "auto": abi.FLAG_ROUTE(abi.ROUTE_AUTO),
+    "fused": abi.FLAG_ROUTE(abi.ROUTE_INSTANCE),
+    "split": abi.FLAG_ROUTE(abi.ROUTE_SPLIT),
+    "wide": abi.FLAG_ROUTE(abi.ROUTE_WIDE),
+}
 
 
 @pytest.fixture(scope="module")
@@ -368,38 +378,26 @@ def test_early_quorum_labels(eng, mode, flags):
     assert_same(g, o)
 
 
-@pytest.mark.parametrize("stream", ["1", "2"])  # 2: the State machine on the stream kernel too
+@pytest.mark.parametrize("route", ["auto", "fused", "split"])
 @pytest.mark.parametrize("flags", [0, abi.FLAG_STATE_MACHINE])
 @pytest.mark.parametrize("lengths", [
     [0, 4, 8, 12, 60, 64, 68, 200, 252, 256, 260, 300, 516],   # lane-aligned: stream batches
     [4, 8, 12, 16, 20, 24, 28, 32],                            # many segments per chunk
     [200], [300, 600, 900, 1200]])                             # C2 / C3 shapes
-def test_stream_segments(eng, monkeypatch, stream, flags, lengths):
+def test_stream_segments(eng, route, flags, lengths):
     """Instance lengths that are multiples of 4 make every batch a vote stream
-    whose chunks straddle instances (agnes_stream.hip): segments, per-segment
+    whose chunks straddle instances (agnes_sweep.hip): segments, per-segment
     thresholds and carries, per-segment State::apply, several power sets."""
-    if stream == "2" and not flags:
-        pytest.skip("same launch as stream=1 without the State machine")
-    monkeypatch.setenv("AGNES_STREAM", stream)
+    if route == "split" and not flags:
+        pytest.skip("same launch as fused without the State machine")
     hb = _ragged_batch(31 + len(lengths), 6000, 17, 3, lengths)
     power = ol.gen_power(3, 5, 17, abi.POWER_UNIFORM, 1, 50)
     hb.instance_set = (np.arange(hb.n_instances) * 7 % 5).astype(np.uint32)
-    cfg = abi.config(abi.MODE_REFERENCE, flags, 3)
+    cfg = abi.config(abi.MODE_REFERENCE, flags | ROUTES[route], 3)
     st = _start_states(hb.n_instances) if flags & abi.FLAG_STATE_MACHINE else None
     g, o = run_both(eng, cfg, hb, power, None, st)
     assert_same(g, o)
     assert (g[0] & abi.CODE_EVENT_MASK != 0).any()
-
-
-@pytest.mark.parametrize("name", ["c2_sm", "c3_small", "c4_small"])
-def test_stream_state_machine_generated(eng, monkeypatch, name):
-    """The generated configs with the State machine forced onto the stream
-    kernel (AGNES_STREAM=2); c4 (RoundSkip) stays on the per-instance kernel."""
-    monkeypatch.setenv("AGNES_STREAM", "2")
-    p, hb, power, cfg = _make(name)
-    states = _start_states(p.n_instances) if cfg.flags & abi.FLAG_STATE_MACHINE else None
-    g, o = run_both(eng, cfg, hb, power, None, states)
-    assert_same(g, o)
 
 
 def test_stream_mixed_domains(eng):
@@ -415,29 +413,28 @@ def test_stream_mixed_domains(eng):
     assert_same(g, o)
 
 
-@pytest.mark.parametrize("route", ["split", "fast_split", "fused"])
+@pytest.mark.parametrize("route", ["auto", "split", "fused"])
 @pytest.mark.parametrize("mode,flags", [
     (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE),
     (abi.MODE_DEDUP, abi.FLAG_STATE_MACHINE | abi.FLAG_ROUND_SKIP)])
-def test_deferred_instances_and_set_fallback(eng, monkeypatch, route, mode, flags):
+def test_deferred_instances_and_set_fallback(eng, route, mode, flags):
     """Instances whose sums may reach 2^31 (len * maxpow) deferred by the u32 kernels
     to the i64 LIST kernel, mixed with fast ones, with the State machine; no
     instance_set, so the set of instance i is i % n_sets."""
-    _route(monkeypatch, route)
     hb = _ragged_batch(91, 6000, 13, 3, [8, 40, 200, 1200])
     power = ol.gen_power(91, 3, 13, abi.POWER_UNIFORM, 1 << 20, 1 << 21)
     hb.instance_set = None
-    g, o = run_both(eng, abi.config(mode, flags, 3), hb, power, None, _start_states(hb.n_instances))
+    g, o = run_both(eng, abi.config(mode, flags | ROUTES[route], 3), hb, power, None,
+                    _start_states(hb.n_instances))
     assert_same(g, o)
 
 
-def test_epoch_table_recycling(eng, monkeypatch):
+def test_epoch_table_recycling(eng):
     """DEDUP/RoundSkip tables tag entries with per-instance epochs; with few
-    epoch bits the tables are cleared every 3 instances (chunks cut there)."""
-    monkeypatch.setenv("AGNES_DEBUG_EPOCH_SHIFT", "30")
+    epoch bits (AGNES_FLAG_EPOCH_BITS(30)) the tables are cleared every 3 instances."""
     hb = _ragged_batch(5, 6000, 11, 2, [0, 1, 4, 9, 40, 70, 150])
     power = ol.gen_power(5, 4, 11, abi.POWER_UNIFORM, 1, 9)
-    cfg = abi.config(abi.MODE_DEDUP, abi.FLAG_ROUND_SKIP | abi.FLAG_STATE_MACHINE, 2)
+    cfg = abi.config(abi.MODE_DEDUP, abi.FLAG_ROUND_SKIP | abi.FLAG_STATE_MACHINE | abi.FLAG_EPOCH_BITS(30), 2)
     g, o = run_both(eng, cfg, hb, power, None, _start_states(hb.n_instances))
     assert_same(g, o)
     assert (g[0] & 7 == abi.CODE_REJECTED).any()
@@ -466,29 +463,11 @@ def test_c3_shard_parity(eng):
     assert_same(g, o)
 
 
-# Every route the launcher can take with the State machine on (agnes_kernels.hip
-# launch_mode): the default split (tally kernel, then the apply pass), the fused
-# per-instance kernel, the fused stream kernel, the per-instance tally + apply pass.
-ROUTES = {
-    "split": {},
-    "fused": {"AGNES_APPLY": "0"},
-    "stream_fused": {"AGNES_STREAM": "2"},
-    "fast_split": {"AGNES_STREAM": "0", "AGNES_APPLY": "2"},
-}
-
-
-def _route(monkeypatch, route):
-    for k in ("AGNES_STREAM", "AGNES_APPLY"):
-        monkeypatch.delenv(k, raising=False)
-    for k, v in ROUTES[route].items():
-        monkeypatch.setenv(k, v)
-
-
 @pytest.mark.parametrize("route", list(ROUTES))
 @pytest.mark.parametrize("name", ["c2_sm", "c3_small", "c4_small"])
-def test_routes_generated(eng, monkeypatch, route, name):
-    _route(monkeypatch, route)
+def test_routes_generated(eng, route, name):
     p, hb, power, cfg = _make(name)
+    cfg = abi.config(cfg.mode, cfg.flags | ROUTES[route], cfg.max_rounds)
     g, o = run_both(eng, cfg, hb, power, None, _start_states(p.n_instances))
     assert_same(g, o)
 
@@ -497,10 +476,10 @@ def test_routes_generated(eng, monkeypatch, route, name):
 @pytest.mark.parametrize("mode,flags", [
     (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE),
     (abi.MODE_DEDUP, abi.FLAG_STATE_MACHINE | abi.FLAG_ROUND_SKIP)])
-def test_routes_ragged_and_labels(eng, monkeypatch, route, mode, flags):
+def test_routes_ragged_and_labels(eng, route, mode, flags):
     """Ragged instances (many per chunk, empty ones) and early quorums whose nil
     votes carry labels from earlier lanes / chunks."""
-    _route(monkeypatch, route)
+    flags |= ROUTES[route]
     hb = _ragged_batch(21, 20000, 9, 3, [0, 0, 1, 2, 3, 5, 8, 13, 63, 64, 65, 130, 200])
     power = ol.gen_power(21, 13, 9, abi.POWER_UNIFORM, 1, 20)
     g, o = run_both(eng, abi.config(mode, flags, 3), hb, power, None, _start_states(hb.n_instances))
@@ -512,11 +491,10 @@ def test_routes_ragged_and_labels(eng, monkeypatch, route, mode, flags):
 
 
 @pytest.mark.parametrize("route", list(ROUTES))
-def test_routes_valid_from_input(eng, monkeypatch, route):
+def test_routes_valid_from_input(eng, route):
     """States entering in Precommit with `valid` already at their round
     (set_valid_value, state_machine.rs:202): a nil vote that reaches the value
     quorum first must set valid to its bucket's last value (round_votes.rs:50-54)."""
-    _route(monkeypatch, route)
     rng = np.random.default_rng(44)
     hb = _ragged_batch(44, 8000, 3, 2, [4, 8, 12, 40, 200])
     power = np.ones((1, 3), np.int64)
@@ -528,5 +506,6 @@ def test_routes_valid_from_input(eng, monkeypatch, route):
     st["valid_present"][sel] = 1
     st["valid_round"][sel] = 0
     st["valid_value"][sel] = 7  # a value no vote carries
-    g, o = run_both(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 2), hb, power, None, st)
+    g, o = run_both(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE | ROUTES[route], 2), hb, power,
+                    None, st)
     assert_same(g, o)

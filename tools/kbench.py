@@ -77,15 +77,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("variants", nargs="*", default=list(VARIANTS))
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--dbg", default="", help="comma list of AGNES_DEBUG_SKIP values to sweep")
     args = ap.parse_args()
     eng = Engine(0)
-    for d in (args.dbg.split(",") if args.dbg else [None]):
-        if d is not None:
-            os.environ["AGNES_DEBUG_SKIP"] = d
-            print(json.dumps({"AGNES_DEBUG_SKIP": d}), flush=True)
-        for v in args.variants:
-            run(eng, v, args.iters)
+    for v in args.variants:
+        run(eng, v, args.iters)
 
 
 if __name__ == "__main__":
