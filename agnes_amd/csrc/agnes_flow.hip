@@ -54,10 +54,11 @@ constexpr uint32_t SMALLB = 4u; /* batch size of the work queue's tail          
  * (0: no such set); the State machine's view: the roles its step keeps (one byte per
  * vote, 0 without the State machine), State.round in every byte, 0xFF bytes when it
  * enters in Precommit (valid from the start); the P1 and C positions (stream-relative,
- * ~0: none); locked value, decision value, decision round | F_LOCK << 8, step.  The
- * valid candidates, (position + 1) << 32 | value, are kept beside (vtab). */
-constexpr uint32_t R_Q2 = 0, R_PBASE = 1, R_NV = 2, R_SMASK = 3, R_EQ = 4, R_VALL = 5, R_P1 = 6, R_C = 7,
-                   R_LOCK = 8, R_DEC = 9, R_DF = 10, R_STEP = 11, RECW = 12;
+ * ~0: none); decision round | F_LOCK (P1 was a PolkaValue); step.  The last valid
+ * candidate's position + 1 is kept beside (vtab).  The values these positions name
+ * are read when the batch ends (its States are written one chunk later). */
+constexpr uint32_t R_Q2 = 0, R_PBASE = 1, R_NV = 2, R_EQ8 = 3, R_SMASK = 4, R_EQ = 5, R_VALL = 6, R_STEP = 7, R_P1 = 8,
+                   R_C = 9, R_DF = 10, RECW = 12;
 constexpr uint32_t F_LOCK = 0x100u;
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 
@@ -79,7 +80,7 @@ __host__ __device__ inline uint32_t carry_bytes(uint32_t R) { return (uint32_t)a
 /* per-wave LDS: DMA slot | carried executors (2 copies x (vw[2R], vn[2R]) u32) |
  * instance records | (State machine) valid candidates, two batches' staged States */
 __host__ __device__ inline uint32_t lds_bytes(bool sm, uint32_t R) {
-    return F_BYTES + carry_bytes(R) + FB * RECW * 4u + (sm ? FB * 8u + 2u * FB * 64u : 0u);
+    return F_BYTES + carry_bytes(R) + FB * RECW * 4u + (sm ? FB * 4u + 2u * FB * 64u : 0u);
 }
 
 __device__ __forceinline__ uint32_t zero_marks(uint32_t x) { /* 0x80 in the bytes of x that are zero */
@@ -146,7 +147,7 @@ struct Hdr {
 };
 
 template <bool PC, bool SM, bool R1>
-__global__ __launch_bounds__(256) void flow(agnes_tally_args a, uint32_t lds_per_wave) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void flow(agnes_tally_args a, uint32_t lds_per_wave) {
     const uint32_t lane = lane_id();
     const uint32_t wave = rfl(threadIdx.x >> 6);
     const uint32_t R = R1 ? 1u : a.max_rounds, nv = a.n_vals, ns = a.n_sets, n = a.vb.n_instances;
@@ -166,8 +167,8 @@ __global__ __launch_bounds__(256) void flow(agnes_tally_args a, uint32_t lds_per
     uint32_t* const crow = reinterpret_cast<uint32_t*>(base + F_BYTES);
     const uint32_t cw = 4u * R; /* one carry copy: vw[2R] then vn[2R] */
     uint32_t* const itab = reinterpret_cast<uint32_t*>(base + F_BYTES + carry_bytes(R));
-    unsigned long long* const vtab = reinterpret_cast<unsigned long long*>(base + F_BYTES + carry_bytes(R) + FB * RECW * 4u);
-    unsigned char* const sb = base + F_BYTES + carry_bytes(R) + FB * RECW * 4u + FB * 8u;
+    uint32_t* const vtab = reinterpret_cast<uint32_t*>(base + F_BYTES + carry_bytes(R) + FB * RECW * 4u);
+    unsigned char* const sb = base + F_BYTES + carry_bytes(R) + FB * RECW * 4u + FB * 4u;
     const agnes_state* const st_in = a.states_in ? a.states_in : a.states;
     uint32_t cpar = 0;
     uint64_t pf_at = ~0ull;
@@ -257,41 +258,94 @@ __global__ __launch_bounds__(256) void flow(agnes_tally_args a, uint32_t lds_per
         glds16(reinterpret_cast<const unsigned char*>(st_in + h.s0) + 16u * (lane < 4u * m ? lane : 0u),
                sb + par * (FB * 64u));
     };
-    auto dma_chunk = [&](uint64_t c) { /* the chunk's columns into the slot */
-        /* at the columns' end a lane past n_votes reads the chunk's first group instead
-         * (its votes lie past the stream: never active) */
-        uint32_t va = o16, vb = o16, ba = o4, bb = o4;
-        if (c + CH > NV) {
-            const uint64_t lim = NV - c;
-            const bool ia = 4u * lane + 4u <= lim, ib = 256u + 4u * lane + 4u <= lim;
-            va = ia ? o16 : 0u;
-            vb = ib ? o16 : 0u;
-            ba = ia ? o4 : 0u;
-            bb = ib ? o4 : 0u;
-        }
+    auto dma_chunk = [&](uint64_t c, uint32_t lo, uint32_t lim) { /* the chunk's votes lo..lim into the slot */
         __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): the slot's LDS reads are done */
-        sdma16(a.vb.instance + c, va, slotl + F_INST);
-        sdma16(a.vb.instance + c + 256u, vb, slotl + F_INST + 1024u);
-        sdma16(a.vb.value + c, va, slotl + F_VALUE);
-        sdma16(a.vb.value + c + 256u, vb, slotl + F_VALUE + 1024u);
-        sdma16(a.vb.validator + c, va, slotl + F_VAL);
-        sdma16(a.vb.validator + c + 256u, vb, slotl + F_VAL + 1024u);
-        sdma4(a.vb.round + c, ba, slotl + F_ROUND);
-        sdma4(a.vb.round + c + 256u, bb, slotl + F_ROUND + 256u);
-        sdma4(a.vb.type + c, ba, slotl + F_TYPE);
-        sdma4(a.vb.type + c + 256u, bb, slotl + F_TYPE + 256u);
+        if (lo == 0u && lim >= CH) {
+            sdma16(a.vb.instance + c, o16, slotl + F_INST);
+            sdma16(a.vb.instance + c + 256u, o16, slotl + F_INST + 1024u);
+            sdma16(a.vb.value + c, o16, slotl + F_VALUE);
+            sdma16(a.vb.value + c + 256u, o16, slotl + F_VALUE + 1024u);
+            sdma16(a.vb.validator + c, o16, slotl + F_VAL);
+            sdma16(a.vb.validator + c + 256u, o16, slotl + F_VAL + 1024u);
+            sdma4(a.vb.round + c, o4, slotl + F_ROUND);
+            sdma4(a.vb.round + c + 256u, o4, slotl + F_ROUND + 256u);
+            sdma4(a.vb.type + c, o4, slotl + F_TYPE);
+            sdma4(a.vb.type + c + 256u, o4, slotl + F_TYPE + 256u);
+        } else { /* a stream's first or last chunk: only its lanes load (4-vote groups; the
+                  * rest of the slot is never read as active) */
+            if (4u * lane >= lo && 4u * lane < lim) {
+                sdma16(a.vb.instance + c, o16, slotl + F_INST);
+                sdma16(a.vb.value + c, o16, slotl + F_VALUE);
+                sdma16(a.vb.validator + c, o16, slotl + F_VAL);
+                sdma4(a.vb.round + c, o4, slotl + F_ROUND);
+                sdma4(a.vb.type + c, o4, slotl + F_TYPE);
+            }
+            if (256u + 4u * lane >= lo && 256u + 4u * lane < lim) {
+                sdma16(a.vb.instance + c + 256u, o16, slotl + F_INST + 1024u);
+                sdma16(a.vb.value + c + 256u, o16, slotl + F_VALUE + 1024u);
+                sdma16(a.vb.validator + c + 256u, o16, slotl + F_VAL + 1024u);
+                sdma4(a.vb.round + c + 256u, o4, slotl + F_ROUND + 256u);
+                sdma4(a.vb.type + c + 256u, o4, slotl + F_TYPE + 256u);
+            }
+        }
     };
 
     /* deferred code stores: issued behind the next chunk's gather and DMA (vmcnt
      * retires in issue order) */
     uint64_t dc_at = ~0ull;
-    uint32_t dc0 = 0, dc1 = 0, dc_act = 0; /* dc_act: 2 both units, 1 unit A only */
+    uint32_t dc0 = 0, dc1 = 0, dc_act = 0; /* dc_act: bit 0 unit A, bit 1 unit B active */
     auto flush = [&]() {
         if (dc_at != ~0ull) {
-            if (dc_act == 2u) sstore8(a.codes + dc_at, o8, dc0, dc1);
+            if (dc_act == 3u) sstore8(a.codes + dc_at, o8, dc0, dc1);
             else if (dc_act == 1u) sstore4(a.codes + dc_at, o8, dc0);
+            else if (dc_act == 2u) sstore4(a.codes + dc_at, o8 + 4u, dc1);
             dc_at = ~0ull;
         }
+    };
+
+    /* A finished batch's States wait for the values at its P1 / C / valid positions:
+     * LDS-DMA'd at the batch's end straight into the staged States' locked / valid /
+     * decision value words (lane 16 k' of a load writes the State 4 j + k'), and the
+     * States are patched from the records and written out at the next chunk's top,
+     * behind its DMA wait (no register stays live across the chunks). */
+    uint32_t pend_m = 0, pend_s0 = 0, pend_par = 0;
+    auto dma_values = [&](uint32_t mm, uint64_t s0v, uint32_t par) {
+        const uint32_t* const vcol = a.vb.value + s0v;
+        for (uint32_t j = 0; 4u * j < mm; ++j) {
+            const uint32_t k = 4u * j + (lane >> 4);
+            const bool own = (lane & 15u) == 0u && k < mm;
+            uint32_t p1 = NONE, cc = NONE, df = 0, vp = 0;
+            if (own) {
+                const uint32_t* const rk = itab + RECW * k;
+                p1 = rk[R_P1];
+                cc = rk[R_C];
+                df = rk[R_DF];
+                vp = vtab[k];
+            }
+            const uint32_t ml = lds_addr(sb + par * (FB * 64u)) + 256u * j;
+            if ((df & F_LOCK) && p1 < cc) sdma4(vcol, 4u * p1, ml + 40u);  /* locked_value   */
+            if (vp) sdma4(vcol, 4u * (vp - 1u), ml + 44u);                 /* valid_value    */
+            if (cc != NONE) sdma4(vcol, 4u * cc, ml + 48u);                /* decision_value */
+        }
+    };
+    auto finalize = [&]() { /* the staged States patched from the records and written out */
+        unsigned char* const sbp = sb + pend_par * (FB * 64u);
+        if (lane < pend_m) {
+            const uint32_t* const rk = itab + RECW * lane;
+            const uint32_t p1 = rk[R_P1], cc = rk[R_C], df = rk[R_DF], vp = vtab[lane];
+            uint32_t* const sp = reinterpret_cast<uint32_t*>(sbp + 64u * lane);
+            const uint32_t step = cc != NONE ? (uint32_t)AGNES_STEP_COMMIT
+                                             : (p1 < cc ? (uint32_t)AGNES_STEP_PRECOMMIT : rk[R_STEP]);
+            uint32_t fl = (sp[13] & ~0xFFu) | step;
+            if ((df & F_LOCK) && p1 < cc) { sp[4] = sp[2]; sp[5] = sp[3]; fl |= 1u << 8; }
+            if (vp) { sp[6] = sp[2]; sp[7] = sp[3]; fl |= 1u << 16; }
+            if (cc != NONE) { sp[8] = df & 0xFFu; sp[9] = 0u; fl |= 1u << 24; }
+            sp[13] = fl;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (lane < 4u * pend_m)
+            reinterpret_cast<uint4*>(a.states + pend_s0)[lane] = *reinterpret_cast<const uint4*>(sbp + o16);
+        pend_m = 0;
     };
 
     Hdr H, N;
@@ -321,10 +375,31 @@ __global__ __launch_bounds__(256) void flow(agnes_tally_args a, uint32_t lds_per
             w0 = rdl(w0, 0u);
             if (lane < m) a.walk[w0 + lane] = H.s0 + lane;
         } else {
-            { /* instance records */
-                const uint32_t q2k = shfl(H.q2, HI + lane);
-                const uint32_t setk = shfl(H.olo, HI + lane);
-                if (lane < m) {
+            /* the instance records' constants (written at the first chunk's top, once the
+             * batch before has been finalized from its records) */
+            const uint32_t q2k = shfl(H.q2, HI + lane);
+            const uint32_t setk = shfl(H.olo, HI + lane);
+            /* the stream: instance starts relative to its first vote */
+            const uint64_t S0 = u64of(rdl(H.olo, 0u), rdl(H.ohi, 0u));
+            const uint32_t s0lo = (uint32_t)S0;
+            /* chunks at 128-vote boundaries (whole lines of every column): the first one
+             * starts `lead` votes before the stream; positions are relative to Sa */
+            const uint64_t Sa = S0 & ~127ull;
+            const uint32_t lead = (uint32_t)(S0 - Sa);
+            const uint32_t Lend = rdl(H.olo, m) - s0lo + lead;
+            const uint32_t rl = H.olo - s0lo + lead;
+            const uint32_t rn = shfl(rl, lane + 1u);
+            const uint64_t NE = ballot(lane < m && rn > rl);
+            const uint32_t relv = lane <= m ? rl : 0x7FFFFFFFu;
+            const uint64_t mm64 = (1ull << m) - 1ull;
+
+            for (uint32_t rc = 0; rc < Lend; rc += CH) {
+                const uint64_t c = Sa + rc;
+                const uint32_t lo_r = rc == 0u ? lead : 0u; /* the chunk's active votes: lo_r .. hi_r */
+                if (pf_at != c) dma_chunk(c, lo_r, Lend - rc); /* not prefetched: a wave's first chunk */
+                dma_wait(); /* this chunk's DMA (and a new batch's States) have landed */
+                if (SM && pend_m) finalize(); /* the batch before (its values landed too) */
+                if (rc == 0u && lane < m) { /* instance records */
                     uint32_t* const rk = itab + RECW * lane;
                     rk[R_Q2] = q2k;
                     rk[R_PBASE] = setk < ns ? setk * nv : 0u;
@@ -333,23 +408,8 @@ __global__ __launch_bounds__(256) void flow(agnes_tally_args a, uint32_t lds_per
                     rk[R_P1] = NONE;
                     rk[R_C] = NONE;
                     rk[R_DF] = 0u;
-                    if (SM) vtab[lane] = 0ull;
+                    if (SM) vtab[lane] = 0u;
                 }
-            }
-            /* the stream: instance starts relative to its first vote */
-            const uint64_t S0 = u64of(rdl(H.olo, 0u), rdl(H.ohi, 0u));
-            const uint32_t s0lo = (uint32_t)S0;
-            const uint32_t Lend = rdl(H.olo, m) - s0lo;
-            const uint32_t rl = H.olo - s0lo;
-            const uint32_t rn = shfl(rl, lane + 1u);
-            const uint64_t NE = ballot(lane < m && rn > rl);
-            const uint32_t relv = lane <= m ? rl : 0x7FFFFFFFu;
-            const uint64_t mm64 = (1ull << m) - 1ull;
-
-            for (uint32_t rc = 0; rc < Lend; rc += CH) {
-                const uint64_t c = S0 + rc;
-                if (pf_at != c) dma_chunk(c); /* not prefetched: a wave's first chunk */
-                dma_wait(); /* this chunk's DMA (and a new batch's States) have landed */
                 if (SM && smf) { /* the State machine's view of each instance (state_machine.rs:184) */
                     if (lane < m) {
                         const uint32_t* const sp = reinterpret_cast<const uint32_t*>(sbh + 64u * lane);
@@ -359,6 +419,7 @@ __global__ __launch_bounds__(256) void flow(agnes_tally_args a, uint32_t lds_per
                         if (rnd < 0 || rnd > 255) smask &= X_C * 0x01010101u; /* no vote round equals State.round */
                         uint32_t* const rk = itab + RECW * lane;
                         rk[R_SMASK] = smask;
+                        rk[R_EQ8] = (rnd >= 0 && rnd <= 255) ? (uint32_t)rnd : 0x100u;
                         rk[R_EQ] = rep4((uint32_t)rnd);
                         rk[R_VALL] = step == AGNES_STEP_PRECOMMIT ? 0xFFFFFFFFu : 0u;
                         rk[R_STEP] = step;
@@ -377,14 +438,14 @@ __global__ __launch_bounds__(256) void flow(agnes_tally_args a, uint32_t lds_per
 
                 /* ---- segments: the instances the chunk straddles, at unit granularity ---- */
                 const uint32_t tj = relv - rc; /* instance start relative to the chunk */
-                const uint32_t k0 = 63u - (uint32_t)__builtin_clzll(ballot((int32_t)tj <= 0) & mm64);
-                uint64_t bk = ballot(tj - 1u < CH - 1u) & NE; /* non-empty, starting inside */
+                const uint32_t k0 = 63u - (uint32_t)__builtin_clzll(ballot((int32_t)tj <= (int32_t)lo_r) & mm64);
+                uint64_t bk = ballot(tj - lo_r - 1u < CH - lo_r - 1u) & NE; /* non-empty, starting inside */
                 const bool multi = bk != 0ull;
                 const bool cont0 = ((ballot((int32_t)tj < 0) >> k0) & 1ull) != 0ull;
                 const uint32_t left = Lend - rc;
                 const bool lastc = left > CH && !ballot(tj == CH);
                 const uint32_t hi_r = left < CH ? left : CH;
-                const bool actA = o8 < hi_r, actB = o8 + 4u < hi_r;
+                const bool actA = o8 >= lo_r && o8 < hi_r, actB = o8 + 4u >= lo_r && o8 + 4u < hi_r;
                 uint32_t kA = k0, kB = k0, sA = 0, klast = k0, slast = 0;
                 bool split = false;
                 if (multi) {
@@ -410,7 +471,7 @@ __global__ __launch_bounds__(256) void flow(agnes_tally_args a, uint32_t lds_per
                     sA = wA >> 8;
                     kB = wB & 0xFFu;
                 }
-                const uint4 recA = *reinterpret_cast<const uint4*>(itab + RECW * kA); /* q2, pbase, nv, smw */
+                const uint4 recA = *reinterpret_cast<const uint4*>(itab + RECW * kA); /* q2, pbase, nv, State.round (0x100: none) */
                 const uint4 recB = multi ? *reinterpret_cast<const uint4*>(itab + RECW * kB) : recA;
 
                 /* ---- K1: votes of the chunk + validation + weight gather ---- */
@@ -479,7 +540,7 @@ __global__ __launch_bounds__(256) void flow(agnes_tally_args a, uint32_t lds_per
                     /* K1: w = power[set][validator] (consensus_executor.rs:62-63 ->
                      * validators.rs:7); a vote that checked out weighs 0 */
                     const uint32_t pbA = recA.y, pbB = recB.y;
-                    if (all_ok && hi_r == CH) {
+                    if (all_ok && lo_r == 0u && hi_r == CH) {
 #pragma unroll
                         for (uint32_t s = 0; s < LV; ++s) {
                             const uint32_t idx = (s < 4u ? pbA : pbB) + val[s];
@@ -501,10 +562,19 @@ __global__ __launch_bounds__(256) void flow(agnes_tally_args a, uint32_t lds_per
                                       "v"(w[6]), "v"(w[7]));
                 { /* the next chunk by LDS-DMA (this stream's, or the next batch's first) */
                     uint64_t nc = ~0ull;
-                    if (rc + CH < Lend) nc = c + CH;
-                    else if (N.s0 < N.e0 && N.stage == 3u && N.stream) nc = u64of(rdl(N.olo, 0u), rdl(N.ohi, 0u));
-                    if (nc != ~0ull) {
-                        dma_chunk(nc);
+                    uint32_t nl = 0, nlo = 0;
+                    if (rc + CH < Lend) {
+                        nc = c + CH;
+                        nl = Lend - rc - CH;
+                    } else if (N.s0 < N.e0 && N.stage == 3u && N.stream) {
+                        const uint32_t mN = N.e0 - N.s0;
+                        const uint64_t n0 = u64of(rdl(N.olo, 0u), rdl(N.ohi, 0u));
+                        nc = n0 & ~127ull;
+                        nlo = (uint32_t)(n0 - nc);
+                        nl = rdl(N.olo, mN) - (uint32_t)n0 + nlo;
+                    }
+                    if (nc != ~0ull && nl != nlo) {
+                        dma_chunk(nc, nlo, nl);
                         pf_at = nc;
                     } else {
                         pf_at = ~0ull;
@@ -537,6 +607,11 @@ __global__ __launch_bounds__(256) void flow(agnes_tally_args a, uint32_t lds_per
                     rset = wave_or(rb);
                 }
                 uint32_t lv0 = 0, lv1 = 0; /* levels 0..3, byte s & 3 of unit s >> 2 */
+                /* (State machine) quorums crossed before each unit: bit 0 / 2 the prevote nil or
+                 * value one at State.round (P1 is then behind the unit A / B), bit 1 / 3 a precommit
+                 * value one (C behind it) -- the sums only grow, so a unit's first candidate is
+                 * the instance's first exactly when its bit is clear */
+                uint32_t cf = 0;
                 while (rset) {
                     const uint32_t r = (uint32_t)__builtin_ctz(rset);
                     rset &= rset - 1u;
@@ -624,6 +699,22 @@ __global__ __launch_bounds__(256) void flow(agnes_tally_args a, uint32_t lds_per
                         if (s < 4u) l0 |= l << bs;
                         else l1 |= l << bs;
                     }
+                    if (SM) {
+                        /* unit A: its running sums before the lane exceed q2 <=> the threshold on the
+                         * lane prefix is negative; unit B (same instance): the prefix through vote 3
+                         * exceeds it; a split lane's unit B starts its instance (nothing before) */
+                        const bool eA_ = R1 || r == recA.w, eB_ = R1 || r == recB.w;
+                        const uint32_t p3vp = (uint32_t)P3 & 0xFFFFu, p3np = (uint32_t)P3 >> 16;
+                        const uint32_t p3vc = (uint32_t)(P3 >> 32) & 0xFFFFu;
+                        const int32_t tvp = (int32_t)(uint32_t)TVa, tnp = (int32_t)(uint32_t)TNa;
+                        const int32_t tvc = (int32_t)(uint32_t)(TVa >> 32);
+                        cf |= (eA_ && (tvp < 0 || tnp < 0)) ? 1u : 0u;
+                        cf |= tvc < 0 ? 2u : 0u;
+                        if (!split) {
+                            cf |= (eB_ && ((int32_t)p3vp > tvp || (int32_t)p3np > tnp)) ? 4u : 0u;
+                            cf |= (int32_t)p3vc > tvc ? 8u : 0u;
+                        }
+                    }
                     lv0 |= l0 & rm0;
                     lv1 |= l1 & rm1;
                     if (lastc) { /* the last segment's executors after the chunk (lane 0 writes) */
@@ -653,87 +744,91 @@ __global__ __launch_bounds__(256) void flow(agnes_tally_args a, uint32_t lds_per
                 if (SM) {
                     uint32_t* const rA = itab + RECW * kA;
                     uint32_t* const rB = itab + RECW * kB;
-                    const uint2 eA = *reinterpret_cast<const uint2*>(rA + R_EQ); /* State.round bytes, valid-from-start */
-                    const uint2 eB = *reinterpret_cast<const uint2*>(rB + R_EQ);
+                    /* State.round bytes, valid-from-start, P1, C */
+                    const uint4 eA = *reinterpret_cast<const uint4*>(rA + R_SMASK); /* smask, eq, vall, step */
+                    const uint4 eB = *reinterpret_cast<const uint4*>(rB + R_SMASK);
                     /* the roles of a unit's votes its step keeps; all but the commit one only at
                      * State.round (state_machine.rs:184-211) */
                     auto roles = [&](uint32_t smask, uint32_t eq, uint32_t r4, uint32_t c4, bool act) -> uint32_t {
-                        const uint32_t eqb = mark_bytes(zero_marks(r4 ^ eq));
+                        /* one round (R1): every vote is of round 0 */
+                        const uint32_t eqb = R1 ? (eq == 0u ? 0xFFFFFFFFu : 0u) : mark_bytes(zero_marks(r4 ^ eq));
                         const uint32_t x = __builtin_amdgcn_perm(XT_HI, XT_LO, c4 & 0x07070707u) & smask &
                                            (eqb | (X_C * 0x01010101u));
                         return act ? x : 0u;
                     };
-                    const uint32_t x0 = roles(recA.w, eA.x, r8[0], c0, actA), x1 = roles(recB.w, eB.x, r8[1], c1, actB);
+                    const uint32_t x0 = roles(eA.x, eA.y, r8[0], c0, actA), x1 = roles(eB.x, eB.y, r8[1], c1, actB);
                     if (ballot((x0 | x1) != 0u)) {
                         const uint32_t pos0 = rc + o8, pos1 = pos0 + 4u; /* stream-relative */
-                        /* the first commit and P1 candidate of each instance: atomic min */
-                        {
-                            const uint32_t cb0 = x0 & (X_C * 0x01010101u), cb1 = x1 & (X_C * 0x01010101u);
-                            const uint32_t pb0 = x0 & (X_P1 * 0x01010101u), pb1 = x1 & (X_P1 * 0x01010101u);
-                            if (cb0) atomicMin(rA + R_C, pos0 + ((uint32_t)__builtin_ctz(cb0) >> 3));
-                            if (pb0) atomicMin(rA + R_P1, pos0 + ((uint32_t)__builtin_ctz(pb0) >> 3));
-                            if (cb1) atomicMin(rB + R_C, pos1 + ((uint32_t)__builtin_ctz(cb1) >> 3));
-                            if (pb1) atomicMin(rB + R_P1, pos1 + ((uint32_t)__builtin_ctz(pb1) >> 3));
-                        }
-                        __builtin_amdgcn_wave_barrier();
-                        const uint2 pcA = *reinterpret_cast<const uint2*>(rA + R_P1);
-                        const uint2 pcB = *reinterpret_cast<const uint2*>(rB + R_P1);
-                        /* messages of one unit (4 votes at pos), branch-free; lo_bytes(d) = 0xFF
-                         * in the bytes below d, d clamped to 0..4 */
-                        auto lo_bytes = [](int32_t d) -> uint32_t {
-                            const uint32_t k = (uint32_t)min(max(d, 0), 4);
-                            return (uint32_t)((0xFFFFFFFFull << (8u * k)) >> 32);
+                        /* P1 / C relative to each unit: behind it (-1) when its quorum was crossed
+                         * before the unit, else the unit's first candidate byte (4: none).  The
+                         * Prevote step ends at P1 or at C, whichever comes first (a P1 after the
+                         * commit never happens); the unit holding the instance's P1 / C records it. */
+                        auto geom = [&](uint32_t x, uint32_t crossedP, uint32_t crossedC, uint32_t pos, uint32_t* rk,
+                                        int32_t& dP, int32_t& dC, bool& p1ok) {
+                            const uint32_t pm = x & (X_P1 * 0x01010101u), cm = x & (X_C * 0x01010101u);
+                            const int32_t bP = pm ? (int32_t)((uint32_t)__builtin_ctz(pm) >> 3) : 4;
+                            const int32_t bC = cm ? (int32_t)((uint32_t)__builtin_ctz(cm) >> 3) : 4;
+                            dC = crossedC ? -1 : bC;
+                            const int32_t p = crossedP ? -1 : bP;
+                            p1ok = p < dC;
+                            dP = p1ok ? p : dC;
+                            if (!crossedC && bC < 4) rk[R_C] = pos + (uint32_t)bC;
+                            if (!crossedP && p1ok && bP < 4) rk[R_P1] = pos + (uint32_t)bP;
                         };
-                        auto unit = [&](uint32_t x, uint32_t pos, uint2 pc, uint32_t vall, uint32_t nnb, uint32_t& atP,
-                                        uint32_t& atC, uint32_t& vc) -> uint32_t {
-                            const uint32_t p1 = pc.x, cc = pc.y;
-                            /* (a P1 after the commit never happens: then the Prevote step ends at C) */
-                            const bool p1ok = p1 < cc;
-                            const int32_t dC = cc == NONE ? 4 : (int32_t)(cc - pos);
-                            const int32_t dP = p1ok ? (int32_t)(p1 - pos) : dC;
-                            const uint32_t alive = lo_bytes(dC), pre = lo_bytes(dP);
-                            atP = p1ok ? lo_bytes(dP + 1) ^ pre : 0u; /* the P1 vote's byte */
-                            atC = lo_bytes(dC + 1) ^ alive; /* the commit vote's byte */
-                            /* TimeoutPrevote before P1 (:196), TimeoutPrecommit before C (:208);
-                             * precommit(r, v) / (r, None) at P1 (:197-198); Decision at C (:211) */
-                            uint32_t msg = (x & ((pre & (X_TP * 0x01010101u)) | (alive & (X_TC * 0x01010101u)))) << 2;
-                            msg |= atP & ((AGNES_VMSG_PRECOMMIT_NIL << AGNES_CODE_MSG_SHIFT) * 0x01010101u +
-                                          (x & (X_PV * 0x01010101u)));
-                            msg |= atC & ((AGNES_VMSG_DECISION << AGNES_CODE_MSG_SHIFT) * 0x01010101u);
-                            /* valid: non-nil PolkaValues at State.round from P1 on (or from the
-                             * start, entering in Precommit), before C (:198, :202) */
+                        /* (an earlier chunk's P1 / C: in the record -- a round absent from this
+                         * chunk has no crossing bit) */
+                        const uint2 qA = *reinterpret_cast<const uint2*>(rA + R_P1);
+                        const uint2 qB = *reinterpret_cast<const uint2*>(rB + R_P1);
+                        int32_t dPA, dCA, dPB, dCB;
+                        bool okA, okB;
+                        geom(x0, (cf & 1u) | (qA.x != NONE ? 1u : 0u), (cf & 2u) | (qA.y != NONE ? 1u : 0u), pos0, rA,
+                             dPA, dCA, okA);
+                        geom(x1, (cf & 4u) | (qB.x != NONE ? 1u : 0u), (cf & 8u) | (qB.y != NONE ? 1u : 0u), pos1, rB,
+                             dPB, dCB, okB);
+                        const uint32_t nn0 = ~mark_bytes(nb0 << 3), nn1 = ~mark_bytes(nb1 << 3); /* non-nil votes */
+                        /* TimeoutPrevote before P1 (:196), TimeoutPrecommit before C (:208); valid:
+                         * non-nil PolkaValues at State.round from P1 on (or from the start, entering
+                         * in Precommit), before C (:198, :202) */
+                        auto base_msg = [&](uint32_t x, uint32_t pre, uint32_t alive, uint32_t vall, uint32_t nnb,
+                                            uint32_t& vc) -> uint32_t {
                             vc = x & alive & (~pre | vall) & nnb & (X_PV * 0x01010101u);
-                            return msg;
+                            return (x & ((pre & (X_TP * 0x01010101u)) | (alive & (X_TC * 0x01010101u)))) << 2;
                         };
-                        uint32_t aP0, aC0, v0, aP1, aC1, v1;
-                        c0 |= unit(x0, pos0, pcA, eA.y, ~mark_bytes(nb0 << 3), aP0, aC0, v0);
-                        c1 |= unit(x1, pos1, pcB, eB.y, ~mark_bytes(nb1 << 3), aP1, aC1, v1);
+                        uint32_t v0, v1, aP0 = 0, aC0 = 0, aP1 = 0, aC1 = 0;
+                        const bool inA = (uint32_t)dPA < 4u || (uint32_t)dCA < 4u;
+                        const bool inB = (uint32_t)dPB < 4u || (uint32_t)dCB < 4u;
+                        if (!ballot(inA || inB)) { /* no P1 or C inside any unit: whole-unit masks */
+                            c0 |= base_msg(x0, dPA >= 4 ? 0xFFFFFFFFu : 0u, dCA >= 4 ? 0xFFFFFFFFu : 0u, eA.z, nn0, v0);
+                            c1 |= base_msg(x1, dPB >= 4 ? 0xFFFFFFFFu : 0u, dCB >= 4 ? 0xFFFFFFFFu : 0u, eB.z, nn1, v1);
+                        } else {
+                            /* lo_bytes(d) = 0xFF in the bytes below d, d clamped to 0..4 */
+                            auto lo_bytes = [](int32_t d) -> uint32_t {
+                                const uint32_t k = (uint32_t)min(max(d, 0), 4);
+                                return (uint32_t)((0xFFFFFFFFull << (8u * k)) >> 32);
+                            };
+                            auto unit = [&](uint32_t x, int32_t dP, int32_t dC, bool p1ok, uint32_t vall, uint32_t nnb,
+                                            uint32_t& atP, uint32_t& atC, uint32_t& vc) -> uint32_t {
+                                const uint32_t alive = lo_bytes(dC), pre = lo_bytes(dP);
+                                atP = p1ok ? lo_bytes(dP + 1) ^ pre : 0u; /* the P1 vote's byte */
+                                atC = lo_bytes(dC + 1) ^ alive;         /* the commit vote's byte */
+                                /* precommit(r, v) / (r, None) at P1 (:197-198); Decision at C (:211) */
+                                uint32_t msg = base_msg(x, pre, alive, vall, nnb, vc);
+                                msg |= atP & ((AGNES_VMSG_PRECOMMIT_NIL << AGNES_CODE_MSG_SHIFT) * 0x01010101u +
+                                              (x & (X_PV * 0x01010101u)));
+                                msg |= atC & ((AGNES_VMSG_DECISION << AGNES_CODE_MSG_SHIFT) * 0x01010101u);
+                                return msg;
+                            };
+                            c0 |= unit(x0, dPA, dCA, okA, eA.z, nn0, aP0, aC0, v0);
+                            c1 |= unit(x1, dPB, dCB, okB, eB.z, nn1, aP1, aC1, v1);
+                        }
                         const uint32_t lk0 = aP0 & (x0 << 3) & 0x80808080u, lk1 = aP1 & (x1 << 3) & 0x80808080u;
                         if (ballot((lk0 | lk1 | aC0 | aC1 | v0 | v1) != 0u)) { /* the few lanes with a State write */
-                            auto vat = [&](uint32_t h, uint32_t b) { /* value of vote b of unit h */
-                                const uint32_t* const v = value + 4u * h;
-                                return b == 0u ? v[0] : (b == 1u ? v[1] : (b == 2u ? v[2] : v[3]));
-                            };
-                            if (lk0) { rA[R_LOCK] = vat(0u, (uint32_t)__builtin_ctz(lk0) >> 3); rA[R_DF] |= F_LOCK; }
-                            if (lk1) { rB[R_LOCK] = vat(1u, (uint32_t)__builtin_ctz(lk1) >> 3); rB[R_DF] |= F_LOCK; }
-                            if (aC0) {
-                                const uint32_t b = (uint32_t)__builtin_ctz(aC0) >> 3;
-                                rA[R_DEC] = vat(0u, b);
-                                rA[R_DF] = (rA[R_DF] & F_LOCK) | ((r8[0] >> (8u * b)) & 0xFFu);
-                            }
-                            if (aC1) {
-                                const uint32_t b = (uint32_t)__builtin_ctz(aC1) >> 3;
-                                rB[R_DEC] = vat(1u, b);
-                                rB[R_DF] = (rB[R_DF] & F_LOCK) | ((r8[1] >> (8u * b)) & 0xFFu);
-                            }
-                            if (v0) {
-                                const uint32_t b = (31u - (uint32_t)__builtin_clz(v0)) >> 3;
-                                atomicMax(vtab + kA, ((unsigned long long)(pos0 + b + 1u) << 32) | vat(0u, b));
-                            }
-                            if (v1) {
-                                const uint32_t b = (31u - (uint32_t)__builtin_clz(v1)) >> 3;
-                                atomicMax(vtab + kB, ((unsigned long long)(pos1 + b + 1u) << 32) | vat(1u, b));
-                            }
+                            if (lk0) atomicOr(rA + R_DF, F_LOCK);
+                            if (lk1) atomicOr(rB + R_DF, F_LOCK);
+                            if (aC0) atomicOr(rA + R_DF, (r8[0] >> (8u * ((uint32_t)__builtin_ctz(aC0) >> 3))) & 0xFFu);
+                            if (aC1) atomicOr(rB + R_DF, (r8[1] >> (8u * ((uint32_t)__builtin_ctz(aC1) >> 3))) & 0xFFu);
+                            if (v0) atomicMax(vtab + kA, pos0 + ((31u - (uint32_t)__builtin_clz(v0)) >> 3) + 1u);
+                            if (v1) atomicMax(vtab + kB, pos1 + ((31u - (uint32_t)__builtin_clz(v1)) >> 3) + 1u);
                         }
                     }
                 }
@@ -741,33 +836,26 @@ __global__ __launch_bounds__(256) void flow(agnes_tally_args a, uint32_t lds_per
                 /* codes (deferred) */
                 dc0 = c0;
                 dc1 = c1;
-                dc_act = actB ? 2u : (actA ? 1u : 0u);
+                dc_act = (actA ? 1u : 0u) | (actB ? 2u : 0u);
                 dc_at = c;
                 __builtin_amdgcn_wave_barrier();
             }
         }
-        /* batch end: the records into the staged States, the States out, then the next batch */
-        if (SM && m) {
-            if (smf) dma_wait(); /* no chunk ran: the staged States are still in flight */
-        }
-        if (SM && m && H.stream) { /* (a walk-list batch's States are the walk kernel's) */
-            if (!smf && lane < m) {
-                const uint32_t* const rk = itab + RECW * lane;
-                uint32_t* const sp = reinterpret_cast<uint32_t*>(sbh + 64u * lane);
-                const uint32_t p1 = rk[R_P1], cc = rk[R_C], df = rk[R_DF];
-                const uint64_t vd = vtab[lane];
-                const uint32_t step = cc != NONE ? (uint32_t)AGNES_STEP_COMMIT
-                                                 : (p1 < cc ? (uint32_t)AGNES_STEP_PRECOMMIT : rk[R_STEP]);
-                uint32_t fl = (sp[13] & ~0xFFu) | step;
-                if ((df & F_LOCK) && p1 < cc) { sp[4] = sp[2]; sp[5] = sp[3]; sp[10] = rk[R_LOCK]; fl |= 1u << 8; }
-                if (vd) { sp[6] = sp[2]; sp[7] = sp[3]; sp[11] = (uint32_t)vd; fl |= 1u << 16; }
-                if (cc != NONE) { sp[8] = df & 0xFFu; sp[9] = 0u; sp[12] = rk[R_DEC]; fl |= 1u << 24; }
-                sp[13] = fl;
-            }
-            __builtin_amdgcn_wave_barrier();
-            if (lane < 4u * m) {
-                const uint4 v = *reinterpret_cast<const uint4*>(sbh + o16);
-                reinterpret_cast<uint4*>(a.states + H.s0)[lane] = v;
+        /* batch end: the States out (a walk-list batch's are the walk kernel's) */
+        if (SM && (m || pend_m)) {
+            if (smf || pend_m) dma_wait(); /* no chunk ran: staged States / pending values in flight */
+            if (pend_m) finalize();        /* the batch before, when this one ran no chunk */
+            if (m && H.stream) {
+                if (smf) { /* no vote: the States as they came */
+                    if (lane < 4u * m)
+                        reinterpret_cast<uint4*>(a.states + H.s0)[lane] = *reinterpret_cast<const uint4*>(sbh + o16);
+                } else { /* the values the records' positions name requested; the States
+                          * written at the next chunk's top (behind its DMA wait) */
+                    dma_values(m, u64of(rdl(H.olo, 0u), rdl(H.ohi, 0u)) & ~127ull, spar); /* positions from Sa */
+                    pend_m = m;
+                    pend_s0 = H.s0;
+                    pend_par = spar;
+                }
             }
         }
         if (N.s0 >= N.e0) break;
@@ -781,6 +869,10 @@ __global__ __launch_bounds__(256) void flow(agnes_tally_args a, uint32_t lds_per
         range_of(rdl(tq, 0u), N.s0, N.e0); /* the batch after, grabbed one batch ago */
         if (lane == 0) tq = atomicAdd(ctr, 1u);
         hdr1(N);
+    }
+    if (SM && pend_m) {
+        dma_wait();
+        finalize();
     }
     flush();
     const uint32_t nb = rdl(scan(bad), 63u);

@@ -7,6 +7,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <initializer_list>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); return 1; } } while (0)
 
@@ -108,8 +109,8 @@ static float timeit(K k, int blocks, size_t lds, int reps, A... args) {
 }
 
 template <int D, int VAL>
-static void run(Cols c, const char* name) {
-    for (int wpc : {8, 12, 16}) {
+static void run(Cols c, const char* name, std::initializer_list<int> wpcs = {8, 12, 16}) {
+    for (int wpc : wpcs) {
         /* LDS per wave so that wpc waves fit a CU (4 waves per block) */
         const uint32_t lpw = (160u * 1024u / wpc) & ~15u;
         if (lpw < D * SLOT) continue;
@@ -127,11 +128,15 @@ int main() {
     CK(hipMemset((void*)c.inst, 1, n * 4)); CK(hipMemset((void*)c.value, 2, n * 4)); CK(hipMemset((void*)c.val, 3, n * 4));
     CK(hipMemset((void*)c.round, 4, n)); CK(hipMemset((void*)c.type, 5, n));
     c.n = n;
-    run<1, 0>(c, "ring1");
-    run<1, 320>(c, "ring1");
-    run<1, 640>(c, "ring1");
-    run<2, 0>(c, "ring2");
-    run<2, 320>(c, "ring2");
-    run<2, 640>(c, "ring2");
+    run<1, 0>(c, "ring1", {16});
+    run<1, 320>(c, "ring1", {12, 16});
+    /* every chunk 4 votes off the 128-vote (u8 column line) alignment */
+    Cols m = c;
+    m.inst += 4; m.value += 4; m.val += 4; m.round += 4; m.type += 4; m.out += 4; m.n -= 512;
+    run<1, 0>(m, "ring1 mis4", {16});
+    run<1, 320>(m, "ring1 mis4", {12, 16});
+    m = c;
+    m.inst += 32; m.value += 32; m.val += 32; m.round += 32; m.type += 32; m.out += 32; m.n -= 512;
+    run<1, 320>(m, "ring1 mis32", {12, 16});
     return 0;
 }
