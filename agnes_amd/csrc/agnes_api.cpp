@@ -30,6 +30,8 @@ struct agnes_ctx {
     uint32_t n_vals = 0;
     unsigned long long* d_err = nullptr;
     hipStream_t last_stream = nullptr;
+    bool used = false;               /* a call has enqueued work on last_stream */
+    hipEvent_t order_ev = nullptr;   /* orders a call on another stream after it */
     bool all_fast = false;     /* every set inside the u32 fast domain */
     uint32_t* d_list = nullptr; /* [list_cap] deferred instances, [list_cap] walk list, then
                                    AGNES_QUEUE_WORDS counters (agnes_internal.h) */
@@ -51,6 +53,27 @@ int status_of(hipError_t e) {
     do {                                             \
         hipError_t e_ = (expr);                      \
         if (e_ != hipSuccess) return status_of(e_);  \
+    } while (0)
+
+/* The ctx scratch (queue counters, deferred / walk lists, the invalid counter, the
+ * edge-scan scratch) is shared by every call: a call on a different stream than
+ * the previous one waits for that stream's work first (one event), so calls on
+ * one ctx never overlap (include/agnes.h, agnes_ctx). */
+int order_stream(agnes_ctx* c, hipStream_t st) {
+    if (c->used && c->last_stream != st) {
+        if (!c->order_ev) AGNES_TRY(hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming));
+        AGNES_TRY(hipEventRecord(c->order_ev, c->last_stream));
+        AGNES_TRY(hipStreamWaitEvent(st, c->order_ev, 0));
+    }
+    c->last_stream = st;
+    c->used = true;
+    return AGNES_OK;
+}
+
+#define AGNES_ORDER(c, st)                          \
+    do {                                            \
+        const int o_ = order_stream((c), (st));     \
+        if (o_ != AGNES_OK) return o_;              \
     } while (0)
 
 void free_power(agnes_ctx* c) {
@@ -208,6 +231,7 @@ void agnes_ctx_destroy(agnes_ctx* c) {
     if (c->d_err) (void)hipFree(c->d_err);
     if (c->d_list) (void)hipFree(c->d_list);
     if (c->d_scan) (void)hipFree(c->d_scan);
+    if (c->order_ev) (void)hipEventDestroy(c->order_ev);
     delete c;
 }
 
@@ -273,6 +297,7 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     const int64_t lpw = agnes_lds_bytes_per_wave(cfg, c->n_vals);
     if (lpw < 0) return (int)lpw;
     AGNES_TRY(hipSetDevice(c->device));
+    AGNES_ORDER(c, st);
     const bool wide_all = b->weight != nullptr || carry != nullptr || !sets_fast;
     if (!wide_all && (!c->d_list || c->list_cap < b->n_instances)) {
         /* [list_cap] deferred instances | [list_cap] walk list | counters */
@@ -329,7 +354,6 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     } else {
         a.epoch_shift = 31;
     }
-    c->last_stream = st;
     return status_of(agnes_launch_tally(&a, cfg->mode, c->num_cus, wide_all, st));
 }
 
@@ -373,14 +397,16 @@ int agnes_apply_events(agnes_ctx* c, agnes_state* states, uint32_t n, const uint
                        const agnes_event* ev, agnes_message* msgs, uint32_t flags, void* stream) {
     if (!c || (n && (!states || !off))) return AGNES_E_INVALID;
     AGNES_TRY(hipSetDevice(c->device));
-    c->last_stream = (hipStream_t)stream;
+    AGNES_ORDER(c, (hipStream_t)stream);
     return status_of(agnes_launch_apply_events(states, n, off, ev, msgs, flags, (hipStream_t)stream));
 }
 
 /* ---------------- edge-triggered summary ---------------- */
 
 static bool edges_args_ok(const agnes_config* cfg, const agnes_vote_batch* b, const uint8_t* codes) {
+    /* the walks read codes, round and type 4 bytes at a time */
     return cfg && b && cfg->max_rounds >= 1u && cfg->max_rounds <= 256u &&
+           !(((uintptr_t)codes | (uintptr_t)b->round | (uintptr_t)b->type) & 3u) &&
            (b->n_instances == 0 || (b->offsets && (b->n_votes == 0 || (codes && b->round && b->type))));
 }
 
@@ -388,7 +414,7 @@ int agnes_edge_offsets(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_b
                        uint64_t* offsets, void* stream) {
     if (!c || !offsets || !edges_args_ok(cfg, b, codes)) return AGNES_E_INVALID;
     AGNES_TRY(hipSetDevice(c->device));
-    c->last_stream = (hipStream_t)stream;
+    AGNES_ORDER(c, (hipStream_t)stream);
     const uint64_t words = agnes_edges_scratch_words(b->n_instances);
     if (words > c->scan_cap) {
         if (c->d_scan) AGNES_TRY(hipFree(c->d_scan));
@@ -403,9 +429,9 @@ int agnes_edge_offsets(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_b
 
 int agnes_edges(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, const uint8_t* codes,
                 const uint64_t* offsets, agnes_edge* out, void* stream) {
-    if (!c || !offsets || !out || !edges_args_ok(cfg, b, codes)) return AGNES_E_INVALID;
+    if (!c || !offsets || !out || !edges_args_ok(cfg, b, codes) || ((uintptr_t)out & 15u)) return AGNES_E_INVALID;
     AGNES_TRY(hipSetDevice(c->device));
-    c->last_stream = (hipStream_t)stream;
+    AGNES_ORDER(c, (hipStream_t)stream);
     return status_of(agnes_launch_edges(b, codes, cfg->max_rounds, const_cast<uint64_t*>(offsets), out,
                                         nullptr, (hipStream_t)stream));
 }
@@ -418,7 +444,7 @@ static int dedup_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     if (b->n_votes && (!b->instance || !b->round || !b->type || !b->validator)) return AGNES_E_INVALID;
     if (c->n_vals == 0) return AGNES_E_INVALID; /* no power table: no validator range */
     AGNES_TRY(hipSetDevice(c->device));
-    c->last_stream = (hipStream_t)stream;
+    AGNES_ORDER(c, (hipStream_t)stream);
     if (b->instance_set) return AGNES_E_UNSUPPORTED; /* one instance: its set is reserved % n_sets */
     const uint32_t set = cfg->reserved % (c->n_sets ? c->n_sets : 1u);
     return status_of(agnes_launch_dedup(b, cfg->reserved, cfg->max_rounds, c->n_vals, set < c->n_sets, base,
@@ -440,7 +466,7 @@ int agnes_dedup_mask(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_bat
 int agnes_dedup_reject(agnes_ctx* c, const uint8_t* type_masked, uint64_t n, uint8_t* codes, void* stream) {
     if (!c || (n && (!type_masked || !codes))) return AGNES_E_INVALID;
     AGNES_TRY(hipSetDevice(c->device));
-    c->last_stream = (hipStream_t)stream;
+    AGNES_ORDER(c, (hipStream_t)stream);
     return status_of(agnes_launch_dedup_reject(type_masked, n, codes, (hipStream_t)stream));
 }
 
@@ -466,7 +492,7 @@ int agnes_gen_votes_device(agnes_ctx* c, const agnes_gen_params* p, const uint64
     if (!c || !agnes_gen_params_ok(p) || !d_offsets) return AGNES_E_INVALID;
     if (n_votes && (!instance || !round || !type || !value || !validator)) return AGNES_E_INVALID;
     AGNES_TRY(hipSetDevice(c->device));
-    c->last_stream = (hipStream_t)stream;
+    AGNES_ORDER(c, (hipStream_t)stream);
     return status_of(agnes_launch_gen(p, d_offsets, n_votes, instance, round, type, value,
                                       validator, (hipStream_t)stream));
 }

@@ -63,8 +63,12 @@ __global__ __launch_bounds__(256) void mask_kernel(DedupArgs a, const unsigned l
         uint64_t key;
         const uint32_t t = a.type[j];
         uint32_t o;
+        /* a vote failing the DEDUP checks is INVALID in the one-stream DEDUP tally
+         * (oracle orc_tally: DEDUP needs its validator); 0xFF makes the carried
+         * REFERENCE tally reject it too, whatever column it reads (a weight column
+         * does not look at the validator) */
         if (valid_key(a, j, key)) o = first[key] == a.base + j ? t : AGNES_TYPE_MASKED;
-        else o = t == AGNES_TYPE_MASKED ? 0xFFu : t; /* stays invalid, never taken for masked */
+        else o = 0xFFu;
         type_out[j] = (uint8_t)o;
     }
 }

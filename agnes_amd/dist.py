@@ -10,6 +10,7 @@ Collectives are used only for
 """
 from __future__ import annotations
 
+import time
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
@@ -114,6 +115,49 @@ def gather_decisions(local: np.ndarray, group=None) -> np.ndarray:
     return np.concatenate(parts) if parts else local
 
 
+def gather_edges(recs: torch.Tensor, group=None) -> list:
+    """all_gather of every rank's edge records (agnes_edge, 16 B each; any device
+    tensor whose rows are records), variable length: the counts first, then the
+    records padded to the longest; returns the list of each rank's records (rows
+    in rank order), on recs' device.  One rank: [recs]."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return [recs]
+    world = dist.get_world_size(group)
+    flat = recs.contiguous().view(torch.uint8).reshape(recs.shape[0], -1) if recs.numel() else \
+        torch.zeros((0, 16), dtype=torch.uint8, device=recs.device)
+    rec = flat.shape[1]
+    n = torch.tensor([flat.shape[0]], dtype=torch.int64, device=recs.device)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    counts = [int(c.item()) for c in ns]
+    m = max(counts)
+    buf = torch.zeros((m, rec), dtype=torch.uint8, device=recs.device)
+    buf[: flat.shape[0]] = flat
+    bufs = [torch.zeros_like(buf) for _ in range(world)]
+    dist.all_gather(bufs, buf, group=group)
+    return [bufs[r][: counts[r]] for r in range(world)]
+
+
+def gather_edges_timed(recs: torch.Tensor, group=None, reps: int = 3) -> dict:
+    """gather_edges timed over ranks (best of reps, max over ranks): the bench's
+    exchange step of emitted records, outside its timed region."""
+    best = None
+    for _ in range(reps):
+        dist.barrier(group=group)
+        if recs.is_cuda:
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        parts = gather_edges(recs, group)
+        if recs.is_cuda:
+            torch.cuda.synchronize()
+        dt = max_over_ranks(time.perf_counter() - t0, group)
+        best = dt if best is None else min(best, dt)
+    total = sum(int(p.shape[0]) for p in parts)
+    nbytes = sum(int(p.numel()) for p in parts)
+    return {"records": total, "bytes": nbytes, "ms": best * 1e3,
+            "GBps": nbytes / best / 1e9 if best > 0 else None}
+
+
 # ---------------------------------------------------------------------------
 # C5: ONE instance split into contiguous stream slices (SURVEY.md §8(e)) — the
 # path's one real exchange step.  is_quorum (round_votes.rs:31-33) needs the
@@ -216,7 +260,7 @@ INT64_MAX = (1 << 63) - 1
 
 def tally_one_instance_dedup(tally_carried, dedup_first, dedup_mask, dedup_reject, n_votes: int,
                              n_vals: int, cfg: abi.Config, n_segments: int, device, base: int = 0,
-                             inst_id: int = 0, group=None, offsets=None):
+                             group=None, offsets=None):
     """C5 in DEDUP mode ("DEDUP mode adds an all-reduce(min) on
     first_index").  A vote's slice cannot see whether an earlier slice (or rank)
     already counted its (round, type, validator), so the first vote of every key is
@@ -233,7 +277,9 @@ def tally_one_instance_dedup(tally_carried, dedup_first, dedup_mask, dedup_rejec
       dedup_reject()            the masked votes' codes -> REJECTED.
     The codes equal tallying the whole instance as one DEDUP stream (offsets: as
     tally_one_instance's, for a HIP-graph capture).  A stream
-    continued across calls would also carry `first`; not offered here."""
+    continued across calls would also carry `first`; not offered here.
+    The instance's id is cfg.reserved, for the DEDUP checks and for the carried
+    tally alike (one source)."""
     first = torch.full((2 * cfg.max_rounds * n_vals,), INT64_MAX, dtype=torch.int64, device=device)
     dedup_first(base, first)
     if dist.is_initialized() and dist.get_world_size(group) > 1:
@@ -242,7 +288,7 @@ def tally_one_instance_dedup(tally_carried, dedup_first, dedup_mask, dedup_rejec
         first = t.to(device)
     dedup_mask(base, first)
     ref = abi.Config(abi.MODE_REFERENCE, cfg.flags, cfg.max_rounds, cfg.reserved)
-    out = tally_one_instance(tally_carried, n_votes, ref, n_segments, device, inst_id, group,
+    out = tally_one_instance(tally_carried, n_votes, ref, n_segments, device, cfg.reserved, group,
                              offsets=offsets)
     dedup_reject()
     return out

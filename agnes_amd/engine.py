@@ -217,6 +217,8 @@ class Engine:
         sh = _stream_handle(stream)
         check(self.lib.agnes_edge_offsets(self.ctx, C.byref(cfg), C.byref(b), _ptr(codes), _ptr(offs), sh),
               "agnes_edge_offsets")
+        if stream is not None:  # the total is read on torch's current stream
+            stream.synchronize()
         n = int(offs[-1].item())
         out = torch.empty((max(n, 1), 16), dtype=torch.uint8, device=self.device)
         if n:

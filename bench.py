@@ -28,13 +28,15 @@ sys.path.insert(0, ROOT)
 
 from agnes_amd import abi  # noqa: E402
 from agnes_amd import dist as adist  # noqa: E402
-from agnes_amd.engine import Engine, states_to_device  # noqa: E402
+from agnes_amd.engine import Engine, states_to_device, states_to_host  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
 BYTES_PER_VOTE = 15            # 14 B canonical SoA in + 1 B code out
 # algorithmic bytes per vote of each engine kernel (names: agnes_kernel_times)
 KERNEL_BYTES_PER_VOTE = {
-    "tally_stream": 15,  # instance, value, validator u32 + round, type u8 in; code u8 out
+    "flow": 15,          # instance, value, validator u32 + round, type u8 in; code u8 out
+    "sweep": 15,
+    "tally_stream": 15,
     "tally_fast": 15,
     "tally_wide": 15,
     "apply_codes": 2,    # code + round u8 in (messages written back sparsely)
@@ -42,6 +44,9 @@ KERNEL_BYTES_PER_VOTE = {
     "dedup_mask": 11,    # the same in, the masked type u8 out
 }
 KERNEL_SYMBOLS = {
+    "flow": "agnes::flow::flow<PC, SM, R1>",
+    "sweep": "agnes::sweep::sweep<PC, SM, false>",
+    "sweep_walk": "agnes::sweep::sweep<PC, SM, true>",
     "tally_stream": "agnes::stream::tally_stream<false, *>",
     "tally_fast": "agnes::fast::tally_fast<...>",
     "tally_wide": "agnes::tally_kernel<true, ...>",
@@ -89,43 +94,66 @@ def start_states(n: int) -> np.ndarray:
     return abi.new_states(n, height=1, step=abi.STEP_PREVOTE, round_=0)
 
 
-def measured_traffic(config: str, kernel: str):
-    """HBM bytes per launch of the tally kernel for this workload, from the
-    rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this same command committed under
-    profiles/ (tools/pmc_traffic.py applies the gfx950 corrections); None if the
-    workload has not been profiled."""
+def measured_traffic(config: str):
+    """HBM bytes per launch of each engine kernel for this workload, from the
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this same command committed under
+    profiles/ (tools/pmc_traffic.py applies the gfx950 corrections of
+    MI355X_MICROARCH.md: FETCH_SIZE x2, WRITE_SIZE as is): {kernel: record}."""
     try:
         with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
-            rec = json.load(f).get(config)
+            rec = json.load(f).get(config) or {}
     except (OSError, ValueError):
-        return None
-    # only a record of the kernel that is measured now
-    return rec if rec and kernel in rec.get("kernel_match", "") else None
+        return {}
+    return rec.get("kernels", {})
+
+
+def host_cpu() -> dict:
+    """The host the CPU baseline ran on: model, logical CPUs, the CPUs this process
+    may run on, and the cgroup CPU quota when one is set."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        quota = None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    return {"model": model, "nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
+            "cgroup_cpu_quota": quota}
 
 
 def cpu_baseline(eng, cfg, batch, power, states0, set_of_instance):
-    """The checker (oracle/, scalar C, pthreads over instances) on the same batch."""
+    """The checker (oracle/, scalar C, one pthread per CPU this process may use,
+    over instances) on the same batch; best of 5."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as ol  # test infrastructure: the CPU baseline leg only
     h = batch.to_host()
     n_inst = len(h["offsets"]) - 1
-    # bounded sample: up to 1M instances (the whole c2 batch: ~2e8 votes, a few s per core-pass)
+    # bounded sample: up to 1M instances (the whole c2 batch: ~2e8 votes)
     limit = min(n_inst, 1_000_000)
     off = h["offsets"][: limit + 1]
     nv = int(off[-1])
     hb = ol.HostBatch(h["instance"][:nv], h["round"][:nv], h["type"][:nv], h["value"][:nv],
                       h["validator"][:nv], off.copy(), set_of_instance[:limit].copy())
-    threads = max(1, min(16, os.cpu_count() or 1))
+    cpu = host_cpu()
+    threads = max(1, cpu["affinity"])
     best = None
-    for _ in range(3):
+    for _ in range(5):
         t0 = time.perf_counter()
-        codes, _, _ = ol.tally(cfg, hb, power, None, states0[:limit], threads=threads)
+        codes, st, _ = ol.tally(cfg, hb, power, None, states0[:limit], threads=threads)
         dt = time.perf_counter() - t0
         best = dt if best is None else min(best, dt)
     return {"value": nv / best, "unit": "votes/s", "cores": threads, "kind": "port",
+            "host": cpu,
             "sample": f"first {limit} instances ({nv} votes) of the same batch, "
-                      f"oracle/agnes_oracle.c orc_tally_mt, best of 3",
-            "codes_prefix": codes}
+                      f"oracle/agnes_oracle.c orc_tally_mt on {threads} threads, best of 5",
+            "codes_prefix": codes, "states_prefix": st}
 
 
 def edge_summary(eng, cfg, batch, codes, reps: int = 5):
@@ -144,7 +172,7 @@ def edge_summary(eng, cfg, batch, codes, reps: int = 5):
     eng.kernel_timing(False)
     nv, ni, ne = batch.n_votes, batch.n_instances, recs.shape[0]
     ab = {"edge_count": 3 * nv + 24 * ni, "edge_scan": 16 * ni, "edge_emit": 3 * nv + 16 * ni + 16 * ne}
-    res = {"edges": int(ne), "edges_per_vote": ne / max(nv, 1)}
+    res = {"edges": int(ne), "edges_per_vote": ne / max(nv, 1), "_records": recs}
     for name, (launches, total) in kt.items():
         avg = total / max(launches, 1)
         res[name] = {"avg_ms": avg, "algorithmic_bytes": ab.get(name),
@@ -159,7 +187,6 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--check", action="store_true", help="compare the CPU sample with the GPU codes")
     args = ap.parse_args()
 
     rank, world, local = adist.env()
@@ -190,13 +217,9 @@ def main():
     codes = torch.empty(batch.n_votes, dtype=torch.uint8, device=eng.device)
     torch.cuda.synchronize()
 
-    def step(ev_pair=None):
-        states.copy_(st0, non_blocking=True)          # State::new for this batch of heights
-        if ev_pair:
-            ev_pair[0].record(stream)
-        eng.tally(cfg, batch, codes, states, stream)
-        if ev_pair:
-            ev_pair[1].record(stream)
+    def step():
+        # State::new for this batch of heights (st0, read in place) -> the States after it
+        eng.tally_states(cfg, batch, codes, st0, states)
 
     for _ in range(args.warmup):
         step()
@@ -204,41 +227,70 @@ def main():
     if eng.last_error_count() != 0:
         raise SystemExit("bench batch has invalid votes")
 
+    # per-kernel times: K eager steps with HIP events around every engine launch (on
+    # the launch stream); the roofline's kernel duration comes from here
+    eng.kernel_timing(True)
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    ktimes = eng.kernel_times()
+    eng.kernel_timing(False)
+
+    # the step (queue reset + flow + walk + list launches) captured once in a HIP graph
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        step()
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        step()
+    g.replay()
+    torch.cuda.synchronize()
+
     pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
              for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    eng.kernel_timing(True)  # HIP events around each engine kernel, on `stream`
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(pairs[k])
+        pairs[k][0].record(stream)
+        g.replay()
+        pairs[k][1].record(stream)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    ktimes = eng.kernel_times()
-    eng.kernel_timing(False)
     elapsed = adist.max_over_ranks(elapsed)
     total_votes_step = adist.sum_over_ranks(batch.n_votes)
     if world > 1:
         dist.barrier()
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in pairs]))
+    step_gpu_ms = float(np.mean([a.elapsed_time(b) for a, b in pairs]))
+
+    edges = edge_summary(eng, cfg, batch, codes)
+    if world > 1:  # every rank's edge records to every rank (RCCL), outside the timed region
+        edges["all_gather"] = adist.gather_edges_timed(edges.pop("_records"))
+    else:
+        edges.pop("_records")
 
     if rank == 0:
         ms_per_step = elapsed * 1e3 / args.steps
         value = total_votes_step * args.steps / elapsed
+        traffic = measured_traffic(args.config)
         # per-kernel: launches, average ms, algorithmic bytes per launch
         kernels = {}
         for name, (launches, total) in ktimes.items():
             avg = total / max(launches, 1)
             ab = KERNEL_BYTES_PER_VOTE.get(name, 0) * batch.n_votes
+            t = traffic.get(name)
             kernels[name] = {"launches": launches, "avg_ms": avg, "algorithmic_bytes": ab,
-                             "GBps": ab / (avg * 1e-3) / 1e9 if ab and avg > 0 else None}
+                             "GBps": ab / (avg * 1e-3) / 1e9 if ab and avg > 0 else None,
+                             "traffic": t.get("traffic_bytes") if t else None}
         dom = max(kernels, key=lambda k: kernels[k]["avg_ms"] * kernels[k]["launches"])
         dom_ms = kernels[dom]["avg_ms"]
-        achieved = KERNEL_BYTES_PER_VOTE[dom] * batch.n_votes / (dom_ms * 1e-3) / 1e9
-        step_kernel_ms = sum(v["avg_ms"] * v["launches"] for v in kernels.values()) / args.steps
-        step_achieved = BYTES_PER_VOTE * batch.n_votes / (step_kernel_ms * 1e-3) / 1e9
-        traffic = measured_traffic(args.config, dom)
+        ab_dom = KERNEL_BYTES_PER_VOTE[dom] * batch.n_votes
+        achieved = ab_dom / (dom_ms * 1e-3) / 1e9
+        path_achieved = BYTES_PER_VOTE * batch.n_votes / (ms_per_step * 1e-3) / 1e9
+        td = traffic.get(dom)
         out = {
             "metric": "votes_tallied_per_sec",
             "value": value,
@@ -256,30 +308,33 @@ def main():
                        "instances_per_gpu": p.n_instances, "validators": p.n_vals,
                        "votes_per_gpu_per_step": batch.n_votes,
                        "mode": "DEDUP" if w["mode"] else "REFERENCE",
-                       "flags": w["flags"], "parallelism": f"instance-sharded x{world}"},
-            "kernel_ms": kernel_ms,
+                       "flags": w["flags"], "parallelism": f"instance-sharded x{world}",
+                       "hip_graph": True},
+            "kernel_ms": step_gpu_ms,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic.get("traffic_bytes") if traffic else None,
-                         "traffic_source": traffic.get("sources") if traffic else None,
+                         "traffic": td.get("traffic_bytes") if td else None,
+                         "traffic_source": td.get("sources") if td else None,
                          "kernel": KERNEL_SYMBOLS.get(dom, dom),
                          "kernel_avg_ms": dom_ms,
                          "bytes_per_vote": KERNEL_BYTES_PER_VOTE[dom],
-                         "algorithmic_bytes": KERNEL_BYTES_PER_VOTE[dom] * batch.n_votes},
-            # the whole hot path (every kernel agnes_tally enqueues) against the same
-            # peak: 15 B/vote algorithmic over the summed kernel time of one step
-            "step_roofline": {"achieved": step_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                              "frac": step_achieved / HBM_PEAK_GBS, "kernel_ms": step_kernel_ms},
+                         "algorithmic_bytes": ab_dom,
+                         # the whole step (every launch agnes_tally_states enqueues, wall
+                         # clock of the timed region) at 15 B/vote against the same peak
+                         "path_achieved": path_achieved,
+                         "path_frac": path_achieved / HBM_PEAK_GBS},
             "kernels": kernels,
+            "edge_summary": edges,
         }
-        out["edge_summary"] = edge_summary(eng, cfg, batch, codes)
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(eng, cfg, batch, power, st0_host, set_of)
-            prefix = cb.pop("codes_prefix")
-            if args.check:
-                g = codes[: len(prefix)].cpu().numpy()
-                # the bench codes come from the LAST step; states were reset each step
-                out["cpu_check_equal"] = bool(np.array_equal(g, prefix))
+            cprefix = cb.pop("codes_prefix")
+            sprefix = cb.pop("states_prefix")
+            # the GPU's codes and States of the last step against the checker's
+            g_codes = codes[: len(cprefix)].cpu().numpy()
+            g_states = states_to_host(states)[: len(sprefix)]
+            out["cpu_check_equal"] = bool(np.array_equal(g_codes, cprefix)
+                                          and np.array_equal(g_states.view(np.uint8), sprefix.view(np.uint8)))
             out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -349,7 +404,7 @@ def bench_one_instance(args, w, eng, rank, world):
             step()
         torch.cuda.current_stream().wait_stream(side)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, stream=side):
             step()
         run = g.replay
         run()
@@ -411,8 +466,7 @@ def bench_one_instance(args, w, eng, rank, world):
             out["cpu_baseline"] = {"value": n / best, "unit": "votes/s", "cores": 1, "kind": "port",
                                    "sample": f"the whole instance ({n} votes), oracle/agnes_oracle.c "
                                              "orc_tally (one instance: one thread), best of 3"}
-            if args.check:
-                out["cpu_check_equal"] = bool(np.array_equal(codes[: hi - lo].cpu().numpy(), want))
+            out["cpu_check_equal"] = bool(np.array_equal(codes[: hi - lo].cpu().numpy(), want[lo:hi]))
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -280,6 +280,13 @@ int agnes_state_apply(const agnes_state* in, int64_t round, const agnes_event* e
 /* ---------------------------------------------------------------------------
  * Batch engine (the hot path).  All array pointers passed to agnes_tally /
  * agnes_apply_events are DEVICE pointers on the context's device.
+ *
+ * Streams: every call is asynchronous on its `stream` (NULL: the default stream).
+ * A context's scratch is shared by its calls, so a call on a different stream
+ * than the context's previous call first waits for that stream (an event): the
+ * calls of one context never overlap.  Use one context per concurrent stream for
+ * overlap; while capturing a HIP graph, make the call before the capture on the
+ * capture stream too (a wait on another stream's event cannot be captured).
  * ------------------------------------------------------------------------- */
 typedef struct agnes_ctx agnes_ctx;
 

@@ -101,7 +101,7 @@ class DedupFake:
         idx = base + np.arange(len(key), dtype=np.int64)
         dup = ok.copy()
         dup[ok] = first[key[ok]] != idx[ok]
-        t[~ok & (t == self.MASKED)] = 0xFF
+        t[~ok] = 0xFF  # invalid in the one-stream DEDUP tally: rejected by the carried tally too
         t[dup] = self.MASKED
         return t
 

@@ -7,6 +7,7 @@ CPU tests drive agnes_amd/dist.py tally_one_instance with the carried-tally
 stand-in (tests/carried_fake.py), including a world_size-2 gloo run; the GPU tests
 drive it on agnes_tally_carried through the C ABI.
 """
+import copy
 import dataclasses
 import os
 import socket
@@ -193,6 +194,28 @@ def test_split_instance_dedup_equals_whole_cpu(segments):
     assert np.array_equal(codes, want)
 
 
+def _with_instance_id(hb, iid):
+    """The same single-instance stream with every vote naming instance `iid` (the
+    split path's id, cfg.reserved; the one-stream reference keeps id 0 = its
+    segment index)."""
+    h = copy.copy(hb)
+    h.instance = np.full_like(np.asarray(hb.instance), iid)
+    return h
+
+
+@pytest.mark.parametrize("segments", [1, 5])
+def test_split_instance_dedup_nonzero_instance_id_cpu(segments):
+    """the DEDUP checks and the carried tally take the instance id from one place
+    (cfg.reserved): a nonzero id still masks every duplicate"""
+    hb, power, cfg = _dedup_instance(seed=17, n_vals=200)
+    hb.validator[[5, 50, 500]] = 10 ** 6  # out of range: INVALID in the one-stream DEDUP tally
+    want, _, _ = ol.tally(cfg, hb, power)
+    cfg9 = abi.config(abi.MODE_DEDUP, 0, cfg.max_rounds, 9)
+    codes, _, _ = _cpu_dedup_slice(_with_instance_id(hb, 9), power, cfg9, 0, hb.n_votes, segments)
+    assert (want == abi.CODE_REJECTED).any() and (want == abi.CODE_INVALID).any()
+    assert np.array_equal(codes, want)
+
+
 def _dedup_worker(rank, world, port, q):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, HERE)
@@ -326,9 +349,27 @@ def test_gpu_split_instance_dedup(eng, segments, n_vals, R):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("weights", [False, True])
+def test_gpu_split_instance_dedup_id_weights(eng, weights):
+    """nonzero instance id (cfg.reserved, one source) and an explicit weight column
+    with out-of-range validators: the split DEDUP codes equal the one-stream DEDUP
+    tally (a vote failing the DEDUP checks is INVALID there, whatever the weights)"""
+    hb, power, cfg = _dedup_instance(seed=23, n_vals=3000, R=2)
+    if weights:
+        hb.weight = np.random.default_rng(5).integers(1, 5000, hb.n_votes).astype(np.int64)
+    hb.validator[[3, 40, 400, hb.n_votes - 1]] = 10 ** 6
+    want, _, _ = ol.tally(cfg, hb, power)
+    cfg7 = abi.config(abi.MODE_DEDUP, 0, cfg.max_rounds, 7)
+    got = _gpu_dedup_run(eng, _with_instance_id(hb, 7), power, cfg7, 9)
+    assert (want == abi.CODE_INVALID).sum() >= 4
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
 def test_gpu_dedup_slices_with_bases(eng):
     """Two slices with their global bases, first-seen tables min-combined (the
-    all_reduce), give the whole stream's mask — and invalid votes are never masked."""
+    all_reduce), give the whole stream's mask — and a vote failing the DEDUP checks
+    is never masked: it is made invalid (0xFF) for the carried tally."""
     from agnes_amd.engine import DeviceBatch
     hb, power, cfg = _dedup_instance(seed=13, n_vals=4000, R=2)
     hb.type[7] = 5
@@ -360,7 +401,7 @@ def test_gpu_dedup_slices_with_bases(eng):
     torch.cuda.synchronize()
     assert torch.equal(torch.cat([ta, tb]), tw)
     t = tw.cpu().numpy()
-    assert t[7] == 5 and t[11] == 0xFF and t[19] == hb.type[19]
+    assert t[7] == 0xFF and t[11] == 0xFF and t[19] == 0xFF  # failing the DEDUP checks: always invalid
     dd = DedupFake(*power.shape)
     f = np.full(K, ad.INT64_MAX, np.int64)
     dd.first(cfg, hb, 0, f)

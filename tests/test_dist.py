@@ -51,10 +51,20 @@ def _worker(rank, world, port, strong, q):
         codes, st, _ = ol.tally(cfg, hb, power, None, st0)
         local_dec = ad.decisions(st, sh.base)
         all_dec = ad.gather_decisions(local_dec)
+        # the bench's exchange of emitted edge records (variable length per rank)
+        import torch
+        _, recs = ol.edges(cfg, hb, codes)
+        recs = recs.copy()
+        recs["instance"] += sh.base                       # global instance / vote indices
+        recs["vote"] += int(ol.gen_offsets(abi.gen_params(seed=0xA6E5, **dict(
+            GEN, n_instances=sh.base + sh.params.n_instances)))[sh.base]) if sh.base else 0
+        parts = ad.gather_edges(torch.from_numpy(recs.view(np.uint8).reshape(len(recs), -1).copy()))
+        edges_all = b"".join(bytes(p_.numpy().tobytes()) for p_ in parts)
+        timed = ad.gather_edges_timed(torch.from_numpy(recs.view(np.uint8).reshape(len(recs), -1).copy()))
         total_votes = ad.sum_over_ranks(hb.n_votes)
         tmax = ad.max_over_ranks(float(rank + 1))
         q.put((rank, sh.base, sh.params.n_instances, codes.tobytes(), st.tobytes(),
-               all_dec.tobytes(), total_votes, tmax))
+               all_dec.tobytes(), total_votes, tmax, edges_all, timed["records"]))
     finally:
         dist.destroy_process_group()
 
@@ -97,7 +107,10 @@ def test_sharded_equals_whole(strong):
     assert b"".join(r[4] for r in res) == st.tobytes()
     # collectives
     dec = ad.decisions(st, 0)
+    _, erecs = ol.edges(cfg, hb, codes)
     for r in res:
+        assert r[8] == erecs.tobytes()        # all_gather of edge records, rank order
+        assert r[9] == len(erecs)
         assert r[5] == dec.tobytes()          # all_gather of decision summaries, rank order
         assert r[6] == hb.n_votes              # sum of per-rank votes
         assert r[7] == 2.0                     # max over ranks
