@@ -18,7 +18,7 @@ import sys
 # engine kernel name (agnes_kernel_times) -> substring of the demangled symbol
 KERNELS = {
     "flow": "agnes::flow::flow<",
-    "sweep": "agnes::sweep::sweep<",
+    "sweep_walk": "agnes::sweep::sweep<",
     "tally_fast": "agnes::fast::tally_fast<",
     "apply_codes": "agnes::apply::apply_codes<",
     "tally_list": "agnes::tally_kernel<",
