@@ -8,7 +8,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 NIL = 0xFFFFFFFF
 
 OK, E_INVALID, E_UNSUPPORTED, E_DEVICE, E_NOMEM, E_NODEVICE = 0, -1, -2, -3, -4, -5
@@ -130,6 +130,9 @@ MESSAGE_DTYPE = np.dtype([("round", "<i8"), ("pol_round", "<i8"), ("value", "<u4
 EDGE_DTYPE = np.dtype([("vote", "<u8"), ("instance", "<u4"), ("round", "u1"), ("type", "u1"),
                        ("code", "u1"), ("prev", "u1")])
 assert EDGE_DTYPE.itemsize == 16
+VOTE_EVENT_DTYPE = np.dtype([("vote", "<u8"), ("instance", "<u4"), ("value", "<u4"), ("round", "u1"),
+                             ("kind", "u1"), ("message", "u1"), ("pad", "u1", (5,))])  # agnes_vote_event
+assert VOTE_EVENT_DTYPE.itemsize == 24
 VOTE_COUNT_DTYPE = np.dtype([("value_w", "<i8"), ("nil_w", "<i8"), ("value", "<u4"),
                              ("reserved", "<u4")])  # agnes_vote_count
 assert STATE_DTYPE.itemsize == 64 and EVENT_DTYPE.itemsize == 24 and MESSAGE_DTYPE.itemsize == 24

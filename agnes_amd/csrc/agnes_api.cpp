@@ -436,6 +436,36 @@ int agnes_edges(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b
                                         nullptr, (hipStream_t)stream));
 }
 
+/* ---------------- event stream ---------------- */
+
+int agnes_event_offsets(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, const uint8_t* codes,
+                        uint64_t* offsets, void* stream) {
+    if (!c || !offsets || !edges_args_ok(cfg, b, codes)) return AGNES_E_INVALID;
+    AGNES_TRY(hipSetDevice(c->device));
+    AGNES_ORDER(c, (hipStream_t)stream);
+    const uint64_t words = agnes_edges_scratch_words(b->n_instances);
+    if (words > c->scan_cap) {
+        if (c->d_scan) AGNES_TRY(hipFree(c->d_scan));
+        c->d_scan = nullptr;
+        c->scan_cap = 0;
+        AGNES_TRY(hipMalloc(&c->d_scan, words * sizeof(uint64_t)));
+        c->scan_cap = words;
+    }
+    return status_of(agnes_launch_events(b, codes, cfg->max_rounds, offsets, nullptr, c->d_scan,
+                                         (hipStream_t)stream));
+}
+
+int agnes_events(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, const uint8_t* codes,
+                 const uint64_t* offsets, agnes_vote_event* out, void* stream) {
+    if (!c || !offsets || !out || !edges_args_ok(cfg, b, codes) || ((uintptr_t)out & 7u)) return AGNES_E_INVALID;
+    if (cfg->max_rounds > 64u) return AGNES_E_UNSUPPORTED; /* the value slots of a lane's executors in LDS */
+    if (b->n_votes && (!b->value || ((uintptr_t)b->value & 3u))) return AGNES_E_INVALID;
+    AGNES_TRY(hipSetDevice(c->device));
+    AGNES_ORDER(c, (hipStream_t)stream);
+    return status_of(agnes_launch_events(b, codes, cfg->max_rounds, const_cast<uint64_t*>(offsets), out,
+                                         nullptr, (hipStream_t)stream));
+}
+
 /* ---------------- DEDUP for a split instance ---------------- */
 
 static int dedup_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint64_t base,

@@ -179,6 +179,18 @@ __global__ __launch_bounds__(SCAN_T) void scan_add(uint64_t* x, uint64_t n, cons
 
 /* ------------------------------------------------------------------ */
 
+hipError_t agnes_launch_offsets_scan(uint64_t* offs, uint32_t n, uint64_t* scratch, hipStream_t st) {
+    using namespace agnes::edges;
+    const uint64_t nb = agnes_edges_scratch_words(n);
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(scan_blocks, dim3((uint32_t)nb), dim3(SCAN_T), 0, st, offs + 1, (uint64_t)n, scratch);
+    if (nb > 1u) {
+        hipLaunchKernelGGL(scan_parts, dim3(1), dim3(SCAN_T), 0, st, scratch, nb);
+        hipLaunchKernelGGL(scan_add, dim3((uint32_t)nb), dim3(SCAN_T), 0, st, offs + 1, (uint64_t)n, scratch);
+    }
+    return hipGetLastError();
+}
+
 uint64_t agnes_edges_scratch_words(uint32_t n_instances) {
     return ((uint64_t)n_instances + agnes::edges::SCAN_BLK - 1u) / agnes::edges::SCAN_BLK;
 }
@@ -201,14 +213,8 @@ hipError_t agnes_launch_edges(const agnes_vote_batch* vb, const uint8_t* codes, 
             if (w16) hipLaunchKernelGGL((edge_walk<false, EW>), grid, blk, lds, st, a);
             else hipLaunchKernelGGL((edge_walk<false, 4u>), grid, blk, lds, st, a);
         }
-        const uint64_t nb = agnes_edges_scratch_words(n);
         AgnesKt kt("edge_scan", st);
-        hipLaunchKernelGGL(scan_blocks, dim3((uint32_t)nb), dim3(SCAN_T), 0, st, offs + 1, (uint64_t)n, scratch);
-        if (nb > 1u) {
-            hipLaunchKernelGGL(scan_parts, dim3(1), dim3(SCAN_T), 0, st, scratch, nb);
-            hipLaunchKernelGGL(scan_add, dim3((uint32_t)nb), dim3(SCAN_T), 0, st, offs + 1, (uint64_t)n, scratch);
-        }
-        return hipGetLastError();
+        return agnes_launch_offsets_scan(offs, n, scratch, st);
     }
     if (n == 0) return hipSuccess;
     AgnesKt kt("edge_emit", st);

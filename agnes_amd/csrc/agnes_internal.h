@@ -100,6 +100,11 @@ hipError_t agnes_launch_gen(const agnes_gen_params* p, const uint64_t* d_offsets
 /* the edge summary (agnes_edges.hip): out == nullptr -> count pass + exclusive scan of
  * offs (scratch: agnes_edges_scratch_words u64); else the emit pass */
 uint64_t agnes_edges_scratch_words(uint32_t n_instances);
+/* offs[1..n] := inclusive scan of the per-instance counts (offs[0] = 0 left as is) */
+hipError_t agnes_launch_offsets_scan(uint64_t* offs, uint32_t n, uint64_t* scratch, hipStream_t stream);
+/* the event stream (agnes_events.hip): out == nullptr -> count pass + scan, else emit */
+hipError_t agnes_launch_events(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds,
+                               uint64_t* offs, agnes_vote_event* out, uint64_t* scratch, hipStream_t stream);
 hipError_t agnes_launch_edges(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds,
                               uint64_t* offs, agnes_edge* out, uint64_t* scratch, hipStream_t stream);
 

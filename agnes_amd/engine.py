@@ -226,6 +226,26 @@ class Engine:
                                        _ptr(out), sh), "agnes_edges")
         return offs, out[:n]
 
+    def events(self, cfg: abi.Config, batch: DeviceBatch, codes: torch.Tensor, stream=None):
+        """The event stream of coded votes (agnes_event_offsets + agnes_events).
+        Returns (offsets int64 [n_instances + 1], records uint8 [n_events, 24] — view
+        the host copy as abi.VOTE_EVENT_DTYPE).  Reads the total back (one sync)."""
+        if codes.dtype != torch.uint8 or codes.numel() < batch.n_votes:
+            raise ValueError("codes must be a uint8 tensor of n_votes")
+        b = batch.c()
+        offs = torch.empty(batch.n_instances + 1, dtype=torch.int64, device=self.device)
+        sh = _stream_handle(stream)
+        check(self.lib.agnes_event_offsets(self.ctx, C.byref(cfg), C.byref(b), _ptr(codes), _ptr(offs), sh),
+              "agnes_event_offsets")
+        if stream is not None:  # the total is read on torch's current stream
+            stream.synchronize()
+        n = int(offs[-1].item())
+        out = torch.empty((max(n, 1), 24), dtype=torch.uint8, device=self.device)
+        if n:
+            check(self.lib.agnes_events(self.ctx, C.byref(cfg), C.byref(b), _ptr(codes), _ptr(offs),
+                                        _ptr(out), sh), "agnes_events")
+        return offs, out[:n]
+
     # -- synthetic workloads ------------------------------------------------
     def gen_offsets(self, p: abi.GenParams) -> np.ndarray:
         off = np.zeros(p.n_instances + 1, dtype=np.uint64)

@@ -180,6 +180,32 @@ def edge_summary(eng, cfg, batch, codes, reps: int = 5):
     return res
 
 
+def event_stream(eng, cfg, batch, codes, reps: int = 3):
+    """The stream-compacted event output (agnes_event_offsets + agnes_events: every
+    Some(Event) with its payload) of the last step's codes, timed OUTSIDE the
+    bench's timed region.  Algorithmic bytes: the count walk reads the codes (1 B /
+    vote) and writes 8 B per instance; the emit walk reads code, round, type and
+    value (7 B / vote) and writes 24 B per event."""
+    eng.events(cfg, batch, codes)
+    torch.cuda.synchronize()
+    eng.kernel_timing(True)
+    for _ in range(reps):
+        offs, recs = eng.events(cfg, batch, codes)
+    torch.cuda.synchronize()
+    kt = eng.kernel_times()
+    eng.kernel_timing(False)
+    nv, ni, ne = batch.n_votes, batch.n_instances, recs.shape[0]
+    ab = {"event_count": nv + 16 * ni, "event_scan": 16 * ni, "event_emit": 7 * nv + 8 * ni + 24 * ne}
+    res = {"events": int(ne), "events_per_vote": ne / max(nv, 1)}
+    for name, (launches, total) in kt.items():
+        avg = total / max(launches, 1)
+        res[name] = {"avg_ms": avg, "algorithmic_bytes": ab.get(name),
+                     "GBps": ab[name] / (avg * 1e-3) / 1e9 if name in ab and avg > 0 else None}
+    del offs, recs
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -266,6 +292,7 @@ def main():
         dist.barrier()
     step_gpu_ms = float(np.mean([a.elapsed_time(b) for a, b in pairs]))
 
+    events = event_stream(eng, cfg, batch, codes)
     edges = edge_summary(eng, cfg, batch, codes)
     if world > 1:  # every rank's edge records to every rank (RCCL), outside the timed region
         edges["all_gather"] = adist.gather_edges_timed(edges.pop("_records"))
@@ -325,6 +352,7 @@ def main():
                          "path_frac": path_achieved / HBM_PEAK_GBS},
             "kernels": kernels,
             "edge_summary": edges,
+            "event_stream": events,
         }
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(eng, cfg, batch, power, st0_host, set_of)

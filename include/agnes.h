@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AGNES_ABI_VERSION 2u
+#define AGNES_ABI_VERSION 3u
 
 /* ---------------------------------------------------------------------------
  * Status codes (reference never fails, state_machine.rs:212; these report
@@ -416,6 +416,38 @@ int agnes_edge_offsets(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote
  * batch and codes. */
 int agnes_edges(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
                 const uint8_t* codes, const uint64_t* offsets, agnes_edge* out, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Event stream: every Some(Event) the batch's votes produced, stream-compacted
+ * (instance then vote order) with the Event's payload — what a caller of
+ * VoteExecutor::apply (vote_executor.rs:20-23, via ConsensusExecutor::apply_vote,
+ * consensus_executor.rs:61-69) collects vote by vote.  A vote gives at most two
+ * records: a RoundSkip (code bit AGNES_CODE_SKIP, applied first) and its
+ * VoteExecutor event (code bits 0..2 = 1..5).  The Value a PolkaValue /
+ * PrecommitValue carries is its VoteCount's value slot after the vote (the last
+ * non-nil value added, round_votes.rs:50-54, 58-59): the walk follows the value
+ * column over the votes the tally added (every code but INVALID and REJECTED),
+ * from VoteCount::new's Value{} (0) — executors carried from an earlier call
+ * (agnes_tally_carried) are not followed.
+ * ------------------------------------------------------------------------- */
+typedef struct agnes_vote_event {
+    uint64_t vote;     /* index of the vote in the batch                             */
+    uint32_t instance; /* the vote's segment (instance) index                        */
+    uint32_t value;    /* PolkaValue / PrecommitValue: the Value; else AGNES_NIL      */
+    uint8_t round;     /* Vote.round                                                 */
+    uint8_t kind;      /* AGNES_EV_POLKA_ANY .. AGNES_EV_PRECOMMIT_VALUE, _ROUND_SKIP */
+    uint8_t message;   /* the vote's State machine message nibble (code >> 4)        */
+    uint8_t pad[5];
+} agnes_vote_event;
+
+/* Pass 1: offsets (DEVICE, n_instances + 1): exclusive offsets of each instance's
+ * records, offsets[n_instances] = the total.  codes as agnes_tally left them. */
+int agnes_event_offsets(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
+                        const uint8_t* codes, uint64_t* offsets, void* stream);
+/* Pass 2: the records into out (DEVICE, offsets[n_instances] records, 8-B aligned);
+ * reads codes, round, type and value.  max_rounds <= 64. */
+int agnes_events(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
+                 const uint8_t* codes, const uint64_t* offsets, agnes_vote_event* out, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Synthetic workload generator (counter-based splitmix64; identical on host

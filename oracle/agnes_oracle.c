@@ -293,7 +293,7 @@ static int needs_validator(const agnes_config* cfg, const agnes_vote_batch* b) {
 
 static int tally_range(const agnes_config* cfg, const agnes_vote_batch* b, const orc_power* pw,
                        uint8_t* codes, agnes_state* states, uint32_t i0, uint32_t i1,
-                       tally_scratch* sc, uint64_t* n_invalid) {
+                       tally_scratch* sc, uint64_t* n_invalid, uint32_t* labels) {
     const uint32_t R = cfg->max_rounds;
     const uint32_t nv = pw ? pw->n_vals : 0;
     const int dedup = cfg->mode == AGNES_MODE_DEDUP;
@@ -312,6 +312,7 @@ static int tally_range(const agnes_config* cfg, const agnes_vote_batch* b, const
         for (uint64_t j = b->offsets[i]; j < b->offsets[i + 1]; ++j) {
             const uint32_t r = b->round[j], t = b->type[j], val = b->validator[j];
             const uint32_t value = b->value[j];
+            if (labels) labels[j] = AGNES_NIL;
             if (b->instance[j] != i || r >= R || t > 1u || (need_val && (!set_ok || val >= nv)) ||
                 (!b->weight && !set_ok)) {
                 codes[j] = AGNES_CODE_INVALID;
@@ -337,6 +338,7 @@ static int tally_range(const agnes_config* cfg, const agnes_vote_batch* b, const
             uint32_t tv = 0;
             const uint32_t th = orc_vc_add(&sc->cnt[r * 2u + t], value, w, &tv);
             const uint32_t ev = orc_to_event(t, th);
+            if (labels && (ev == AGNES_EV_POLKA_VALUE || ev == AGNES_EV_PRECOMMIT_VALUE)) labels[j] = tv;
             const int skip = skip_on && orc_is_one_third(sc->skip_w[r], total);
             uint8_t code = (uint8_t)(ev_to_code(ev) | (skip ? AGNES_CODE_SKIP : 0u));
             if (st) {
@@ -398,7 +400,7 @@ int orc_tally(const agnes_config* cfg, const agnes_vote_batch* b, const orc_powe
         return AGNES_E_NOMEM;
     }
     uint64_t bad = 0;
-    int rc = tally_range(cfg, b, pw, codes, states, 0, b->n_instances, &sc, &bad);
+    int rc = tally_range(cfg, b, pw, codes, states, 0, b->n_instances, &sc, &bad, NULL);
     scratch_free(&sc);
     if (n_invalid) *n_invalid = bad;
     return rc;
@@ -410,6 +412,7 @@ typedef struct mt_job {
     const orc_power* pw;
     uint8_t* codes;
     agnes_state* states;
+    uint32_t* labels;
     uint32_t i0, i1;
     uint64_t bad;
     int rc;
@@ -422,7 +425,7 @@ static void* mt_run(void* arg) {
     if (!scratch_alloc(&sc, j->cfg->max_rounds, j->pw ? j->pw->n_vals : 0)) {
         j->rc = AGNES_E_NOMEM;
     } else {
-        j->rc = tally_range(j->cfg, j->b, j->pw, j->codes, j->states, j->i0, j->i1, &sc, &j->bad);
+        j->rc = tally_range(j->cfg, j->b, j->pw, j->codes, j->states, j->i0, j->i1, &sc, &j->bad, j->labels);
     }
     scratch_free(&sc);
     return NULL;
@@ -430,6 +433,12 @@ static void* mt_run(void* arg) {
 
 int orc_tally_mt(const agnes_config* cfg, const agnes_vote_batch* b, const orc_power* pw,
                  uint8_t* codes, agnes_state* states, uint64_t* n_invalid, int threads) {
+    return orc_tally_labels(cfg, b, pw, codes, states, n_invalid, NULL, threads);
+}
+
+int orc_tally_labels(const agnes_config* cfg, const agnes_vote_batch* b, const orc_power* pw,
+                     uint8_t* codes, agnes_state* states, uint64_t* n_invalid, uint32_t* labels,
+                     int threads) {
     if (!check_args(cfg, b, codes)) return AGNES_E_INVALID;
     if (threads < 1) threads = 1;
     if ((uint32_t)threads > b->n_instances) threads = b->n_instances ? (int)b->n_instances : 1;
@@ -448,7 +457,7 @@ int orc_tally_mt(const agnes_config* cfg, const agnes_vote_batch* b, const orc_p
         uint32_t end = cur;
         while (end < b->n_instances && b->offsets[end] < target) ++end;
         if (t == threads - 1) end = b->n_instances;
-        jobs[t] = (mt_job){cfg, b, pw, codes, states, cur, end, 0, AGNES_OK};
+        jobs[t] = (mt_job){cfg, b, pw, codes, states, labels, cur, end, 0, AGNES_OK};
         cur = end;
     }
     for (int t = 0; t < threads; ++t) pthread_create(&th[t], NULL, mt_run, &jobs[t]);
@@ -515,6 +524,51 @@ int orc_edges(const agnes_config* cfg, const agnes_vote_batch* b, const uint8_t*
                 ++k;
             }
             level[key] = (uint8_t)nl;
+        }
+        offsets[i + 1] = k;
+    }
+    return AGNES_OK;
+}
+
+/* The event stream (include/agnes.h agnes_vote_event): per instance, in vote
+ * order, the Some(Event)s of ConsensusExecutor::apply_vote (consensus_executor.rs:
+ * 61-69): a RoundSkip first when the vote completed +1/3 of a higher round (the
+ * extension's event, code bit AGNES_CODE_SKIP), then the VoteExecutor event
+ * (vote_executor.rs:20-36, code bits 0..2), whose Value is the one the tally's
+ * VoteCount gave it (labels, orc_tally_labels).  offsets[n+1] always written; out
+ * (NULL: count only) gets the records. */
+int orc_events(const agnes_config* cfg, const agnes_vote_batch* b, const uint8_t* codes,
+               const uint32_t* labels, uint64_t* offsets, agnes_vote_event* out) {
+    static const uint8_t kind_of[8] = {AGNES_EV_NONE, AGNES_EV_POLKA_ANY, AGNES_EV_POLKA_NIL,
+                                       AGNES_EV_POLKA_VALUE, AGNES_EV_PRECOMMIT_ANY,
+                                       AGNES_EV_PRECOMMIT_VALUE, AGNES_EV_NONE, AGNES_EV_NONE};
+    if (!cfg || !b || !offsets || (out && !labels)) return AGNES_E_INVALID;
+    uint64_t k = 0;
+    offsets[0] = 0;
+    for (uint32_t i = 0; i < b->n_instances; ++i) {
+        uint64_t lo = b->offsets[i], hi = b->offsets[i + 1];
+        if (lo > b->n_votes) lo = b->n_votes;
+        if (hi > b->n_votes) hi = b->n_votes;
+        for (uint64_t j = lo; j < hi; ++j) {
+            const uint32_t c = codes[j], ev = c & AGNES_CODE_EVENT_MASK;
+            if (ev == AGNES_CODE_INVALID || ev == AGNES_CODE_REJECTED) continue;
+            for (int pass = 0; pass < 2; ++pass) {
+                const uint32_t kind = pass == 0 ? ((c & AGNES_CODE_SKIP) ? AGNES_EV_ROUND_SKIP : AGNES_EV_NONE)
+                                                : kind_of[ev];
+                if (kind == AGNES_EV_NONE) continue;
+                if (out) {
+                    agnes_vote_event* e = &out[k];
+                    memset(e, 0, sizeof(*e));
+                    e->vote = j;
+                    e->instance = i;
+                    e->value = (kind == AGNES_EV_POLKA_VALUE || kind == AGNES_EV_PRECOMMIT_VALUE) ? labels[j]
+                                                                                              : AGNES_NIL;
+                    e->round = b->round[j];
+                    e->kind = (uint8_t)kind;
+                    e->message = (uint8_t)(c >> AGNES_CODE_MSG_SHIFT);
+                }
+                ++k;
+            }
         }
         offsets[i + 1] = k;
     }

@@ -76,6 +76,16 @@ int orc_tally(const agnes_config* cfg, const agnes_vote_batch* batch, const orc_
 /* same, instances split over `threads` pthreads (CPU baseline) */
 int orc_tally_mt(const agnes_config* cfg, const agnes_vote_batch* batch, const orc_power* pw,
                  uint8_t* codes, agnes_state* states, uint64_t* n_invalid, int threads);
+/* orc_tally_mt that also writes, per vote, the Value its VoteExecutor event
+ * carries (labels[j]: the VoteCount's value slot for PolkaValue / PrecommitValue,
+ * AGNES_NIL otherwise) */
+int orc_tally_labels(const agnes_config* cfg, const agnes_vote_batch* batch, const orc_power* pw,
+                     uint8_t* codes, agnes_state* states, uint64_t* n_invalid, uint32_t* labels,
+                     int threads);
+/* the event stream (agnes_event_offsets + agnes_events) from the tally's codes and
+ * labels: offsets[n_instances + 1]; out NULL = count only */
+int orc_events(const agnes_config* cfg, const agnes_vote_batch* batch, const uint8_t* codes,
+               const uint32_t* labels, uint64_t* offsets, agnes_vote_event* out);
 /* batched State::apply over explicit event lists */
 int orc_apply_events(agnes_state* states, uint32_t n_instances, const uint64_t* ev_offsets,
                      const agnes_event* events, agnes_message* msgs, uint32_t flags);

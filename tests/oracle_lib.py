@@ -56,6 +56,9 @@ def lib():
                                 C.POINTER(OrcPower), P, P, C.POINTER(C.c_uint64)]
         L.orc_tally_mt.argtypes = [C.POINTER(abi.Config), C.POINTER(abi.VoteBatch),
                                    C.POINTER(OrcPower), P, P, C.POINTER(C.c_uint64), C.c_int]
+        L.orc_tally_labels.argtypes = [C.POINTER(abi.Config), C.POINTER(abi.VoteBatch),
+                                       C.POINTER(OrcPower), P, P, C.POINTER(C.c_uint64), P, C.c_int]
+        L.orc_events.argtypes = [C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P]
         L.orc_apply_events.argtypes = [P, C.c_uint32, P, P, P, C.c_uint32]
         L.orc_edges.argtypes = [C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P]
         L.orc_set_totals.argtypes = [P, C.c_uint32, C.c_uint32, P]
@@ -170,6 +173,38 @@ def tally(cfg: abi.Config, b: HostBatch, power: Optional[np.ndarray], totals=Non
     if rc != 0:
         raise RuntimeError(f"orc_tally rc={rc}")
     return codes, st, int(nbad.value)
+
+
+def events(cfg: abi.Config, b: HostBatch, power: Optional[np.ndarray], totals=None, states=None,
+           threads: int = 1):
+    """The tally with the Value each VoteExecutor event carries (orc_tally_labels),
+    then the event stream (orc_events).  Returns (codes, states_out, n_invalid,
+    offsets u64 [n+1], records abi.VOTE_EVENT_DTYPE)."""
+    codes = np.zeros(b.n_votes, dtype=np.uint8)
+    labels = np.zeros(max(b.n_votes, 1), dtype=np.uint32)
+    pw_struct = None
+    if power is not None:
+        power = np.ascontiguousarray(power, dtype=np.int64)
+        if totals is None:
+            totals = set_totals(power)
+        totals = np.ascontiguousarray(totals, dtype=np.int64)
+        pw_struct = OrcPower(_p(power), _p(totals), power.shape[0], power.shape[1])
+    st = None if states is None else np.array(states, dtype=abi.STATE_DTYPE, copy=True)
+    nbad = C.c_uint64(0)
+    cb = b.c()
+    pw_ref = C.byref(pw_struct) if pw_struct is not None else None
+    rc = lib().orc_tally_labels(C.byref(cfg), C.byref(cb), pw_ref, _p(codes), _p(st), C.byref(nbad),
+                                _p(labels), max(1, threads))
+    if rc != 0:
+        raise RuntimeError(f"orc_tally_labels rc={rc}")
+    offs = np.zeros(b.n_instances + 1, dtype=np.uint64)
+    rc = lib().orc_events(C.byref(cfg), C.byref(cb), _p(codes), _p(labels), _p(offs), None)
+    assert rc == 0, rc
+    out = np.zeros(int(offs[-1]), dtype=abi.VOTE_EVENT_DTYPE)
+    rc = lib().orc_events(C.byref(cfg), C.byref(cb), _p(codes), _p(labels), _p(offs),
+                          _p(out) if len(out) else None)
+    assert rc == 0, rc
+    return codes, st, int(nbad.value), offs, out
 
 
 def edges(cfg: abi.Config, b: HostBatch, codes: np.ndarray):
