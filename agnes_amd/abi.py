@@ -130,6 +130,7 @@ MESSAGE_DTYPE = np.dtype([("round", "<i8"), ("pol_round", "<i8"), ("value", "<u4
 EDGE_DTYPE = np.dtype([("vote", "<u8"), ("instance", "<u4"), ("round", "u1"), ("type", "u1"),
                        ("code", "u1"), ("prev", "u1")])
 assert EDGE_DTYPE.itemsize == 16
+FOLD_RESET, FOLD_APPLY, FOLD_CARRY_ZERO_NONE, FOLD_ZERO_LABELS, FOLD_TOTAL_ZERO_LABELS = 0x1, 0x2, 0x4, 0x8, 0x10
 VOTE_EVENT_DTYPE = np.dtype([("vote", "<u8"), ("instance", "<u4"), ("value", "<u4"), ("round", "u1"),
                              ("kind", "u1"), ("message", "u1"), ("pad", "u1", (5,))])  # agnes_vote_event
 assert VOTE_EVENT_DTYPE.itemsize == 24

@@ -436,6 +436,16 @@ int agnes_edges(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b
                                         nullptr, (hipStream_t)stream));
 }
 
+/* ---------------- C5: the fold of one instance's slices ---------------- */
+
+int agnes_fold_counts(agnes_ctx* c, agnes_vote_count* counts, uint32_t n_slices, uint32_t keys,
+                      const agnes_vote_count* carry, agnes_vote_count* totals, uint32_t flags, void* stream) {
+    if (!c || (n_slices && keys && !counts) || keys > 512u || (flags & ~0x1Fu)) return AGNES_E_INVALID;
+    AGNES_TRY(hipSetDevice(c->device));
+    AGNES_ORDER(c, (hipStream_t)stream);
+    return status_of(agnes_launch_fold(counts, n_slices, keys, carry, totals, flags, (hipStream_t)stream));
+}
+
 /* ---------------- event stream ---------------- */
 
 int agnes_event_offsets(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, const uint8_t* codes,

@@ -102,6 +102,10 @@ hipError_t agnes_launch_gen(const agnes_gen_params* p, const uint64_t* d_offsets
 uint64_t agnes_edges_scratch_words(uint32_t n_instances);
 /* offs[1..n] := inclusive scan of the per-instance counts (offs[0] = 0 left as is) */
 hipError_t agnes_launch_offsets_scan(uint64_t* offs, uint32_t n, uint64_t* scratch, hipStream_t stream);
+/* the fold of one instance's slices' VoteCounts (agnes_fold.hip) */
+hipError_t agnes_launch_fold(agnes_vote_count* counts, uint32_t n_slices, uint32_t keys,
+                             const agnes_vote_count* carry, agnes_vote_count* totals, uint32_t flags,
+                             hipStream_t stream);
 /* the event stream (agnes_events.hip): out == nullptr -> count pass + scan, else emit */
 hipError_t agnes_launch_events(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds,
                                uint64_t* offs, agnes_vote_event* out, uint64_t* scratch, hipStream_t stream);

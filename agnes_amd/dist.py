@@ -204,7 +204,7 @@ def fold_counts(w: torch.Tensor, lab: torch.Tensor):
 
 
 def tally_one_instance(tally_carried, n_votes: int, cfg: abi.Config, n_segments: int, device,
-                       inst_id: int = 0, group=None, prior=None, offsets=None):
+                       inst_id: int = 0, group=None, prior=None, offsets=None, fold=None):
     """C5 driver.  This rank holds a contiguous slice (n_votes votes) of ONE
     instance's stream; ranks hold consecutive slices in rank order.  The slice is
     cut into n_segments segments (one wave each) and tallied twice:
@@ -219,6 +219,8 @@ def tally_one_instance(tally_carried, n_votes: int, cfg: abi.Config, n_segments:
     [K]) before this call (a stream continued across calls), None = RoundVotes::new.
     offsets: segment_offsets(n_votes, n_segments) already on `device` (lets a caller
     capture the whole step in a HIP graph).
+    fold: Engine.fold_counts (agnes_fold_counts, HIP): the folds run as one kernel
+    each on the device; None: torch ops (CPU tensors in the tests).
     Returns the instance's (w, label) after every rank's votes."""
     K = 2 * cfg.max_rounds
     if offsets is None:
@@ -228,6 +230,8 @@ def tally_one_instance(tally_carried, n_votes: int, cfg: abi.Config, n_segments:
         off = offsets
         S = off.numel() - 1
     one = abi.Config(cfg.mode, cfg.flags | abi.FLAG_ONE_INSTANCE, cfg.max_rounds, inst_id)
+    if fold is not None:
+        return _tally_one_instance_hip(tally_carried, fold, one, off, S, K, device, group, prior)
     counts = torch.zeros((S, K, 3), dtype=torch.int64, device=device)
     counts[..., 2] = NIL
     tally_carried(one, off, counts)                                    # pass A
@@ -255,12 +259,41 @@ def tally_one_instance(tally_carried, n_votes: int, cfg: abi.Config, n_segments:
     return fin_w, torch.where(fin_lab == NIL, torch.zeros_like(fin_lab), fin_lab)
 
 
+def _tally_one_instance_hip(tally_carried, fold, one, off, S, K, device, group, prior):
+    """tally_one_instance with the folds as agnes_fold_counts launches (no torch
+    kernels between the two carried passes on one GPU)."""
+    counts = torch.empty((S, K, 3), dtype=torch.int64, device=device)
+    fold(counts, flags=abi.FOLD_RESET)                                 # RoundVotes::new per slice
+    tally_carried(one, off, counts)                                    # pass A
+    pr = None
+    if prior is not None:
+        pw, pl = prior
+        pr = torch.cat([pw, pl.unsqueeze(-1)], dim=-1).to(device).contiguous()
+    fin = torch.empty((K, 3), dtype=torch.int64, device=device)
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        mine = torch.empty((K, 3), dtype=torch.int64, device=device)
+        fold(counts, totals=mine)                                      # this slice's total
+        t = mine.to(_device_for(group))
+        parts = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(parts, t, group=group)                         # the exchange step
+        ranks = torch.stack(parts).to(device).contiguous()             # [world, K, 3]
+        fold(ranks, carry=pr, totals=fin,                              # ranks before each rank
+             flags=abi.FOLD_APPLY | abi.FOLD_CARRY_ZERO_NONE | abi.FOLD_TOTAL_ZERO_LABELS)
+        fold(counts, carry=ranks[rank].contiguous(), flags=abi.FOLD_APPLY | abi.FOLD_ZERO_LABELS)
+    else:
+        fold(counts, carry=pr, totals=fin,
+             flags=abi.FOLD_APPLY | abi.FOLD_ZERO_LABELS | abi.FOLD_CARRY_ZERO_NONE | abi.FOLD_TOTAL_ZERO_LABELS)
+    tally_carried(one, off, counts)                                    # pass B
+    return fin[:, :2], fin[:, 2]
+
+
 INT64_MAX = (1 << 63) - 1
 
 
 def tally_one_instance_dedup(tally_carried, dedup_first, dedup_mask, dedup_reject, n_votes: int,
                              n_vals: int, cfg: abi.Config, n_segments: int, device, base: int = 0,
-                             group=None, offsets=None):
+                             group=None, offsets=None, fold=None):
     """C5 in DEDUP mode ("DEDUP mode adds an all-reduce(min) on
     first_index").  A vote's slice cannot see whether an earlier slice (or rank)
     already counted its (round, type, validator), so the first vote of every key is
@@ -289,7 +322,7 @@ def tally_one_instance_dedup(tally_carried, dedup_first, dedup_mask, dedup_rejec
     dedup_mask(base, first)
     ref = abi.Config(abi.MODE_REFERENCE, cfg.flags, cfg.max_rounds, cfg.reserved)
     out = tally_one_instance(tally_carried, n_votes, ref, n_segments, device, cfg.reserved, group,
-                             offsets=offsets)
+                             offsets=offsets, fold=fold)
     dedup_reject()
     return out
 

@@ -156,6 +156,19 @@ class Engine:
         check(self.lib.agnes_tally_carried(self.ctx, C.byref(cfg), C.byref(b), _ptr(codes), _ptr(counts),
                                            _stream_handle(stream)), "agnes_tally_carried")
 
+    def fold_counts(self, counts: torch.Tensor, carry: Optional[torch.Tensor] = None,
+                    totals: Optional[torch.Tensor] = None, flags: int = 0, stream=None):
+        """agnes_fold_counts on counts = contiguous int64 [S, K, 3] (agnes_vote_count
+        records); carry / totals: int64 [K, 3] or None."""
+        if counts.dtype != torch.int64 or not counts.is_contiguous() or counts.dim() != 3:
+            raise ValueError("counts must be a contiguous int64 [S, K, 3] tensor")
+        S, K = counts.shape[0], counts.shape[1]
+        for t in (carry, totals):
+            if t is not None and (t.dtype != torch.int64 or not t.is_contiguous() or t.numel() < 3 * K):
+                raise ValueError("carry / totals must be contiguous int64 [K, 3] tensors")
+        check(self.lib.agnes_fold_counts(self.ctx, _ptr(counts), S, K, _ptr(carry), _ptr(totals), flags,
+                                         _stream_handle(stream)), "agnes_fold_counts")
+
     # -- DEDUP for one instance split over slices (C5) --------------------------
     def dedup_first(self, cfg: abi.Config, batch: DeviceBatch, base: int, first: torch.Tensor, stream=None):
         """agnes_dedup_first: first = int64 [2 * max_rounds * n_vals], INT64_MAX-initialised."""

@@ -406,8 +406,9 @@ def bench_one_instance(args, w, eng, rank, world):
                 tc, lambda base, f: eng.dedup_first(cfg, src, base, f),
                 lambda base, f: eng.dedup_mask(cfg, src, base, f, tmask),
                 lambda: eng.dedup_reject(tmask, codes, hi - lo), hi - lo, p.n_vals, cfg, segs,
-                eng.device, base=lo, offsets=off)
-        return adist.tally_one_instance(tc, hi - lo, cfg, segs, eng.device, 0, None, offsets=off)
+                eng.device, base=lo, offsets=off, fold=eng.fold_counts)
+        return adist.tally_one_instance(tc, hi - lo, cfg, segs, eng.device, 0, None, offsets=off,
+                                        fold=eng.fold_counts)
 
     for _ in range(args.warmup):
         step()
@@ -424,7 +425,7 @@ def bench_one_instance(args, w, eng, rank, world):
     # one GPU: the step is ~20 short launches (two tallies + the folds), so it is
     # captured once in a HIP graph and replayed; over ranks the all_gather stays eager
     run = step
-    graph = world == 1 and not os.environ.get("AGNES_NO_GRAPH")
+    graph = world == 1
     if graph:
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())

@@ -337,6 +337,25 @@ typedef struct agnes_vote_count {
 int agnes_tally_carried(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
                         uint8_t* codes, agnes_vote_count* counts, void* stream);
 
+/* The fold of one instance's slices (C5, agnes_amd/dist.py tally_one_instance):
+ * counts (DEVICE, [n_slices][keys]) hold each slice's partial VoteCounts (value
+ * AGNES_NIL: no value written); partials fold like consecutive add_vote calls
+ * (round_votes.rs:48-56: weights add, wrapping; the later value slot wins).
+ *   AGNES_FOLD_RESET   every record := VoteCount::new with no value (AGNES_NIL)
+ *   AGNES_FOLD_APPLY   every slice := carry (or zero) + the slices before it: the
+ *                      carry-in of the next agnes_tally_carried pass
+ *   totals (or NULL)   [keys] := carry + every slice
+ * carry (DEVICE [keys] or NULL); flags also choose the label conventions:
+ * AGNES_FOLD_CARRY_ZERO_NONE reads a carry label 0 as "none", _ZERO_LABELS /
+ * _TOTAL_ZERO_LABELS write "none" as 0 (VoteCount::new's Value{}). */
+#define AGNES_FOLD_RESET 0x1u
+#define AGNES_FOLD_APPLY 0x2u
+#define AGNES_FOLD_CARRY_ZERO_NONE 0x4u
+#define AGNES_FOLD_ZERO_LABELS 0x8u
+#define AGNES_FOLD_TOTAL_ZERO_LABELS 0x10u
+int agnes_fold_counts(agnes_ctx* ctx, agnes_vote_count* counts, uint32_t n_slices, uint32_t keys,
+                      const agnes_vote_count* carry, agnes_vote_count* totals, uint32_t flags, void* stream);
+
 /* DEDUP for one instance split over slices (C5; agnes_amd/dist.py
  * tally_one_instance_dedup).  The carried tally is REFERENCE only, so the first
  * vote of each (round, type, validator) is found up front:

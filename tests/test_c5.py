@@ -266,20 +266,58 @@ def _gpu_tc(eng, db, codes):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("hip_fold", [False, True])
 @pytest.mark.parametrize("segments,n_vals,R,nil", [(1, 3000, 1, 200), (7, 3000, 2, 200),
                                                    (64, 20000, 1, 200), (300, 20000, 3, 300),
                                                    (33, 5000, 2, 900)])
-def test_gpu_split_instance(eng, segments, n_vals, R, nil):
+def test_gpu_split_instance(eng, segments, n_vals, R, nil, hip_fold):
     from agnes_amd.engine import DeviceBatch
     hb, power, cfg = _instance(seed=11 + segments, n_vals=n_vals, R=R, nil=nil)
     want, _, _ = ol.tally(cfg, hb, power)
     eng.upload_power(power)
     db = DeviceBatch.from_host(hb, eng.device)
     codes = torch.zeros(hb.n_votes, dtype=torch.uint8, device=eng.device)
-    ad.tally_one_instance(_gpu_tc(eng, db, codes), hb.n_votes, cfg, segments, eng.device)
+    fw, fl = ad.tally_one_instance(_gpu_tc(eng, db, codes), hb.n_votes, cfg, segments, eng.device,
+                                   fold=eng.fold_counts if hip_fold else None)
     torch.cuda.synchronize()
     assert np.array_equal(codes.cpu().numpy(), want)
     assert eng.last_error_count() == 0
+    # the final VoteCounts equal the checker stand-in's one-stream fold
+    cw, cl = ad.tally_one_instance(_fake_tc(CarriedFake(power), hb, 0, hb.n_votes, np.zeros(hb.n_votes, np.uint8)),
+                                   hb.n_votes, cfg, 1, torch.device("cpu"))
+    assert np.array_equal(fw.cpu().numpy(), cw.numpy()) and np.array_equal(fl.cpu().numpy(), cl.numpy())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S,K", [(1, 2), (7, 4), (1000, 2), (5000, 8)])
+def test_gpu_fold_counts_equals_torch_fold(eng, S, K):
+    """agnes_fold_counts (reset / apply / totals, carry, label conventions) against
+    dist.fold_counts on random partials (wrapping weights, sparse labels)"""
+    rng = np.random.default_rng(S * 31 + K)
+    w = rng.integers(-(1 << 62), 1 << 62, (S, K, 2), dtype=np.int64)
+    lab = np.where(rng.random((S, K)) < 0.3, rng.integers(0, 1 << 31, (S, K)), ad.NIL).astype(np.int64)
+    carry = np.concatenate([rng.integers(-(1 << 62), 1 << 62, (K, 2), dtype=np.int64),
+                            rng.choice([0, 5, 77], (K, 1))], axis=1).astype(np.int64)
+    counts = torch.from_numpy(np.concatenate([w, lab[..., None]], axis=-1)).to(eng.device).contiguous()
+    cr = torch.from_numpy(carry).to(eng.device).contiguous()
+    tot = torch.empty((K, 3), dtype=torch.int64, device=eng.device)
+    eng.fold_counts(counts, carry=cr, totals=tot,
+                    flags=abi.FOLD_APPLY | abi.FOLD_ZERO_LABELS | abi.FOLD_CARRY_ZERO_NONE | abi.FOLD_TOTAL_ZERO_LABELS)
+    # torch: prior (label 0 = none) as the first "slice"
+    pl = np.where(carry[:, 2] == 0, ad.NIL, carry[:, 2])
+    allw = torch.from_numpy(np.concatenate([carry[None, :, :2], w])).contiguous()
+    alll = torch.from_numpy(np.concatenate([pl[None], lab])).contiguous()
+    ex_w, ex_lab, t_w, t_lab = ad.fold_counts(allw, alll)
+    ex_lab = torch.where(ex_lab == ad.NIL, torch.zeros_like(ex_lab), ex_lab)
+    t_lab = torch.where(t_lab == ad.NIL, torch.zeros_like(t_lab), t_lab)
+    got = counts.cpu().numpy()
+    assert np.array_equal(got[..., :2], ex_w[1:].numpy())
+    assert np.array_equal(got[..., 2], ex_lab[1:].numpy())
+    tg = tot.cpu().numpy()
+    assert np.array_equal(tg[:, :2], t_w.numpy()) and np.array_equal(tg[:, 2], t_lab.numpy())
+    eng.fold_counts(counts, flags=abi.FOLD_RESET)
+    r = counts.cpu().numpy()
+    assert (r[..., :2] == 0).all() and (r[..., 2] == ad.NIL).all()
 
 
 @pytest.mark.gpu
@@ -320,7 +358,7 @@ def test_gpu_tally_carried_rejects(eng):
         eng.tally_carried(abi.config(abi.MODE_DEDUP, 0, 1), db, codes, counts)
 
 
-def _gpu_dedup_run(eng, hb, power, cfg, segments):
+def _gpu_dedup_run(eng, hb, power, cfg, segments, hip_fold=True):
     from agnes_amd.engine import DeviceBatch
     eng.upload_power(power)
     db = DeviceBatch.from_host(hb, eng.device)
@@ -332,7 +370,8 @@ def _gpu_dedup_run(eng, hb, power, cfg, segments):
                                 lambda base, f: eng.dedup_first(cfg, db, base, f),
                                 lambda base, f: eng.dedup_mask(cfg, db, base, f, tmask),
                                 lambda: eng.dedup_reject(tmask, codes, n),
-                                n, power.shape[1], cfg, segments, eng.device)
+                                n, power.shape[1], cfg, segments, eng.device,
+                                fold=eng.fold_counts if hip_fold else None)
     torch.cuda.synchronize()
     return codes.cpu().numpy()
 
