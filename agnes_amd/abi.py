@@ -8,7 +8,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 NIL = 0xFFFFFFFF
 
 OK, E_INVALID, E_UNSUPPORTED, E_DEVICE, E_NOMEM, E_NODEVICE = 0, -1, -2, -3, -4, -5
@@ -22,6 +22,8 @@ STEP_NEW_ROUND, STEP_PROPOSE, STEP_PREVOTE, STEP_PRECOMMIT, STEP_COMMIT = range(
 EV_NONE = 0xFF
 MSG_NONE, MSG_NEW_ROUND, MSG_PROPOSAL, MSG_VOTE, MSG_TIMEOUT, MSG_DECISION = range(6)
 TIMEOUT_PROPOSE, TIMEOUT_PREVOTE, TIMEOUT_PRECOMMIT = range(3)
+# agnes_apply_msgs message kinds (agnes.h AGNES_IN_*)
+IN_VOTE, IN_PROPOSAL, IN_TIMEOUT, IN_NEW_ROUND = range(4)
 
 CODE_NONE, CODE_POLKA_ANY, CODE_POLKA_NIL, CODE_POLKA_VALUE = 0, 1, 2, 3
 CODE_PRECOMMIT_ANY, CODE_PRECOMMIT_VALUE, CODE_INVALID, CODE_REJECTED = 4, 5, 6, 7

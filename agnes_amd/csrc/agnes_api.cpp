@@ -401,6 +401,25 @@ int agnes_apply_events(agnes_ctx* c, agnes_state* states, uint32_t n, const uint
     return status_of(agnes_launch_apply_events(states, n, off, ev, msgs, flags, (hipStream_t)stream));
 }
 
+int agnes_apply_msgs(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, const uint8_t* kinds,
+                     const int32_t* pol, uint8_t* codes, agnes_state* states, agnes_message* msgs, void* stream) {
+    if (!c || !cfg || !b || cfg->max_rounds < 1u) return AGNES_E_INVALID;
+    if (cfg->mode != AGNES_MODE_REFERENCE || (cfg->flags & (AGNES_FLAG_ROUND_SKIP | AGNES_FLAG_ONE_INSTANCE)) ||
+        cfg->max_rounds > 16u)
+        return AGNES_E_UNSUPPORTED;
+    if (b->n_instances && (!b->offsets || !states)) return AGNES_E_INVALID;
+    if (b->n_votes && (!kinds || !codes || !msgs || !b->instance || !b->round || !b->type || !b->value ||
+                       (!b->weight && !b->validator)))
+        return AGNES_E_INVALID;
+    if (!b->weight && !c->d_sets) return AGNES_E_INVALID; /* the power table weighs the votes */
+    AGNES_TRY(hipSetDevice(c->device));
+    const hipStream_t st = (hipStream_t)stream;
+    AGNES_ORDER(c, st);
+    AGNES_TRY(hipMemsetAsync(c->d_err, 0, sizeof(unsigned long long), st));
+    return status_of(agnes_launch_apply_msgs(b, kinds, pol, c->d_power, c->d_sets, c->n_sets, c->n_vals,
+                                             cfg->max_rounds, cfg->flags, states, msgs, codes, c->d_err, st));
+}
+
 /* ---------------- edge-triggered summary ---------------- */
 
 static bool edges_args_ok(const agnes_config* cfg, const agnes_vote_batch* b, const uint8_t* codes) {

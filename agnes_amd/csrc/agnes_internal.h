@@ -93,6 +93,10 @@ int64_t agnes_fast_lds_per_wave(uint32_t mode, uint32_t flags, uint32_t max_roun
 hipError_t agnes_launch_apply_events(agnes_state* states, uint32_t n, const uint64_t* off,
                                      const agnes_event* ev, agnes_message* msgs, uint32_t flags,
                                      hipStream_t stream);
+hipError_t agnes_launch_apply_msgs(const agnes_vote_batch* vb, const uint8_t* kind, const int32_t* pol,
+                                  const int64_t* power, const agnes_set_info* sets, uint32_t n_sets, uint32_t n_vals,
+                                  uint32_t max_rounds, uint32_t flags, agnes_state* states, agnes_message* msgs,
+                                  uint8_t* codes, unsigned long long* n_invalid, hipStream_t stream);
 hipError_t agnes_launch_gen(const agnes_gen_params* p, const uint64_t* d_offsets, uint64_t n_votes,
                             uint32_t* instance, uint8_t* round, uint8_t* type, uint32_t* value,
                             uint32_t* validator, hipStream_t stream);

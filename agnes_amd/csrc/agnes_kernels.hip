@@ -1026,6 +1026,120 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
 /* ------------------------------------------------------------------ */
 /* batched State::apply over explicit events: one instance per lane    */
 
+/* ------------------------------------------------------------------ */
+/* ConsensusExecutor::apply_msg over a batch of message streams        */
+/* (consensus_executor.rs:54-79), one instance per lane.               */
+
+/* is_quorum in the reference's wrapping i64 (round_votes.rs:31-33) */
+__device__ __forceinline__ bool q23_wrap(int64_t v, int64_t total) {
+    return (int64_t)((uint64_t)v * 3u) > (int64_t)((uint64_t)total * 2u);
+}
+
+struct MsgArgs {
+    agnes_vote_batch vb; /* the messages: instance, round, type (vote type / timeout step), value, validator */
+    const uint8_t* kind; /* AGNES_IN_* per message */
+    const int32_t* pol;  /* Proposal.pol_round per message (NULL: -1) */
+    const int64_t* power;
+    const agnes_set_info* sets;
+    uint32_t n_sets, n_vals, max_rounds, flags;
+    agnes_state* states;
+    agnes_message* msgs;
+    uint8_t* codes;
+    unsigned long long* n_invalid;
+};
+
+/* Per lane: its instance's VoteCounts (round_votes.rs:15-19) in LDS, [key][lane] for
+ * value_w, nil_w and the value slot; the State in registers.  Every message in
+ * stream order: a Vote through VoteExecutor::apply (:61-69; the engine's
+ * validation and power-table weight, vote_executor.rs:20-36) then its event, a
+ * Proposal as Event::Proposal(pol_round, value) (:56-60), a Timeout as its Timeout
+ * event (:70-77), a NewRound input as Event::NewRound / NewRoundProposer(value)
+ * (the executor's answer to its own NewRound message, :31-33) — each applied at
+ * the message's round (apply_event, :82-86). */
+__global__ __launch_bounds__(64) void apply_msgs_kernel(MsgArgs a) {
+    const uint32_t lane = threadIdx.x, i = blockIdx.x * 64u + lane;
+    const uint32_t K = 2u * a.max_rounds;
+    int64_t* const vw = reinterpret_cast<int64_t*>(agnes_smem);
+    int64_t* const nw = vw + (size_t)K * 64u;
+    uint32_t* const lab = reinterpret_cast<uint32_t*>(nw + (size_t)K * 64u);
+    if (i >= a.vb.n_instances) return;
+    for (uint32_t k = 0; k < K; ++k) { /* RoundVotes::new (round_votes.rs:36-45, 83-90) */
+        vw[k * 64u + lane] = 0;
+        nw[k * 64u + lane] = 0;
+        lab[k * 64u + lane] = 0u;
+    }
+    const uint32_t set = a.vb.instance_set ? a.vb.instance_set[i] : (a.n_sets ? i % a.n_sets : 0u);
+    const bool set_ok = set < a.n_sets;
+    const int64_t total = set_ok ? a.sets[set].total : 0;
+    Sm s = sm_load(&a.states[i]);
+    uint64_t bad = 0;
+    const uint64_t NV = a.vb.n_votes;
+    uint64_t lo = a.vb.offsets[i], hi = a.vb.offsets[i + 1u];
+    lo = lo < NV ? lo : NV;
+    hi = hi < NV ? hi : NV;
+    for (uint64_t j = lo; j < hi; ++j) {
+        const uint32_t kd = a.kind[j], r = a.vb.round[j], t = a.vb.type[j], v = a.vb.value[j];
+        uint32_t code = AGNES_CODE_NONE, ev = AGNES_EV_NONE, ev_val = 0;
+        int64_t pol = 0;
+        if (kd == AGNES_IN_VOTE) {
+            const uint32_t x = a.vb.validator[j];
+            const bool need_val = a.vb.weight == nullptr;
+            if (a.vb.instance[j] != i || r >= a.max_rounds || t > 1u || (need_val && (!set_ok || x >= a.n_vals))) {
+                code = AGNES_CODE_INVALID;
+                ++bad;
+            } else {
+                const int64_t w = a.vb.weight ? a.vb.weight[j] : a.power[(uint64_t)set * a.n_vals + x];
+                const uint32_t key = (r * 2u + t) * 64u + lane;
+                if (v != AGNES_NIL) { /* add_vote :50-54, one value slot */
+                    vw[key] = (int64_t)((uint64_t)vw[key] + (uint64_t)w);
+                    lab[key] = v;
+                } else {
+                    nw[key] = (int64_t)((uint64_t)nw[key] + (uint64_t)w);
+                }
+                const int64_t sv = vw[key], sn = nw[key];
+                uint32_t level = 0; /* :58-66 */
+                if (q23_wrap(sv, total)) level = 3;
+                else if (q23_wrap(sn, total)) level = 2;
+                else if (q23_wrap((int64_t)((uint64_t)sv + (uint64_t)sn), total)) level = 1;
+                /* to_event, vote_executor.rs:26-36 */
+                if (level) {
+                    if (t == AGNES_PREVOTE) ev = level == 3 ? AGNES_EV_POLKA_VALUE : (level == 2 ? AGNES_EV_POLKA_NIL : AGNES_EV_POLKA_ANY);
+                    else ev = level == 3 ? AGNES_EV_PRECOMMIT_VALUE : (level == 2 ? AGNES_EV_NONE : AGNES_EV_PRECOMMIT_ANY);
+                }
+                ev_val = lab[key];
+                code = ev == AGNES_EV_NONE ? AGNES_CODE_NONE : ev - AGNES_EV_POLKA_ANY + AGNES_CODE_POLKA_ANY;
+            }
+        } else if (kd == AGNES_IN_PROPOSAL) {
+            ev = AGNES_EV_PROPOSAL;
+            ev_val = v;
+            pol = a.pol ? (int64_t)a.pol[j] : -1;
+        } else if (kd == AGNES_IN_TIMEOUT && t <= 2u) {
+            ev = t == AGNES_TIMEOUT_PROPOSE ? AGNES_EV_TIMEOUT_PROPOSE
+                                            : (t == AGNES_TIMEOUT_PREVOTE ? AGNES_EV_TIMEOUT_PREVOTE : AGNES_EV_TIMEOUT_PRECOMMIT);
+        } else if (kd == AGNES_IN_NEW_ROUND) {
+            ev = v != AGNES_NIL ? AGNES_EV_NEW_ROUND_PROPOSER : AGNES_EV_NEW_ROUND;
+            ev_val = v;
+        } else {
+            code = AGNES_CODE_INVALID; /* not a message kind */
+            ++bad;
+        }
+        MsgOut m;
+        const bool has = ev != AGNES_EV_NONE && sm_apply(s, (int64_t)r, ev, ev_val, pol, a.flags, m);
+        agnes_message o;
+        o.round = has ? m.round : 0;
+        o.pol_round = has ? m.pol_round : 0;
+        o.value = has ? m.value : 0;
+        o.kind = (uint8_t)(has ? m.kind : AGNES_MSG_NONE);
+        o.vote_type = (uint8_t)(has ? m.vote_type : 0);
+        o.timeout_step = (uint8_t)(has ? m.timeout_step : 0);
+        o.pad = 0;
+        a.msgs[j] = o;
+        a.codes[j] = (uint8_t)code;
+    }
+    sm_store(&a.states[i], s);
+    if (bad) atomicAdd(a.n_invalid, (unsigned long long)bad);
+}
+
 __global__ __launch_bounds__(256) void apply_events_kernel(agnes_state* states, uint32_t n,
                                                            const uint64_t* off,
                                                            const agnes_event* ev,
@@ -1225,6 +1339,19 @@ hipError_t agnes_launch_tally(const agnes_tally_args* a, uint32_t mode, int num_
                         : launch_mode<0, true, false>(a, lpw, num_cus, wide_all, st);
     return sm ? launch_mode<0, false, true>(a, lpw, num_cus, wide_all, st)
               : launch_mode<0, false, false>(a, lpw, num_cus, wide_all, st);
+}
+
+hipError_t agnes_launch_apply_msgs(const agnes_vote_batch* vb, const uint8_t* kind, const int32_t* pol,
+                                  const int64_t* power, const agnes_set_info* sets, uint32_t n_sets, uint32_t n_vals,
+                                  uint32_t max_rounds, uint32_t flags, agnes_state* states, agnes_message* msgs,
+                                  uint8_t* codes, unsigned long long* n_invalid, hipStream_t st) {
+    const uint32_t n = vb->n_instances;
+    if (n == 0) return hipSuccess;
+    agnes::MsgArgs a{*vb, kind, pol, power, sets, n_sets, n_vals, max_rounds, flags, states, msgs, codes, n_invalid};
+    const size_t lds = (size_t)2u * max_rounds * 64u * (2u * sizeof(int64_t) + sizeof(uint32_t));
+    AgnesKt kt("apply_msgs", st);
+    hipLaunchKernelGGL(agnes::apply_msgs_kernel, dim3((n + 63u) / 64u), dim3(64), lds, st, a);
+    return hipGetLastError();
 }
 
 hipError_t agnes_launch_apply_events(agnes_state* states, uint32_t n, const uint64_t* off,

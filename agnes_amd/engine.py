@@ -219,6 +219,24 @@ class Engine:
                                           _ptr(events), _ptr(msgs), flags,
                                           _stream_handle(stream)), "agnes_apply_events")
 
+    def apply_msgs(self, cfg: abi.Config, batch: DeviceBatch, kinds: torch.Tensor, pol_round,
+                   codes: torch.Tensor, states: torch.Tensor, msgs: torch.Tensor, stream=None):
+        """Batched ConsensusExecutor::apply_msg (agnes_apply_msgs): kinds uint8
+        [n_votes] (abi.IN_*), pol_round int32 [n_votes] or None, codes uint8
+        [n_votes], states uint8 [n, 64] in place, msgs uint8 [n_votes, 24]."""
+        n = batch.n_votes
+        if kinds.dtype != torch.uint8 or kinds.numel() < n or codes.dtype != torch.uint8 or codes.numel() < n:
+            raise ValueError("kinds and codes must be uint8 tensors of n_votes")
+        if msgs.numel() < 24 * n or states.numel() < 64 * batch.n_instances:
+            raise ValueError("msgs / states too small")
+        if pol_round is not None and (pol_round.dtype != torch.int32 or pol_round.numel() < n):
+            raise ValueError("pol_round must be an int32 tensor of n_votes")
+        b = batch.c()
+        check(self.lib.agnes_apply_msgs(self.ctx, C.byref(cfg), C.byref(b), _ptr(kinds),
+                                        None if pol_round is None else _ptr(pol_round), _ptr(codes),
+                                        _ptr(states), _ptr(msgs), _stream_handle(stream)),
+              "agnes_apply_msgs")
+
     def edges(self, cfg: abi.Config, batch: DeviceBatch, codes: torch.Tensor, stream=None):
         """Edge-triggered summary of coded votes (agnes_edge_offsets + agnes_edges).
         Returns (offsets int64 [n_instances + 1], records uint8 [n_edges, 16] — view

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AGNES_ABI_VERSION 3u
+#define AGNES_ABI_VERSION 4u
 
 /* ---------------------------------------------------------------------------
  * Status codes (reference never fails, state_machine.rs:212; these report
@@ -398,6 +398,32 @@ int64_t agnes_lds_bytes_per_wave(const agnes_config* cfg, uint32_t n_vals);
 int agnes_apply_events(agnes_ctx* ctx, agnes_state* states, uint32_t n_instances,
                        const uint64_t* ev_offsets, const agnes_event* events, agnes_message* msgs,
                        uint32_t flags, void* stream);
+
+/* Batched ConsensusExecutor::apply_msg (consensus_executor.rs:54-86) over
+ * per-instance message streams: instance i applies messages [offsets[i],
+ * offsets[i+1]) of `batch` in order, against its own VoteCounts (one executor per
+ * (round, type), starting at VoteCount::new) and states[i] (in place).  The
+ * batch's columns are read per message kind (kinds[j], AGNES_IN_*):
+ *   VOTE       Message::Vote (:61-69): instance, round, type, value, validator
+ *              (or weight) as agnes_tally, then State::apply(round, event)
+ *   PROPOSAL   Message::Proposal (:56-60): Event::Proposal(pol_round[j], value)
+ *              at round (pol_round NULL: -1 for every proposal)
+ *   TIMEOUT    Message::Timeout (:70-77): type = AGNES_TIMEOUT_* -> TimeoutX at round
+ *   NEW_ROUND  the executor's own NewRound (execute, :31-33): Event::NewRound at
+ *              round, or NewRoundProposer(value) when value != AGNES_NIL
+ * msgs[j] receives the Option<Message> of message j (kind AGNES_MSG_NONE = None),
+ * codes[j] the vote's tally code (bits 0..2; INVALID for a bad vote or kind, NONE
+ * for the other kinds; agnes_last_error_count counts the INVALIDs).  REFERENCE mode without RoundSkip (else
+ * AGNES_E_UNSUPPORTED); cfg->flags AGNES_FLAG_DISTINCT_VALUES applies; the State
+ * machine is implied; max_rounds <= 16.  All pointers DEVICE; one instance per
+ * lane (latency bound: messages of one instance are sequential). */
+#define AGNES_IN_VOTE 0u
+#define AGNES_IN_PROPOSAL 1u
+#define AGNES_IN_TIMEOUT 2u
+#define AGNES_IN_NEW_ROUND 3u
+int agnes_apply_msgs(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch, const uint8_t* kinds,
+                     const int32_t* pol_round, uint8_t* codes, agnes_state* states, agnes_message* msgs,
+                     void* stream);
 
 /* ---------------------------------------------------------------------------
  * Edge-triggered summary of a coded batch.

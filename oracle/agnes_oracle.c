@@ -483,6 +483,75 @@ int orc_apply_events(agnes_state* states, uint32_t n, const uint64_t* off, const
     return AGNES_OK;
 }
 
+/* ConsensusExecutor::apply_msg over per-instance message streams
+ * (consensus_executor.rs:54-86; include/agnes.h agnes_apply_msgs).  One
+ * ConsensusExecutor per instance: a VoteCount per (round, type) (the HeightVotes
+ * the reference leaves as a stub, :5) and the State.  Message kinds:
+ *   VOTE      :61-69  VoteExecutor::apply (the batch validation and weight of
+ *                     orc_tally), then apply_event(v.round, event)
+ *   PROPOSAL  :56-60  Event::Proposal(pol_round, value) at p.round
+ *   TIMEOUT   :70-77  TimeoutPropose / Prevote / Precommit at t.round
+ *   NEW_ROUND         Event::NewRound / NewRoundProposer(value) at round (the
+ *                     executor's own NewRound, execute :31-33) */
+int orc_apply_msgs(const agnes_config* cfg, const agnes_vote_batch* b, const orc_power* pw, const uint8_t* kinds,
+                   const int32_t* pol, uint8_t* codes, agnes_state* states, agnes_message* msgs,
+                   uint64_t* n_invalid) {
+    if (!cfg || !b || !states || !b->offsets || cfg->max_rounds == 0 || cfg->max_rounds > 256u) return AGNES_E_INVALID;
+    if (b->n_votes && (!kinds || !codes || !msgs || !b->instance || !b->round || !b->type || !b->value ||
+                       (!b->weight && !b->validator)))
+        return AGNES_E_INVALID;
+    const uint32_t R = cfg->max_rounds, nv = pw ? pw->n_vals : 0;
+    orc_vote_count* cnt = (orc_vote_count*)calloc((size_t)2u * R, sizeof(orc_vote_count));
+    if (!cnt) return AGNES_E_NOMEM;
+    uint64_t bad = 0;
+    for (uint32_t i = 0; i < b->n_instances; ++i) {
+        const uint32_t set = b->instance_set ? b->instance_set[i] : (pw && pw->n_sets ? i % pw->n_sets : 0);
+        const int set_ok = pw && set < pw->n_sets;
+        const int64_t total = set_ok ? pw->totals[set] : 0;
+        for (uint32_t k = 0; k < 2u * R; ++k) orc_vc_new(&cnt[k], total);
+        for (uint64_t j = b->offsets[i]; j < b->offsets[i + 1]; ++j) {
+            const uint32_t r = b->round[j], t = b->type[j], v = b->value[j];
+            agnes_event e;
+            memset(&e, 0, sizeof(e));
+            e.kind = AGNES_EV_NONE;
+            e.round = r;
+            codes[j] = AGNES_CODE_NONE;
+            if (kinds[j] == AGNES_IN_VOTE) {
+                if (b->instance[j] != i || r >= R || t > 1u || (!b->weight && (!set_ok || b->validator[j] >= nv))) {
+                    codes[j] = AGNES_CODE_INVALID;
+                    ++bad;
+                } else {
+                    const int64_t w = b->weight ? b->weight[j] : pw->power[(uint64_t)set * nv + b->validator[j]];
+                    uint32_t tv = 0;
+                    const uint32_t ev = orc_to_event(t, orc_vc_add(&cnt[r * 2u + t], v, w, &tv));
+                    codes[j] = ev_to_code(ev);
+                    e.kind = (uint8_t)ev;
+                    e.value = tv;
+                }
+            } else if (kinds[j] == AGNES_IN_PROPOSAL) {
+                e.kind = AGNES_EV_PROPOSAL;
+                e.value = v;
+                e.pol_round = pol ? pol[j] : -1;
+            } else if (kinds[j] == AGNES_IN_TIMEOUT && t <= AGNES_TIMEOUT_PRECOMMIT) {
+                e.kind = (uint8_t)(t == AGNES_TIMEOUT_PROPOSE   ? AGNES_EV_TIMEOUT_PROPOSE
+                                   : t == AGNES_TIMEOUT_PREVOTE ? AGNES_EV_TIMEOUT_PREVOTE
+                                                                : AGNES_EV_TIMEOUT_PRECOMMIT);
+            } else if (kinds[j] == AGNES_IN_NEW_ROUND) {
+                e.kind = (uint8_t)(v != AGNES_NIL ? AGNES_EV_NEW_ROUND_PROPOSER : AGNES_EV_NEW_ROUND);
+                e.value = v;
+            } else {
+                codes[j] = AGNES_CODE_INVALID;
+                ++bad;
+            }
+            if (e.kind != AGNES_EV_NONE) orc_state_apply(&states[i], r, &e, cfg->flags, &msgs[j]);
+            else memset(&msgs[j], 0, sizeof(msgs[j]));
+        }
+    }
+    free(cnt);
+    if (n_invalid) *n_invalid = bad;
+    return AGNES_OK;
+}
+
 /* Edge-triggered summary (include/agnes.h agnes_edge).  The
  * per-vote codes are VoteExecutor::apply's level-triggered Option<Event>
  * (vote_executor.rs:20-36) for the vote's (round, type) executor — the

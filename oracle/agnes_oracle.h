@@ -90,6 +90,12 @@ int orc_events(const agnes_config* cfg, const agnes_vote_batch* batch, const uin
 int orc_apply_events(agnes_state* states, uint32_t n_instances, const uint64_t* ev_offsets,
                      const agnes_event* events, agnes_message* msgs, uint32_t flags);
 
+/* batched ConsensusExecutor::apply_msg over per-instance message streams
+ * (agnes_apply_msgs): kinds AGNES_IN_*, pol_round per message (NULL: -1) */
+int orc_apply_msgs(const agnes_config* cfg, const agnes_vote_batch* batch, const orc_power* pw, const uint8_t* kinds,
+                   const int32_t* pol_round, uint8_t* codes, agnes_state* states, agnes_message* msgs,
+                   uint64_t* n_invalid);
+
 /* edge-triggered summary of coded votes (agnes_edge_offsets + agnes_edges):
  * offsets[n_instances + 1]; out NULL = count only */
 int orc_edges(const agnes_config* cfg, const agnes_vote_batch* batch, const uint8_t* codes,

@@ -60,6 +60,8 @@ def lib():
                                        C.POINTER(OrcPower), P, P, C.POINTER(C.c_uint64), P, C.c_int]
         L.orc_events.argtypes = [C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P]
         L.orc_apply_events.argtypes = [P, C.c_uint32, P, P, P, C.c_uint32]
+        L.orc_apply_msgs.argtypes = [C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), C.POINTER(OrcPower),
+                                     P, P, P, P, P, C.POINTER(C.c_uint64)]
         L.orc_edges.argtypes = [C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P]
         L.orc_set_totals.argtypes = [P, C.c_uint32, C.c_uint32, P]
         L.orc_gen_instance_votes.argtypes = [C.POINTER(abi.GenParams), C.c_uint32]
@@ -228,6 +230,31 @@ def apply_events(states: np.ndarray, ev_offsets: np.ndarray, events: np.ndarray,
     rc = lib().orc_apply_events(_p(st), len(st), _p(ev_offsets), _p(events), _p(msgs), flags)
     assert rc == 0, rc
     return st, msgs
+
+
+def apply_msgs(cfg: abi.Config, b, kinds: np.ndarray, pol_round: Optional[np.ndarray],
+               power: Optional[np.ndarray], states: np.ndarray, totals=None):
+    """orc_apply_msgs over a message script (agnes_amd.script.Script or HostBatch +
+    kinds): returns (codes, states_out, msgs abi.MESSAGE_DTYPE, n_invalid)."""
+    n = b.n_votes
+    codes = np.zeros(max(n, 1), dtype=np.uint8)
+    msgs = np.zeros(max(n, 1), dtype=abi.MESSAGE_DTYPE)
+    pw_struct = None
+    if power is not None:
+        power = np.ascontiguousarray(power, dtype=np.int64)
+        totals = set_totals(power) if totals is None else np.ascontiguousarray(totals, dtype=np.int64)
+        pw_struct = OrcPower(_p(power), _p(totals), power.shape[0], power.shape[1])
+    st = np.array(states, dtype=abi.STATE_DTYPE, copy=True)
+    kinds = np.ascontiguousarray(kinds, dtype=np.uint8)
+    pol = None if pol_round is None else np.ascontiguousarray(pol_round, dtype=np.int32)
+    cb = abi.VoteBatch(_p(b.instance), _p(b.round), _p(b.type), _p(b.value), _p(b.validator), _p(b.offsets),
+                       _p(getattr(b, "instance_set", None)), _p(getattr(b, "weight", None)), n, b.n_instances, 0)
+    nbad = C.c_uint64(0)
+    rc = lib().orc_apply_msgs(C.byref(cfg), C.byref(cb), C.byref(pw_struct) if pw_struct is not None else None,
+                              _p(kinds), _p(pol), _p(codes), _p(st), _p(msgs), C.byref(nbad))
+    if rc != 0:
+        raise RuntimeError(f"orc_apply_msgs rc={rc}")
+    return codes[:n], st, msgs[:n], int(nbad.value)
 
 
 def state_apply(state: abi.StateRec, round_: int, ev: abi.Event, flags: int = 0):

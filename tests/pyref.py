@@ -248,3 +248,55 @@ def tally(batch: Batch, power: List[List[int]], totals: List[int], mode: int, fl
                 code |= _vmsg(m1, m2) << 4
             codes[j] = code
     return codes, states
+
+
+IN_VOTE, IN_PROPOSAL, IN_TIMEOUT, IN_NEW_ROUND = range(4)
+_TIMEOUT_EV = {TO_PROPOSE: EV_TIMEOUT_PROPOSE, TO_PREVOTE: EV_TIMEOUT_PREVOTE,
+               TO_PRECOMMIT: EV_TIMEOUT_PRECOMMIT}
+
+
+def apply_msgs(batch: Batch, kinds: List[int], pol_round: Optional[List[int]], power: List[List[int]],
+               totals: List[int], flags: int, max_rounds: int, states: List[State]):
+    """ConsensusExecutor::apply_msg over per-instance message streams
+    (consensus_executor.rs:54-86): one executor per (round, type) per instance,
+    Proposal -> Event::Proposal(pol_round, value) (:56-60), Vote -> VoteExecutor
+    then its event (:61-69), Timeout -> TimeoutX (:70-77), each at the message's
+    round; NewRound input -> NewRound / NewRoundProposer(value).
+    Returns (codes, states, msgs: list of Optional[Msg])."""
+    n = len(batch.round)
+    codes, msgs = [0] * n, [None] * n
+    states = list(states)
+    distinct = bool(flags & FLAG_DISTINCT_VALUES)
+    for i in range(len(batch.offsets) - 1):
+        set_idx = batch.instance_set[i] if batch.instance_set else (i % len(power) if power else 0)
+        set_ok = set_idx < len(power)
+        total = totals[set_idx] if set_ok else 0
+        n_vals = len(power[set_idx]) if set_ok else 0
+        counts: Dict[Tuple[int, int], Count] = {}
+        s = states[i]
+        for j in range(batch.offsets[i], batch.offsets[i + 1]):
+            k, r, t, v = kinds[j], batch.round[j], batch.type[j], batch.value[j]
+            ev, ev_val, pol = EV_NONE, 0, 0
+            if k == IN_VOTE:
+                val = batch.validator[j]
+                if (batch.instance[j] != i or r >= max_rounds or t > 1
+                        or (batch.weight is None and (not set_ok or val >= n_vals))):
+                    codes[j] = CODE_INVALID
+                    continue
+                w = batch.weight[j] if batch.weight is not None else power[set_idx][val]
+                th, ev_val = counts.setdefault((r, t), Count(total)).add(v, w)
+                ev = to_event(t, th)
+                codes[j] = _CODE_OF_EV[ev]
+            elif k == IN_PROPOSAL:
+                ev, ev_val, pol = EV_PROPOSAL, v, (pol_round[j] if pol_round is not None else -1)
+            elif k == IN_TIMEOUT and t in _TIMEOUT_EV:
+                ev = _TIMEOUT_EV[t]
+            elif k == IN_NEW_ROUND:
+                ev, ev_val = (EV_NEW_ROUND_PROPOSER, v) if v != NIL else (EV_NEW_ROUND, 0)
+            else:
+                codes[j] = CODE_INVALID
+                continue
+            if ev != EV_NONE:
+                s, msgs[j] = apply(s, r, ev, ev_val, pol, distinct_values=distinct)
+        states[i] = s
+    return codes, states, msgs
