@@ -22,47 +22,34 @@ static int failures = 0;
         }                                                                    \
     } while (0)
 
-// round_votes.rs:107-132
+// Golden vector of round_votes.rs:107-132: four unit-weight prevotes against a
+// total of 4 give the threshold sequence Init, Init, Any, Value.
 static void add_votes() {
-    Value v{};
-    std::optional<Value> val = v;
-    int64_t total = 4;
-    RoundVotes round_votes(1, 0, total);
-    int64_t weight = 1;
-
-    // add a vote. nothing changes.
-    Vote vote = Vote::new_prevote(0, val);
-    Thresh thresh = round_votes.add_vote(vote, weight);
-    ASSERT_EQ(thresh, Thresh::Init());
-
-    // add it again, nothing changes.
-    thresh = round_votes.add_vote(vote, weight);
-    ASSERT_EQ(thresh, Thresh::Init());
-
-    // add a vote for nil, get Thresh::Any
-    Vote vote_nil = Vote::new_prevote(0, std::nullopt);
-    thresh = round_votes.add_vote(vote_nil, weight);
-    ASSERT_EQ(thresh, Thresh::Any());
-
-    // add vote for value, get Thresh::Value
-    thresh = round_votes.add_vote(vote, weight);
-    ASSERT_EQ(thresh, Thresh::Value_(v));
+    const Value label{};
+    const std::optional<Value> some_label = label;
+    RoundVotes counts(/*height*/ 1, /*round*/ 0, /*total*/ 4);
+    const Vote for_label = Vote::new_prevote(0, some_label);
+    const Vote for_nil = Vote::new_prevote(0, std::nullopt);
+    const Thresh expected[4] = {Thresh::Init(), Thresh::Init(), Thresh::Any(), Thresh::Value_(label)};
+    const Vote* sequence[4] = {&for_label, &for_label, &for_nil, &for_label};
+    for (int k = 0; k < 4; ++k) ASSERT_EQ(counts.add_vote(*sequence[k], 1), expected[k]);
 }
 
-// state_machine.rs:331-345
+// Golden vector of state_machine.rs:331-345: one height through the four
+// events of a proposer's round 0 ends in Commit with each expected message.
 static void happy_case() {
-    Value val{};
-    std::optional<Value> v = val;
-    State s = State::new_(1);
-    auto [s1, m1] = s.apply(0, Event::NewRoundProposer(val));
-    ASSERT_EQ(*m1, Message::proposal_(0, val, -1));
-    auto [s2, m2] = s1.apply(0, Event::Proposal(-1, val));
-    ASSERT_EQ(*m2, Message::prevote(0, v));
-    auto [s3, m3] = s2.apply(0, Event::PolkaValue(val));
-    ASSERT_EQ(*m3, Message::precommit(0, v));
-    auto [s4, m4] = s3.apply(0, Event::PrecommitValue(val));
-    ASSERT_EQ(*m4, Message::decision_(0, val));
-    ASSERT_EQ(s4.step(), Step::Commit);
+    const Value label{};
+    const std::optional<Value> some_label = label;
+    const State start = State::new_(1);
+    auto [proposed, msg_a] = start.apply(0, Event::NewRoundProposer(label));
+    ASSERT_EQ(*msg_a, Message::proposal_(0, label, -1));
+    auto [prevoted, msg_b] = proposed.apply(0, Event::Proposal(-1, label));
+    ASSERT_EQ(*msg_b, Message::prevote(0, some_label));
+    auto [precommitted, msg_c] = prevoted.apply(0, Event::PolkaValue(label));
+    ASSERT_EQ(*msg_c, Message::precommit(0, some_label));
+    auto [committed, msg_d] = precommitted.apply(0, Event::PrecommitValue(label));
+    ASSERT_EQ(*msg_d, Message::decision_(0, label));
+    ASSERT_EQ(committed.step(), Step::Commit);
 }
 
 // C1: VoteExecutor::new(1, 4), weight 1 — vote_executor.rs:26-36
