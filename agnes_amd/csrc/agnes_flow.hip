@@ -55,8 +55,9 @@ constexpr uint32_t SMALLB = 4u; /* batch size of the work queue's tail          
  * vote, 0 without the State machine), State.round in every byte, 0xFF bytes when it
  * enters in Precommit (valid from the start); the P1 and C positions (stream-relative,
  * ~0: none); decision round | F_LOCK (P1 was a PolkaValue); step.  The last valid
- * candidate's position + 1 is kept beside (vtab).  The values these positions name
- * are read when the batch ends (its States are written one chunk later). */
+ * candidate is kept beside (vtab: position + 1 << 32 | its value, an LDS u64 max); the
+ * locked and decision values go straight into the staged States when P1 / C are
+ * found (the vote's value is still in registers). */
 constexpr uint32_t R_Q2 = 0, R_PBASE = 1, R_NV = 2, R_EQ8 = 3, R_SMASK = 4, R_EQ = 5, R_VALL = 6, R_STEP = 7, R_P1 = 8,
                    R_C = 9, R_DF = 10, RECW = 12;
 constexpr uint32_t F_LOCK = 0x100u;
@@ -80,7 +81,7 @@ __host__ __device__ inline uint32_t carry_bytes(uint32_t R) { return (uint32_t)a
 /* per-wave LDS: DMA slot | carried executors (2 copies x (vw[2R], vn[2R]) u32) |
  * instance records | (State machine) valid candidates, two batches' staged States */
 __host__ __device__ inline uint32_t lds_bytes(bool sm, uint32_t R) {
-    return F_BYTES + carry_bytes(R) + FB * RECW * 4u + (sm ? FB * 4u + 2u * FB * 64u : 0u);
+    return F_BYTES + carry_bytes(R) + FB * RECW * 4u + (sm ? FB * 8u + 2u * FB * 64u : 0u);
 }
 
 __device__ __forceinline__ uint32_t zero_marks(uint32_t x) { /* 0x80 in the bytes of x that are zero */
@@ -167,8 +168,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
     uint32_t* const crow = reinterpret_cast<uint32_t*>(base + F_BYTES);
     const uint32_t cw = 4u * R; /* one carry copy: vw[2R] then vn[2R] */
     uint32_t* const itab = reinterpret_cast<uint32_t*>(base + F_BYTES + carry_bytes(R));
-    uint32_t* const vtab = reinterpret_cast<uint32_t*>(base + F_BYTES + carry_bytes(R) + FB * RECW * 4u);
-    unsigned char* const sb = base + F_BYTES + carry_bytes(R) + FB * RECW * 4u + FB * 4u;
+    unsigned long long* const vtab = reinterpret_cast<unsigned long long*>(base + F_BYTES + carry_bytes(R) + FB * RECW * 4u);
+    unsigned char* const sb = base + F_BYTES + carry_bytes(R) + FB * RECW * 4u + FB * 8u;
     const agnes_state* const st_in = a.states_in ? a.states_in : a.states;
     uint32_t cpar = 0;
     uint64_t pf_at = ~0ull;
@@ -303,49 +304,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
         }
     };
 
-    /* A finished batch's States wait for the values at its P1 / C / valid positions:
-     * LDS-DMA'd at the batch's end straight into the staged States' locked / valid /
-     * decision value words (lane 16 k' of a load writes the State 4 j + k'), and the
-     * States are patched from the records and written out at the next chunk's top,
-     * behind its DMA wait (no register stays live across the chunks). */
-    uint32_t pend_m = 0, pend_s0 = 0, pend_par = 0;
-    auto dma_values = [&](uint32_t mm, uint64_t s0v, uint32_t par) {
-        const uint32_t* const vcol = a.vb.value + s0v;
-        for (uint32_t j = 0; 4u * j < mm; ++j) {
-            const uint32_t k = 4u * j + (lane >> 4);
-            const bool own = (lane & 15u) == 0u && k < mm;
-            uint32_t p1 = NONE, cc = NONE, df = 0, vp = 0;
-            if (own) {
-                const uint32_t* const rk = itab + RECW * k;
-                p1 = rk[R_P1];
-                cc = rk[R_C];
-                df = rk[R_DF];
-                vp = vtab[k];
-            }
-            const uint32_t ml = lds_addr(sb + par * (FB * 64u)) + 256u * j;
-            if ((df & F_LOCK) && p1 < cc) sdma4(vcol, 4u * p1, ml + 40u);  /* locked_value   */
-            if (vp) sdma4(vcol, 4u * (vp - 1u), ml + 44u);                 /* valid_value    */
-            if (cc != NONE) sdma4(vcol, 4u * cc, ml + 48u);                /* decision_value */
-        }
-    };
-    auto finalize = [&]() { /* the staged States patched from the records and written out */
-        unsigned char* const sbp = sb + pend_par * (FB * 64u);
-        if (lane < pend_m) {
+    /* a finished batch's staged States patched from its records and written out (the
+     * locked / decision values are in them already, the valid one is in vtab) */
+    auto finalize = [&](uint32_t mm, uint32_t s0, const unsigned char* sbp) {
+        if (lane < mm) {
             const uint32_t* const rk = itab + RECW * lane;
-            const uint32_t p1 = rk[R_P1], cc = rk[R_C], df = rk[R_DF], vp = vtab[lane];
-            uint32_t* const sp = reinterpret_cast<uint32_t*>(sbp + 64u * lane);
+            const uint32_t p1 = rk[R_P1], cc = rk[R_C], df = rk[R_DF];
+            const unsigned long long vv = vtab[lane];
+            uint32_t* const sp = reinterpret_cast<uint32_t*>(const_cast<unsigned char*>(sbp) + 64u * lane);
             const uint32_t step = cc != NONE ? (uint32_t)AGNES_STEP_COMMIT
                                              : (p1 < cc ? (uint32_t)AGNES_STEP_PRECOMMIT : rk[R_STEP]);
             uint32_t fl = (sp[13] & ~0xFFu) | step;
-            if ((df & F_LOCK) && p1 < cc) { sp[4] = sp[2]; sp[5] = sp[3]; fl |= 1u << 8; }
-            if (vp) { sp[6] = sp[2]; sp[7] = sp[3]; fl |= 1u << 16; }
+            if (df & F_LOCK) { sp[4] = sp[2]; sp[5] = sp[3]; fl |= 1u << 8; } /* (P1 precedes any C) */
+            if (vv) { sp[6] = sp[2]; sp[7] = sp[3]; sp[11] = (uint32_t)vv; fl |= 1u << 16; }
             if (cc != NONE) { sp[8] = df & 0xFFu; sp[9] = 0u; fl |= 1u << 24; }
             sp[13] = fl;
         }
         __builtin_amdgcn_wave_barrier();
-        if (lane < 4u * pend_m)
-            reinterpret_cast<uint4*>(a.states + pend_s0)[lane] = *reinterpret_cast<const uint4*>(sbp + o16);
-        pend_m = 0;
+        if (lane < 4u * mm) reinterpret_cast<uint4*>(a.states + s0)[lane] = *reinterpret_cast<const uint4*>(sbp + o16);
     };
 
     Hdr H, N;
@@ -398,7 +374,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                 const uint32_t lo_r = rc == 0u ? lead : 0u; /* the chunk's active votes: lo_r .. hi_r */
                 if (pf_at != c) dma_chunk(c, lo_r, Lend - rc); /* not prefetched: a wave's first chunk */
                 dma_wait(); /* this chunk's DMA (and a new batch's States) have landed */
-                if (SM && pend_m) finalize(); /* the batch before (its values landed too) */
                 if (rc == 0u && lane < m) { /* instance records */
                     uint32_t* const rk = itab + RECW * lane;
                     rk[R_Q2] = q2k;
@@ -408,7 +383,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                     rk[R_P1] = NONE;
                     rk[R_C] = NONE;
                     rk[R_DF] = 0u;
-                    if (SM) vtab[lane] = 0u;
+                    if (SM) vtab[lane] = 0ull;
                 }
                 if (SM && smf) { /* the State machine's view of each instance (state_machine.rs:184) */
                     if (lane < m) {
@@ -822,13 +797,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                             c1 |= unit(x1, dPB, dCB, okB, eB.z, nn1, aP1, aC1, v1);
                         }
                         const uint32_t lk0 = aP0 & (x0 << 3) & 0x80808080u, lk1 = aP1 & (x1 << 3) & 0x80808080u;
-                        if (ballot((lk0 | lk1 | aC0 | aC1 | v0 | v1) != 0u)) { /* the few lanes with a State write */
-                            if (lk0) atomicOr(rA + R_DF, F_LOCK);
-                            if (lk1) atomicOr(rB + R_DF, F_LOCK);
-                            if (aC0) atomicOr(rA + R_DF, (r8[0] >> (8u * ((uint32_t)__builtin_ctz(aC0) >> 3))) & 0xFFu);
-                            if (aC1) atomicOr(rB + R_DF, (r8[1] >> (8u * ((uint32_t)__builtin_ctz(aC1) >> 3))) & 0xFFu);
-                            if (v0) atomicMax(vtab + kA, pos0 + ((31u - (uint32_t)__builtin_clz(v0)) >> 3) + 1u);
-                            if (v1) atomicMax(vtab + kB, pos1 + ((31u - (uint32_t)__builtin_clz(v1)) >> 3) + 1u);
+                        if (ballot((lk0 | lk1 | aC0 | aC1 | v0 | v1) != 0u)) { /* the lanes with a State write */
+                            /* the value of byte b of a unit's votes (registers) */
+                            auto vsel = [&](uint32_t u, uint32_t b) -> uint32_t {
+                                const uint32_t* const vv = value + 4u * u;
+                                const uint32_t lo = (b & 1u) ? vv[1] : vv[0], hi = (b & 1u) ? vv[3] : vv[2];
+                                return (b & 2u) ? hi : lo;
+                            };
+                            uint32_t* const sA = reinterpret_cast<uint32_t*>(sbh + 64u * kA);
+                            uint32_t* const sB = reinterpret_cast<uint32_t*>(sbh + 64u * kB);
+                            if (lk0) { /* locked (:198) */
+                                atomicOr(rA + R_DF, F_LOCK);
+                                sA[10] = vsel(0u, (uint32_t)__builtin_ctz(lk0) >> 3);
+                            }
+                            if (lk1) {
+                                atomicOr(rB + R_DF, F_LOCK);
+                                sB[10] = vsel(1u, (uint32_t)__builtin_ctz(lk1) >> 3);
+                            }
+                            if (aC0) { /* the decision (:211) */
+                                const uint32_t b = (uint32_t)__builtin_ctz(aC0) >> 3;
+                                atomicOr(rA + R_DF, (r8[0] >> (8u * b)) & 0xFFu);
+                                sA[12] = vsel(0u, b);
+                            }
+                            if (aC1) {
+                                const uint32_t b = (uint32_t)__builtin_ctz(aC1) >> 3;
+                                atomicOr(rB + R_DF, (r8[1] >> (8u * b)) & 0xFFu);
+                                sB[12] = vsel(1u, b);
+                            }
+                            if (v0) { /* valid (:198, :202): the last candidate */
+                                const uint32_t b = (31u - (uint32_t)__builtin_clz(v0)) >> 3;
+                                atomicMax(vtab + kA, ((unsigned long long)(pos0 + b + 1u) << 32) | vsel(0u, b));
+                            }
+                            if (v1) {
+                                const uint32_t b = (31u - (uint32_t)__builtin_clz(v1)) >> 3;
+                                atomicMax(vtab + kB, ((unsigned long long)(pos1 + b + 1u) << 32) | vsel(1u, b));
+                            }
                         }
                     }
                 }
@@ -842,20 +845,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
             }
         }
         /* batch end: the States out (a walk-list batch's are the walk kernel's) */
-        if (SM && (m || pend_m)) {
-            if (smf || pend_m) dma_wait(); /* no chunk ran: staged States / pending values in flight */
-            if (pend_m) finalize();        /* the batch before, when this one ran no chunk */
-            if (m && H.stream) {
-                if (smf) { /* no vote: the States as they came */
-                    if (lane < 4u * m)
-                        reinterpret_cast<uint4*>(a.states + H.s0)[lane] = *reinterpret_cast<const uint4*>(sbh + o16);
-                } else { /* the values the records' positions name requested; the States
-                          * written at the next chunk's top (behind its DMA wait) */
-                    dma_values(m, u64of(rdl(H.olo, 0u), rdl(H.ohi, 0u)) & ~127ull, spar); /* positions from Sa */
-                    pend_m = m;
-                    pend_s0 = H.s0;
-                    pend_par = spar;
-                }
+        if (SM && m && H.stream) {
+            if (smf) { /* no vote: the States as they came */
+                dma_wait();
+                if (lane < 4u * m)
+                    reinterpret_cast<uint4*>(a.states + H.s0)[lane] = *reinterpret_cast<const uint4*>(sbh + o16);
+            } else {
+                finalize(m, H.s0, sbh);
             }
         }
         if (N.s0 >= N.e0) break;
@@ -869,10 +865,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
         range_of(rdl(tq, 0u), N.s0, N.e0); /* the batch after, grabbed one batch ago */
         if (lane == 0) tq = atomicAdd(ctr, 1u);
         hdr1(N);
-    }
-    if (SM && pend_m) {
-        dma_wait();
-        finalize();
     }
     flush();
     const uint32_t nb = rdl(scan(bad), 63u);
@@ -942,8 +934,10 @@ static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStrea
 }
 
 bool agnes_flow_supported(const agnes_tally_args* a) {
-    /* rounds 0..14 in the byte checks; the per-wave LDS fits 16 waves per CU */
-    return a->max_rounds <= 15u && agnes::flow::lds_bytes(true, a->max_rounds) * 16u <= 160u * 1024u;
+    /* rounds 0..14 in the byte checks; the per-wave LDS fits the waves a CU holds (16
+     * without the State machine, 12 with it: its VGPRs allow 3 waves per SIMD) */
+    const bool sm = (a->flags & AGNES_FLAG_STATE_MACHINE) != 0 && a->states != nullptr;
+    return a->max_rounds <= 15u && agnes::flow::lds_bytes(sm, a->max_rounds) * (sm ? 12u : 16u) <= 160u * 1024u;
 }
 
 hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t st) {
