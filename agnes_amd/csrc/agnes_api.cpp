@@ -420,6 +420,45 @@ int agnes_apply_msgs(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_bat
                                              cfg->max_rounds, cfg->flags, states, msgs, codes, c->d_err, st));
 }
 
+/* ---------------- C5: the State machine of a split instance ---------------- */
+
+static int one_sm_args(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint64_t base,
+                       const uint8_t* codes, const agnes_state* state, const int64_t* marks) {
+    if (!c || !cfg || !b || !state || !marks) return AGNES_E_INVALID;
+    if (cfg->mode > AGNES_MODE_DEDUP || (cfg->flags & AGNES_FLAG_ROUND_SKIP)) return AGNES_E_UNSUPPORTED;
+    if (b->n_votes && (!codes || !b->round || !b->value)) return AGNES_E_INVALID;
+    if (base + b->n_votes > (1ull << 31) || base + b->n_votes < base) return AGNES_E_UNSUPPORTED;
+    return AGNES_OK;
+}
+
+int agnes_one_sm_scan(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint64_t base,
+                      const uint8_t* codes, const agnes_state* state, int64_t* marks, void* stream) {
+    const int rc = one_sm_args(c, cfg, b, base, codes, state, marks);
+    if (rc != AGNES_OK) return rc;
+    AGNES_TRY(hipSetDevice(c->device));
+    AGNES_ORDER(c, (hipStream_t)stream);
+    return status_of(agnes_launch_one_sm(0, codes, b->round, b->value, b->n_votes, base,
+                                         const_cast<agnes_state*>(state), marks, c->num_cus, (hipStream_t)stream));
+}
+
+int agnes_one_sm_apply(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint64_t base,
+                       uint8_t* codes, const agnes_state* state, int64_t* marks, void* stream) {
+    const int rc = one_sm_args(c, cfg, b, base, codes, state, marks);
+    if (rc != AGNES_OK) return rc;
+    AGNES_TRY(hipSetDevice(c->device));
+    AGNES_ORDER(c, (hipStream_t)stream);
+    return status_of(agnes_launch_one_sm(1, codes, b->round, b->value, b->n_votes, base,
+                                         const_cast<agnes_state*>(state), marks, c->num_cus, (hipStream_t)stream));
+}
+
+int agnes_one_sm_finish(agnes_ctx* c, const int64_t* marks, agnes_state* state, void* stream) {
+    if (!c || !marks || !state) return AGNES_E_INVALID;
+    AGNES_TRY(hipSetDevice(c->device));
+    AGNES_ORDER(c, (hipStream_t)stream);
+    return status_of(agnes_launch_one_sm(2, nullptr, nullptr, nullptr, 0, 0, state, const_cast<int64_t*>(marks),
+                                         c->num_cus, (hipStream_t)stream));
+}
+
 /* ---------------- edge-triggered summary ---------------- */
 
 static bool edges_args_ok(const agnes_config* cfg, const agnes_vote_batch* b, const uint8_t* codes) {

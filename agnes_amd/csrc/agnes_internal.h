@@ -97,6 +97,9 @@ hipError_t agnes_launch_apply_msgs(const agnes_vote_batch* vb, const uint8_t* ki
                                   const int64_t* power, const agnes_set_info* sets, uint32_t n_sets, uint32_t n_vals,
                                   uint32_t max_rounds, uint32_t flags, agnes_state* states, agnes_message* msgs,
                                   uint8_t* codes, unsigned long long* n_invalid, hipStream_t stream);
+/* pass 0 scan, 1 apply, 2 finish (agnes_onesm.hip) */
+hipError_t agnes_launch_one_sm(int pass, const uint8_t* codes, const uint8_t* round, const uint32_t* value, uint64_t n,
+                               uint64_t base, agnes_state* state, int64_t* marks, int num_cus, hipStream_t stream);
 hipError_t agnes_launch_gen(const agnes_gen_params* p, const uint64_t* d_offsets, uint64_t n_votes,
                             uint32_t* instance, uint8_t* round, uint8_t* type, uint32_t* value,
                             uint32_t* validator, hipStream_t stream);

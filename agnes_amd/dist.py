@@ -291,6 +291,37 @@ def _tally_one_instance_hip(tally_carried, fold, one, off, S, K, device, group, 
 INT64_MAX = (1 << 63) - 1
 
 
+def new_one_sm_marks(device) -> torch.Tensor:
+    """agnes_one_sm_* marks before a stream: no P1, no C, no valid candidate."""
+    return torch.tensor([INT64_MAX, INT64_MAX, 0, 0], dtype=torch.int64, device=device)
+
+
+def one_instance_states(sm_scan, sm_apply, sm_finish, marks: torch.Tensor, group=None):
+    """C5 with the State machine: after tally_one_instance[_dedup] wrote this rank's
+    slice codes, the instance's State and the votes' message nibbles
+    (agnes_one_sm_*, include/agnes.h).  Without RoundSkip the vote events move the
+    State only at P1 (first PolkaNil / PolkaValue at State.round in Prevote,
+    state_machine.rs:197-198) and C (first PrecommitValue, :211):
+      scan     every rank's first P1 / C candidates -> all_reduce MIN (2 int64);
+      apply    message nibbles from each vote's position relative to P1 / C, the
+               last valid candidate (:198, :202) and C's round -> all_reduce MAX;
+      finish   the State, identical on every rank.
+    sm_scan(marks) / sm_apply(marks) / sm_finish(marks) run this rank's passes."""
+    multi = dist.is_initialized() and dist.get_world_size(group) > 1
+    sm_scan(marks)
+    if multi:
+        t = marks[:2].to(_device_for(group))
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)        # exchange 1
+        marks[:2].copy_(t.to(marks.device))
+    sm_apply(marks)
+    if multi:
+        t = marks[2:].to(_device_for(group))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)        # exchange 2
+        marks[2:].copy_(t.to(marks.device))
+    sm_finish(marks)
+    return marks
+
+
 def tally_one_instance_dedup(tally_carried, dedup_first, dedup_mask, dedup_reject, n_votes: int,
                              n_vals: int, cfg: abi.Config, n_segments: int, device, base: int = 0,
                              group=None, offsets=None, fold=None):

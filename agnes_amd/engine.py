@@ -169,6 +169,36 @@ class Engine:
         check(self.lib.agnes_fold_counts(self.ctx, _ptr(counts), S, K, _ptr(carry), _ptr(totals), flags,
                                          _stream_handle(stream)), "agnes_fold_counts")
 
+    # -- the State machine of one instance split over slices (C5) -------------
+    def _one_sm_check(self, batch, codes, state, marks):
+        if codes.dtype != torch.uint8 or codes.numel() < batch.n_votes:
+            raise ValueError("codes must be a uint8 tensor of n_votes")
+        if state.numel() < 64 or marks.dtype != torch.int64 or marks.numel() < 4:
+            raise ValueError("state must hold one 64-B agnes_state, marks int64 [4]")
+
+    def one_sm_scan(self, cfg: abi.Config, batch: DeviceBatch, base: int, codes: torch.Tensor,
+                    state: torch.Tensor, marks: torch.Tensor, stream=None):
+        """agnes_one_sm_scan: lowers marks[0..1] to the slice's first P1 / C candidates."""
+        self._one_sm_check(batch, codes, state, marks)
+        b = batch.c()
+        check(self.lib.agnes_one_sm_scan(self.ctx, C.byref(cfg), C.byref(b), base, _ptr(codes), _ptr(state),
+                                         _ptr(marks), _stream_handle(stream)), "agnes_one_sm_scan")
+
+    def one_sm_apply(self, cfg: abi.Config, batch: DeviceBatch, base: int, codes: torch.Tensor,
+                     state: torch.Tensor, marks: torch.Tensor, stream=None):
+        """agnes_one_sm_apply: message nibbles into codes; raises marks[2..3]."""
+        self._one_sm_check(batch, codes, state, marks)
+        b = batch.c()
+        check(self.lib.agnes_one_sm_apply(self.ctx, C.byref(cfg), C.byref(b), base, _ptr(codes), _ptr(state),
+                                          _ptr(marks), _stream_handle(stream)), "agnes_one_sm_apply")
+
+    def one_sm_finish(self, marks: torch.Tensor, state: torch.Tensor, stream=None):
+        """agnes_one_sm_finish: P1, the valid value and C applied to the State."""
+        if state.numel() < 64 or marks.dtype != torch.int64 or marks.numel() < 4:
+            raise ValueError("state must hold one 64-B agnes_state, marks int64 [4]")
+        check(self.lib.agnes_one_sm_finish(self.ctx, _ptr(marks), _ptr(state), _stream_handle(stream)),
+              "agnes_one_sm_finish")
+
     # -- DEDUP for one instance split over slices (C5) --------------------------
     def dedup_first(self, cfg: abi.Config, batch: DeviceBatch, base: int, first: torch.Tensor, stream=None):
         """agnes_dedup_first: first = int64 [2 * max_rounds * n_vals], INT64_MAX-initialised."""

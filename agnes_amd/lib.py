@@ -69,6 +69,9 @@ def load():
         "agnes_last_error_count": ([P, C.POINTER(C.c_uint64)], C.c_int),
         "agnes_lds_bytes_per_wave": ([C.POINTER(abi.Config), C.c_uint32], C.c_int64),
         "agnes_apply_events": ([P, P, C.c_uint32, P, P, P, C.c_uint32, P], C.c_int),
+        "agnes_one_sm_scan": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), C.c_uint64, P, P, P, P], C.c_int),
+        "agnes_one_sm_apply": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), C.c_uint64, P, P, P, P], C.c_int),
+        "agnes_one_sm_finish": ([P, P, P, P], C.c_int),
         "agnes_apply_msgs": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P, P, P], C.c_int),
         "agnes_edge_offsets": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P], C.c_int),
         "agnes_edges": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P], C.c_int),

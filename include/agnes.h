@@ -383,6 +383,32 @@ int agnes_dedup_mask(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_b
 int agnes_dedup_reject(agnes_ctx* ctx, const uint8_t* type_masked, uint64_t n_votes, uint8_t* codes,
                        void* stream);
 
+/* The State machine of ONE instance split into slices (C5 with
+ * AGNES_FLAG_STATE_MACHINE; agnes_amd/dist.py one_instance_states), after the
+ * carried tally wrote the slice's codes.  Without RoundSkip the vote events move
+ * the State only at P1 (the first PolkaNil / PolkaValue at State.round while in
+ * Prevote, state_machine.rs:197-198) and at C (the first PrecommitValue,
+ * :211); every message follows from a vote's position relative to them.
+ *   agnes_one_sm_scan    lowers marks[0] / marks[1] to the slice's first P1 / C
+ *                        candidate (position << 32 | value)
+ *   (the caller min-combines marks[0..1] over the ranks)
+ *   agnes_one_sm_apply   ORs each vote's message nibble into its code; raises
+ *                        marks[2] to the last valid candidate ((position + 1) << 32
+ *                        | value) and marks[3] to C's round + 1
+ *   (the caller max-combines marks[2..3] over the ranks)
+ *   agnes_one_sm_finish  applies P1, the valid value and C to *state.
+ * marks: DEVICE int64[4], initialised to {INT64_MAX, INT64_MAX, 0, 0}; state:
+ * DEVICE, the instance's State before the slice's votes (read by scan / apply,
+ * written by finish).  batch: the slice (round and value columns, n_votes; its
+ * other columns are not read), base = the global index of its first vote;
+ * base + n_votes <= 2^31.  REFERENCE or DEDUP mode, no RoundSkip
+ * (AGNES_E_UNSUPPORTED). */
+int agnes_one_sm_scan(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch, uint64_t base,
+                      const uint8_t* codes, const agnes_state* state, int64_t* marks, void* stream);
+int agnes_one_sm_apply(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch, uint64_t base,
+                       uint8_t* codes, const agnes_state* state, int64_t* marks, void* stream);
+int agnes_one_sm_finish(agnes_ctx* ctx, const int64_t* marks, agnes_state* state, void* stream);
+
 /* Number of votes coded AGNES_CODE_INVALID by the most recent agnes_tally on
  * this context (synchronises the context's stream). */
 int agnes_last_error_count(agnes_ctx* ctx, uint64_t* out);

@@ -107,3 +107,79 @@ class DedupFake:
 
     def reject(self, type_masked: np.ndarray, codes: np.ndarray):
         codes[type_masked == self.MASKED] = abi.CODE_REJECTED
+
+
+class OneSmFake:
+    """CPU stand-in for agnes_one_sm_scan / _apply / _finish (include/agnes.h; TEST
+    INFRASTRUCTURE): the State machine of one instance split into slices, from the
+    slice codes of the carried tally.  Restates state_machine.rs:196-211 for vote
+    events without RoundSkip: P1 = first PolkaNil / PolkaValue at State.round in
+    Prevote, C = first PrecommitValue; messages by position relative to them."""
+
+    MAXM = (1 << 63) - 1
+
+    def __init__(self, state):
+        self.state = state  # abi.STATE_DTYPE record (numpy void), read and written
+
+    def scan(self, codes, round_, value, base, marks):
+        s = self.state
+        if int(s["step"]) == abi.STEP_COMMIT:
+            return
+        e = codes & abi.CODE_EVENT_MASK
+        eqr = round_.astype(np.int64) == int(s["round"])
+        pos = base + np.arange(len(codes), dtype=np.int64)
+        p1 = (int(s["step"]) == abi.STEP_PREVOTE) & eqr & ((e == abi.CODE_POLKA_NIL) | (e == abi.CODE_POLKA_VALUE))
+        if p1.any():
+            j = int(np.argmax(p1))
+            lv = int(value[j]) if e[j] == abi.CODE_POLKA_VALUE else abi.NIL
+            marks[0] = min(int(marks[0]), (int(pos[j]) << 32) | lv)
+        cc = e == abi.CODE_PRECOMMIT_VALUE
+        if cc.any():
+            j = int(np.argmax(cc))
+            marks[1] = min(int(marks[1]), (int(pos[j]) << 32) | int(value[j]))
+
+    def apply(self, codes, round_, value, base, marks):
+        s = self.state
+        if int(s["step"]) == abi.STEP_COMMIT:
+            return
+        C = self.MAXM if int(marks[1]) == self.MAXM else int(marks[1]) >> 32
+        P1 = self.MAXM if int(marks[0]) == self.MAXM else int(marks[0]) >> 32
+        if P1 >= C:
+            P1 = self.MAXM
+        step = int(s["step"])
+        for j in range(len(codes)):
+            e = int(codes[j]) & abi.CODE_EVENT_MASK
+            eqr = int(round_[j]) == int(s["round"])
+            pos = base + j
+            msg = 0
+            if pos < C:
+                if e == abi.CODE_PRECOMMIT_ANY and eqr:
+                    msg = abi.VMSG_TIMEOUT_PRECOMMIT
+                if e == abi.CODE_POLKA_ANY and eqr and step == abi.STEP_PREVOTE and pos < P1:
+                    msg = abi.VMSG_TIMEOUT_PREVOTE
+                if pos == P1:
+                    msg = abi.VMSG_PRECOMMIT_VALUE if e == abi.CODE_POLKA_VALUE else abi.VMSG_PRECOMMIT_NIL
+            elif pos == C:
+                msg = abi.VMSG_DECISION
+                marks[3] = max(int(marks[3]), int(round_[j]) + 1)
+            codes[j] |= msg << abi.CODE_MSG_SHIFT
+            if (e == abi.CODE_POLKA_VALUE and eqr and int(value[j]) != abi.NIL and pos < C
+                    and ((step == abi.STEP_PREVOTE and pos >= P1) or step == abi.STEP_PRECOMMIT)):
+                marks[2] = max(int(marks[2]), ((pos + 1) << 32) | int(value[j]))
+
+    def finish(self, marks):
+        s = self.state
+        if int(s["step"]) == abi.STEP_COMMIT:
+            return
+        m0, m1, m2, m3 = (int(x) for x in marks)
+        C = self.MAXM if m1 == self.MAXM else m1 >> 32
+        P1 = self.MAXM if m0 == self.MAXM else m0 >> 32
+        if P1 < C:
+            s["step"] = abi.STEP_PRECOMMIT
+            if (m0 & 0xFFFFFFFF) != abi.NIL:
+                s["locked_present"], s["locked_round"], s["locked_value"] = 1, s["round"], m0 & 0xFFFFFFFF
+        if m2:
+            s["valid_present"], s["valid_round"], s["valid_value"] = 1, s["round"], m2 & 0xFFFFFFFF
+        if C != self.MAXM:
+            s["step"], s["decided"] = abi.STEP_COMMIT, 1
+            s["decision_round"], s["decision_value"] = m3 - 1, m1 & 0xFFFFFFFF
