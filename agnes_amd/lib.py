@@ -72,6 +72,10 @@ def load():
         "agnes_one_sm_scan": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), C.c_uint64, P, P, P, P], C.c_int),
         "agnes_one_sm_apply": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), C.c_uint64, P, P, P, P], C.c_int),
         "agnes_one_sm_finish": ([P, P, P, P], C.c_int),
+        "agnes_multi_create": ([P, C.c_uint32, P], C.c_int),
+        "agnes_multi_destroy": ([P], None),
+        "agnes_multi_upload_power": ([P, P, C.c_uint32, C.c_uint32, P], C.c_int),
+        "agnes_multi_tally": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P], C.c_int),
         "agnes_apply_msgs": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P, P, P], C.c_int),
         "agnes_edge_offsets": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P], C.c_int),
         "agnes_edges": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P], C.c_int),

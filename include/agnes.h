@@ -452,6 +452,32 @@ int agnes_apply_msgs(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_b
                      void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Native multi-GPU driver: one context, stream and host thread
+ * per device; a HOST batch is cut into contiguous instance ranges balanced by
+ * votes (instances are independent: no collective on the data path), each range
+ * is copied to its device, tallied (agnes_tally) and its codes / States copied
+ * back into the HOST arrays.  The entry a consumer without torch.distributed binds
+ * (agnes_amd/dist.py is the one-process-per-GPU Python equivalent).  A device may
+ * be listed more than once (several contexts on one GPU).
+ * ------------------------------------------------------------------------- */
+typedef struct agnes_multi agnes_multi;
+typedef struct agnes_multi_stats {
+    uint32_t device, i0, i1; /* the range [i0, i1) this device tallied */
+    uint32_t pad;
+    uint64_t n_votes, n_invalid;
+    double h2d_ms, tally_ms, d2h_ms; /* host wall-clock of the three phases */
+} agnes_multi_stats;
+int agnes_multi_create(const int* devices, uint32_t n_devices, agnes_multi** out);
+void agnes_multi_destroy(agnes_multi* m);
+/* agnes_upload_power on every device */
+int agnes_multi_upload_power(agnes_multi* m, const int64_t* power, uint32_t n_sets, uint32_t n_vals,
+                             const int64_t* totals);
+/* batch, codes, states (optional, in/out with AGNES_FLAG_STATE_MACHINE) are HOST
+ * pointers; stats (optional) receives one record per device.  Synchronous. */
+int agnes_multi_tally(agnes_multi* m, const agnes_config* cfg, const agnes_vote_batch* batch, uint8_t* codes,
+                      agnes_state* states, agnes_multi_stats* stats);
+
+/* ---------------------------------------------------------------------------
  * Edge-triggered summary of a coded batch.
  *
  * VoteExecutor::apply is level-triggered (vote_executor.rs:20-36): once a
