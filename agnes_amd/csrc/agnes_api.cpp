@@ -459,6 +459,53 @@ int agnes_one_sm_finish(agnes_ctx* c, const int64_t* marks, agnes_state* state, 
                                          c->num_cus, (hipStream_t)stream));
 }
 
+/* ---------------- validator sets ---------------- */
+
+int agnes_valset_build(agnes_ctx* c, const uint8_t* addr, uint32_t addr_len, const int64_t* power,
+                       const uint32_t* set_of, uint64_t n, uint32_t n_sets, uint32_t* order, uint64_t* set_offsets,
+                       int64_t* power_out, int64_t* totals, uint8_t* addr_out, uint64_t* n_out, void* stream) {
+    if (!c || !n_out || n_sets == 0 || addr_len == 0 || addr_len > 64u || !set_offsets || !totals) return AGNES_E_INVALID;
+    if (n && (!addr || !power || !order || !power_out)) return AGNES_E_INVALID;
+    if (n > (1ull << 30)) return AGNES_E_UNSUPPORTED;
+    AGNES_TRY(hipSetDevice(c->device));
+    const hipStream_t st = (hipStream_t)stream;
+    AGNES_ORDER(c, st);
+    uint32_t N = 2048u; /* the sort's power of two (>= one LDS tile) */
+    while (N < n) N <<= 1;
+    uint32_t* idx = nullptr;
+    uint64_t* pos = nullptr;
+    uint64_t* scr = nullptr;
+    uint32_t* set_out = nullptr;
+    hipError_t e = hipMalloc(&idx, 4ull * N);
+    if (e == hipSuccess) e = hipMalloc(&pos, 8ull * (N + 1ull));
+    if (e == hipSuccess) e = hipMalloc(&scr, 8ull * (agnes_edges_scratch_words(N) + 1u));
+    if (e == hipSuccess) e = hipMalloc(&set_out, 4ull * (n ? n : 1u));
+    if (e == hipSuccess)
+        e = agnes_launch_valset_build(addr, addr_len, power, set_of, (uint32_t)n, n_sets, idx, N, pos, scr, set_out,
+                                      order, power_out, addr_out, set_offsets, totals, st);
+    uint64_t m = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&m, pos + N, sizeof(m), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(idx);
+    (void)hipFree(pos);
+    (void)hipFree(scr);
+    (void)hipFree(set_out);
+    if (e != hipSuccess) return status_of(e);
+    *n_out = m;
+    return AGNES_OK;
+}
+
+int agnes_valset_find(agnes_ctx* c, const uint8_t* sorted_addr, uint32_t addr_len, const uint64_t* set_offsets,
+                      uint32_t n_sets, const uint8_t* q_addr, const uint32_t* q_set, uint64_t n_q, uint64_t* out,
+                      void* stream) {
+    if (!c || !set_offsets || addr_len == 0 || addr_len > 64u || (n_q && (!q_addr || !out || !sorted_addr)))
+        return AGNES_E_INVALID;
+    AGNES_TRY(hipSetDevice(c->device));
+    AGNES_ORDER(c, (hipStream_t)stream);
+    return status_of(agnes_launch_valset_find(sorted_addr, addr_len, set_offsets, n_sets, q_addr, q_set, n_q, out,
+                                              (hipStream_t)stream));
+}
+
 /* ---------------- edge-triggered summary ---------------- */
 
 static bool edges_args_ok(const agnes_config* cfg, const agnes_vote_batch* b, const uint8_t* codes) {

@@ -100,6 +100,14 @@ hipError_t agnes_launch_apply_msgs(const agnes_vote_batch* vb, const uint8_t* ki
 /* pass 0 scan, 1 apply, 2 finish (agnes_onesm.hip) */
 hipError_t agnes_launch_one_sm(int pass, const uint8_t* codes, const uint8_t* round, const uint32_t* value, uint64_t n,
                                uint64_t base, agnes_state* state, int64_t* marks, int num_cus, hipStream_t stream);
+/* validator sets (agnes_valset.hip) */
+hipError_t agnes_launch_valset_build(const uint8_t* addr, uint32_t addr_len, const int64_t* power, const uint32_t* set_of,
+                                     uint32_t n, uint32_t n_sets, uint32_t* idx, uint32_t N, uint64_t* pos,
+                                     uint64_t* scan_scratch, uint32_t* set_out, uint32_t* order, int64_t* power_out,
+                                     uint8_t* addr_out, uint64_t* set_offsets, int64_t* totals, hipStream_t st);
+hipError_t agnes_launch_valset_find(const uint8_t* sorted_addr, uint32_t addr_len, const uint64_t* set_offsets,
+                                    uint32_t n_sets, const uint8_t* q_addr, const uint32_t* q_set, uint64_t n_q,
+                                    uint64_t* out, hipStream_t st);
 hipError_t agnes_launch_gen(const agnes_gen_params* p, const uint64_t* d_offsets, uint64_t n_votes,
                             uint32_t* instance, uint8_t* round, uint8_t* type, uint32_t* value,
                             uint32_t* validator, hipStream_t stream);

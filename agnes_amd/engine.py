@@ -169,6 +169,40 @@ class Engine:
         check(self.lib.agnes_fold_counts(self.ctx, _ptr(counts), S, K, _ptr(carry), _ptr(totals), flags,
                                          _stream_handle(stream)), "agnes_fold_counts")
 
+    # -- validator sets ----------------------------------
+    def valset_build(self, addr: torch.Tensor, power: torch.Tensor, set_of: Optional[torch.Tensor], n_sets: int,
+                     stream=None):
+        """agnes_valset_build: addr uint8 [n, L], power int64 [n], set_of int32 [n]
+        or None.  Returns (order int32 [m], set_offsets int64 [n_sets + 1], power_out
+        int64 [m], totals int64 [n_sets], addr_out uint8 [m, L])."""
+        if addr.dtype != torch.uint8 or addr.dim() != 2 or not addr.is_contiguous():
+            raise ValueError("addr must be a contiguous uint8 [n, addr_len] tensor")
+        n, L = addr.shape
+        if power.dtype != torch.int64 or power.numel() != n or (set_of is not None and set_of.numel() != n):
+            raise ValueError("power int64 [n], set_of int32 [n]")
+        dev = self.device
+        order = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        offs = torch.empty(n_sets + 1, dtype=torch.int64, device=dev)
+        pout = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        tot = torch.empty(n_sets, dtype=torch.int64, device=dev)
+        aout = torch.empty((max(n, 1), L), dtype=torch.uint8, device=dev)
+        m = C.c_uint64(0)
+        check(self.lib.agnes_valset_build(self.ctx, _ptr(addr), L, _ptr(power), _ptr(set_of), n, n_sets,
+                                          _ptr(order), _ptr(offs), _ptr(pout), _ptr(tot), _ptr(aout), C.byref(m),
+                                          _stream_handle(stream)), "agnes_valset_build")
+        k = m.value
+        return order[:k], offs, pout[:k], tot, aout[:k]
+
+    def valset_find(self, sorted_addr: torch.Tensor, set_offsets: torch.Tensor, q_addr: torch.Tensor,
+                    q_set: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        """agnes_valset_find: int64 index per query (-1 when absent)."""
+        n_q, L = q_addr.shape
+        out = torch.empty(max(n_q, 1), dtype=torch.int64, device=self.device)
+        check(self.lib.agnes_valset_find(self.ctx, _ptr(sorted_addr), L, _ptr(set_offsets), set_offsets.numel() - 1,
+                                         _ptr(q_addr), _ptr(q_set), n_q, _ptr(out), _stream_handle(stream)),
+              "agnes_valset_find")
+        return out[:n_q]
+
     # -- the State machine of one instance split over slices (C5) -------------
     def _one_sm_check(self, batch, codes, state, marks):
         if codes.dtype != torch.uint8 or codes.numel() < batch.n_votes:

@@ -452,6 +452,37 @@ int agnes_apply_msgs(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_b
                      void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Validator sets: ValidatorSet, validators.rs:23-56 -- the
+ * intended behaviour; the file does not compile, so no reference output pins it.
+ * A set keeps its validators sorted by address (ValidatorSet::sort, :49-55;
+ * Validator::address = the public key, :15-17) without exact duplicates
+ * (Vec::dedup, a derived PartialEq: same address and power).
+ *
+ * agnes_valset_build builds n_sets sets at once from one flat list: validator i has
+ * address addr[i * addr_len ..] (fixed length, 1..64 B), power power[i] and set
+ * set_of[i] (NULL: set 0; a set id >= n_sets drops the validator).  Outputs, sets
+ * consecutive:
+ *   order[k]        the input index of output validator k (sorted by address; equal
+ *                   addresses by power -- sort_unstable_by leaves them in any order,
+ *                   this is one -- then by input index; a duplicate keeps its first)
+ *   power_out[k]    power[order[k]]: the power row agnes_upload_power takes
+ *   addr_out[k]     (optional) the sorted addresses, for agnes_valset_find
+ *   set_offsets[s]  [n_sets + 1]: set s is outputs [set_offsets[s], set_offsets[s+1])
+ *   totals[s]       the wrapping sum of set s's powers (VoteExecutor::new's
+ *                   total_weight, vote_executor.rs:13)
+ *   *n_out (HOST)   the number of outputs.
+ * DEVICE pointers except n_out; n <= 2^30; synchronous.
+ * agnes_valset_find: for query q (address q_addr[q * addr_len ..], set q_set[q] or 0)
+ * the index of its validator in the built set (ValidatorSet::update / remove: "find
+ * val in list", :39, :44), UINT64_MAX when absent. */
+int agnes_valset_build(agnes_ctx* ctx, const uint8_t* addr, uint32_t addr_len, const int64_t* power,
+                       const uint32_t* set_of, uint64_t n, uint32_t n_sets, uint32_t* order, uint64_t* set_offsets,
+                       int64_t* power_out, int64_t* totals, uint8_t* addr_out, uint64_t* n_out, void* stream);
+int agnes_valset_find(agnes_ctx* ctx, const uint8_t* sorted_addr, uint32_t addr_len, const uint64_t* set_offsets,
+                      uint32_t n_sets, const uint8_t* q_addr, const uint32_t* q_set, uint64_t n_q, uint64_t* out,
+                      void* stream);
+
+/* ---------------------------------------------------------------------------
  * Native multi-GPU driver: one context, stream and host thread
  * per device; a HOST batch is cut into contiguous instance ranges balanced by
  * votes (instances are independent: no collective on the data path), each range

@@ -1,3 +1,4 @@
+#define _GNU_SOURCE
 /*
  * agnes_oracle.c — scalar CPU restatement of Liamsi/agnes (clean-room, plain C).
  * TEST INFRASTRUCTURE ONLY (see agnes_oracle.h): the checker of the HIP engine
@@ -549,6 +550,69 @@ int orc_apply_msgs(const agnes_config* cfg, const agnes_vote_batch* b, const orc
     }
     free(cnt);
     if (n_invalid) *n_invalid = bad;
+    return AGNES_OK;
+}
+
+/* ValidatorSet::new (validators.rs:28-31) with sort + dedup (:49-55), the
+ * intended behaviour (the file does not compile): per set, validators sorted by
+ * address (Validator::address = public key, :15-17), equal addresses by power then
+ * input index (one of the orders sort_unstable_by allows, made deterministic),
+ * exact duplicates (address and power, a derived PartialEq) dropped keeping the
+ * first; totals = the wrapping sum (vote_executor.rs:13's total_weight).  Same
+ * contract as agnes_valset_build (include/agnes.h), host pointers. */
+typedef struct vs_ctx {
+    const uint8_t* addr;
+    const int64_t* power;
+    const uint32_t* set_of;
+    uint32_t addr_len;
+} vs_ctx;
+
+static int vs_cmp3(const vs_ctx* k, uint32_t i, uint32_t j) {
+    const uint32_t si = k->set_of ? k->set_of[i] : 0u, sj = k->set_of ? k->set_of[j] : 0u;
+    if (si != sj) return si < sj ? -1 : 1;
+    const int c = memcmp(k->addr + (size_t)i * k->addr_len, k->addr + (size_t)j * k->addr_len, k->addr_len);
+    if (c) return c < 0 ? -1 : 1;
+    if (k->power[i] != k->power[j]) return k->power[i] < k->power[j] ? -1 : 1;
+    return 0;
+}
+
+static int vs_qcmp(const void* a, const void* b, void* arg) {
+    const uint32_t i = *(const uint32_t*)a, j = *(const uint32_t*)b;
+    const int c = vs_cmp3((const vs_ctx*)arg, i, j);
+    return c ? c : (i < j ? -1 : (i > j ? 1 : 0));
+}
+
+int orc_valset_build(const uint8_t* addr, uint32_t addr_len, const int64_t* power, const uint32_t* set_of,
+                     uint64_t n, uint32_t n_sets, uint32_t* order, uint64_t* set_offsets, int64_t* power_out,
+                     int64_t* totals, uint64_t* n_out) {
+    if (!n_out || !set_offsets || !totals || n_sets == 0 || addr_len == 0 || (n && (!addr || !power || !order)))
+        return AGNES_E_INVALID;
+    uint32_t* idx = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+    if (!idx) return AGNES_E_NOMEM;
+    for (uint64_t i = 0; i < n; ++i) idx[i] = (uint32_t)i;
+    vs_ctx k = {addr, power, set_of, addr_len};
+    qsort_r(idx, n, sizeof(uint32_t), vs_qcmp, &k);
+    uint64_t m = 0;
+    for (uint64_t t = 0; t < n; ++t) {
+        const uint32_t a = idx[t];
+        if ((set_of ? set_of[a] : 0u) >= n_sets) continue;
+        if (t > 0 && vs_cmp3(&k, idx[t - 1], a) == 0) continue; /* Vec::dedup */
+        order[m] = a;
+        if (power_out) power_out[m] = power[a];
+        ++m;
+    }
+    uint64_t o = 0;
+    for (uint32_t s = 0; s <= n_sets; ++s) {
+        while (o < m && (set_of ? set_of[order[o]] : 0u) < s) ++o;
+        set_offsets[s] = s == n_sets ? m : o;
+    }
+    for (uint32_t s = 0; s < n_sets; ++s) {
+        int64_t t = 0;
+        for (uint64_t q = set_offsets[s]; q < set_offsets[s + 1]; ++q) t = wadd(t, power[order[q]]);
+        totals[s] = t;
+    }
+    free(idx);
+    *n_out = m;
     return AGNES_OK;
 }
 

@@ -96,6 +96,11 @@ int orc_apply_msgs(const agnes_config* cfg, const agnes_vote_batch* batch, const
                    const int32_t* pol_round, uint8_t* codes, agnes_state* states, agnes_message* msgs,
                    uint64_t* n_invalid);
 
+/* validator sets (agnes_valset_build's contract, host pointers) */
+int orc_valset_build(const uint8_t* addr, uint32_t addr_len, const int64_t* power, const uint32_t* set_of,
+                     uint64_t n, uint32_t n_sets, uint32_t* order, uint64_t* set_offsets, int64_t* power_out,
+                     int64_t* totals, uint64_t* n_out);
+
 /* edge-triggered summary of coded votes (agnes_edge_offsets + agnes_edges):
  * offsets[n_instances + 1]; out NULL = count only */
 int orc_edges(const agnes_config* cfg, const agnes_vote_batch* batch, const uint8_t* codes,

@@ -60,6 +60,8 @@ def lib():
                                        C.POINTER(OrcPower), P, P, C.POINTER(C.c_uint64), P, C.c_int]
         L.orc_events.argtypes = [C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P]
         L.orc_apply_events.argtypes = [P, C.c_uint32, P, P, P, C.c_uint32]
+        L.orc_valset_build.argtypes = [P, C.c_uint32, P, P, C.c_uint64, C.c_uint32, P, P, P, P,
+                                       C.POINTER(C.c_uint64)]
         L.orc_apply_msgs.argtypes = [C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), C.POINTER(OrcPower),
                                      P, P, P, P, P, C.POINTER(C.c_uint64)]
         L.orc_edges.argtypes = [C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P]
@@ -255,6 +257,24 @@ def apply_msgs(cfg: abi.Config, b, kinds: np.ndarray, pol_round: Optional[np.nda
     if rc != 0:
         raise RuntimeError(f"orc_apply_msgs rc={rc}")
     return codes[:n], st, msgs[:n], int(nbad.value)
+
+
+def valset_build(addr: np.ndarray, power: np.ndarray, set_of: Optional[np.ndarray], n_sets: int):
+    """orc_valset_build: (order u32 [m], set_offsets u64 [n_sets + 1], power_out i64 [m], totals i64)"""
+    addr = np.ascontiguousarray(addr, dtype=np.uint8)
+    n, L = addr.shape
+    power = np.ascontiguousarray(power, dtype=np.int64)
+    so = None if set_of is None else np.ascontiguousarray(set_of, dtype=np.uint32)
+    order = np.zeros(max(n, 1), np.uint32)
+    offs = np.zeros(n_sets + 1, np.uint64)
+    pout = np.zeros(max(n, 1), np.int64)
+    tot = np.zeros(n_sets, np.int64)
+    m = C.c_uint64(0)
+    rc = lib().orc_valset_build(_p(addr), L, _p(power), _p(so), n, n_sets, _p(order), _p(offs), _p(pout), _p(tot),
+                                C.byref(m))
+    assert rc == 0, rc
+    k = m.value
+    return order[:k], offs, pout[:k], tot
 
 
 def state_apply(state: abi.StateRec, round_: int, ev: abi.Event, flags: int = 0):
