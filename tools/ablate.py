@@ -32,7 +32,6 @@ def _lane_now(t):
         j = t.index(b, i)
         blk = re.sub(r"\blane\b", "lane_now()", t[i:j])
         return t[:i] + blk + t[j:]
-    t = sub_in(t, "    auto dma_values = [&]", "    auto finalize = [&]")
     t = sub_in(t, "    auto finalize = [&]", "    Hdr H, N;")
     t = sub_in(t, "                if (rc == 0u && lane < m) { /* instance records */", "                if (SM && smf) {")
     t = sub_in(t, "                if (SM && smf) { /* the State machine", "                /* the next batch")

@@ -12,19 +12,25 @@ usage: tools/pmc_traffic.py FETCH.csv WRITE.csv CONFIG OUT.json
 """
 import csv
 import json
+import re
 import statistics
 import sys
 
-# engine kernel name (agnes_kernel_times) -> substring of the demangled symbol
+# engine kernel name (agnes_kernel_times) -> regex on the demangled symbol
 KERNELS = {
-    "flow": "agnes::flow::flow<",
-    "sweep_walk": "agnes::sweep::sweep<",
-    "tally_fast": "agnes::fast::tally_fast<",
-    "apply_codes": "agnes::apply::apply_codes<",
-    "tally_list": "agnes::tally_kernel<",
-    "edge_walk": "agnes::edges::edge_walk",
-    "event_count": "agnes::events::event_count",
-    "event_emit": "agnes::events::event_emit",
+    "flow": r"agnes::flow::flow<",
+    "sweep_walk": r"agnes::sweep::sweep<\w+, \w+, true>",
+    "sweep": r"agnes::sweep::sweep<\w+, \w+, false>",
+    "tally_fast": r"agnes::fast::tally_fast<",
+    "apply_codes": r"agnes::apply::apply_codes<",
+    "tally_list": r"agnes::tally_kernel<true, \w+, \w+, \w+, true,",
+    "tally_wide": r"agnes::tally_kernel<true, \w+, \w+, \w+, false,",
+    "fold": r"agnes::fold::fold_kernel",
+    "dedup_first": r"agnes::dedup::first_kernel",
+    "dedup_mask": r"agnes::dedup::mask_kernel",
+    "dedup_reject": r"agnes::dedup::reject_kernel",
+    "edge_walk": r"agnes::edges::edge_walk",
+    "event_walk": r"agnes::events::event_walk",
 }
 
 
@@ -34,8 +40,8 @@ def per_launch(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        for k, sub in KERNELS.items():
-            if sub in r["Kernel_Name"]:
+        for k, pat in KERNELS.items():
+            if re.search(pat, r["Kernel_Name"]):
                 vals.setdefault(k, []).append(float(r["Counter_Value"]))
     return {k: (statistics.median(v), len(v)) for k, v in vals.items()}
 
