@@ -57,6 +57,8 @@ VARIANTS = {
                         l = sn > tn ? 2u : l;
                         l = sv > tv ? 3u : l;""", "                        uint32_t l = (sv ^ sn ^ (uint32_t)tv ^ (uint32_t)tn ^ (uint32_t)ta) & 3u;")],
     "k4nowrite": [("if (ballot((lk0 | lk1 | aC0 | aC1 | v0 | v1) != 0u)) {", "if (false) {")],
+    "k4noval": [("                            if (v0) { /* valid (:198, :202): the last candidate */", "                            if (false) {"),
+                ("                            if (v1) {\n                                const uint32_t b = (31u", "                            if (false) {\n                                const uint32_t b = (31u")],
     "k4fast": [("if (!ballot(inA || inB)) { /* no P1 or C inside any unit: whole-unit masks */",
                 "if (true) { (void)inA; (void)inB;")],
     "k4norec": [("if (!crossedC && bC < 4) rk[R_C] = pos + (uint32_t)bC;", "(void)rk;"),

@@ -4,11 +4,11 @@
 # usage: tools/gpu.sh TIMEOUT "command" [files to clear...]
 T=$1; CMD=$2; shift 2
 for f in "$@"; do rm -f "/root/repo/gpurun_out/$f"; done
-for attempt in 1 2 3 4; do
+for attempt in 1 2 3 4 5 6 7 8; do
   /usr/local/graft/bin/gpurun --timeout "$T" -- "$CMD" > /root/repo/gpurun_out/call.log 2>&1
   rc=$?
   if grep -q "status=transient\|backing off" /root/repo/gpurun_out/call.log; then
-    echo "[gpu.sh] transient (attempt $attempt), waiting"; sleep 45; continue
+    echo "[gpu.sh] transient (attempt $attempt), waiting"; sleep 90; continue
   fi
   break
 done
