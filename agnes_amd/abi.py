@@ -162,3 +162,9 @@ def new_states(n: int, height: int = 1, step: int = STEP_NEW_ROUND, round_: int 
     s["round"] = round_
     s["step"] = step
     return s
+
+
+# wire format (include/agnes.h agnes_wire_vote)
+WIRE_BYTES = 104
+WIRE_MAGIC = 0x31564741
+WIRE_OK, WIRE_BAD_FORMAT, WIRE_BAD_VALIDATOR, WIRE_BAD_SIGNATURE, WIRE_BAD_HEIGHT = 0, 1, 2, 3, 4

@@ -459,6 +459,26 @@ int agnes_one_sm_finish(agnes_ctx* c, const int64_t* marks, agnes_state* state, 
                                          c->num_cus, (hipStream_t)stream));
 }
 
+/* ---------------- wire format + Ed25519 ---------------- */
+
+int agnes_wire_ingest(agnes_ctx* c, const agnes_wire_vote* records, uint64_t n, const uint8_t* pubkeys,
+                      uint32_t n_sets, uint32_t n_vals, const uint32_t* instance_set, uint32_t n_instances,
+                      int64_t height, uint32_t max_rounds, uint32_t* instance, uint8_t* round, uint8_t* type,
+                      uint32_t* value, uint32_t* validator, uint8_t* verdict, void* stream) {
+    if (!c || max_rounds == 0u || max_rounds > 256u) return AGNES_E_INVALID;
+    if (n && (!records || !instance || !round || !type || !value || !validator || !verdict)) return AGNES_E_INVALID;
+    if (n && n_sets && n_vals && !pubkeys) return AGNES_E_INVALID;
+    if (((uintptr_t)records & 7u) || ((uintptr_t)pubkeys & 15u)) return AGNES_E_INVALID;
+    if (n > (1ull << 40)) return AGNES_E_UNSUPPORTED;
+    AGNES_TRY(hipSetDevice(c->device));
+    const hipStream_t st = (hipStream_t)stream;
+    AGNES_ORDER(c, st);
+    agnes_wire_args a{records, n, pubkeys, n_sets, n_vals, instance_set, n_instances, max_rounds, height,
+                      instance, value, validator, round, type, verdict};
+    AgnesKt kt("wire_ingest", st);
+    return status_of(agnes_launch_wire_ingest(&a, st));
+}
+
 /* ---------------- validator sets ---------------- */
 
 int agnes_valset_build(agnes_ctx* c, const uint8_t* addr, uint32_t addr_len, const int64_t* power,

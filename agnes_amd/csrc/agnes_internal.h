@@ -108,6 +108,18 @@ hipError_t agnes_launch_valset_build(const uint8_t* addr, uint32_t addr_len, con
 hipError_t agnes_launch_valset_find(const uint8_t* sorted_addr, uint32_t addr_len, const uint64_t* set_offsets,
                                     uint32_t n_sets, const uint8_t* q_addr, const uint32_t* q_set, uint64_t n_q,
                                     uint64_t* out, hipStream_t st);
+struct agnes_wire_args {
+    const agnes_wire_vote* records;
+    uint64_t n;
+    const uint8_t* pubkeys;
+    uint32_t n_sets, n_vals;
+    const uint32_t* instance_set;
+    uint32_t n_instances, max_rounds;
+    int64_t height;
+    uint32_t *instance, *value, *validator;
+    uint8_t *round, *type, *verdict;
+};
+hipError_t agnes_launch_wire_ingest(const agnes_wire_args* a, hipStream_t st);
 hipError_t agnes_launch_gen(const agnes_gen_params* p, const uint64_t* d_offsets, uint64_t n_votes,
                             uint32_t* instance, uint8_t* round, uint8_t* type, uint32_t* value,
                             uint32_t* validator, hipStream_t stream);

@@ -169,6 +169,38 @@ class Engine:
         check(self.lib.agnes_fold_counts(self.ctx, _ptr(counts), S, K, _ptr(carry), _ptr(totals), flags,
                                          _stream_handle(stream)), "agnes_fold_counts")
 
+    # -- wire format + Ed25519 ---------------------------
+    def wire_ingest(self, records: torch.Tensor, pubkeys: torch.Tensor, n_sets: int, n_vals: int, height: int,
+                    max_rounds: int, offsets: torch.Tensor, instance_set: Optional[torch.Tensor] = None,
+                    stream=None):
+        """agnes_wire_ingest: records uint8 [n, 104] (include/agnes.h agnes_wire_vote),
+        pubkeys uint8 [n_sets * n_vals, 32] (the validators' keys, set-major).
+        Returns (DeviceBatch over the decoded columns with the caller's instance
+        offsets, verdict uint8 [n]); a record that failed has type 0xFF, so the tally
+        codes it INVALID."""
+        if records.dtype != torch.uint8 or records.dim() != 2 or records.shape[1] != abi.WIRE_BYTES \
+                or not records.is_contiguous():
+            raise ValueError("records must be a contiguous uint8 [n, 104] tensor")
+        if pubkeys.dtype != torch.uint8 or not pubkeys.is_contiguous() or pubkeys.numel() < 32 * n_sets * n_vals:
+            raise ValueError("pubkeys must be a contiguous uint8 tensor of n_sets * n_vals * 32 bytes")
+        n = records.shape[0]
+        dev = self.device
+        cols = dict(instance=torch.empty(max(n, 4), dtype=torch.int32, device=dev),
+                    round=torch.empty(max(n, 4), dtype=torch.uint8, device=dev),
+                    type=torch.empty(max(n, 4), dtype=torch.uint8, device=dev),
+                    value=torch.empty(max(n, 4), dtype=torch.int32, device=dev),
+                    validator=torch.empty(max(n, 4), dtype=torch.int32, device=dev))
+        verdict = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+        n_inst = 0 if instance_set is None else instance_set.numel()
+        check(self.lib.agnes_wire_ingest(self.ctx, _ptr(records), n, _ptr(pubkeys), n_sets, n_vals,
+                                         _ptr(instance_set), n_inst, height, max_rounds,
+                                         _ptr(cols["instance"]), _ptr(cols["round"]), _ptr(cols["type"]),
+                                         _ptr(cols["value"]), _ptr(cols["validator"]), _ptr(verdict),
+                                         _stream_handle(stream)), "agnes_wire_ingest")
+        b = DeviceBatch(cols["instance"], cols["round"], cols["type"], cols["value"], cols["validator"],
+                        offsets, instance_set, None, n)
+        return b, verdict[:n]
+
     # -- validator sets (SURVEY.md §8(f) 3) ----------------------------------
     def valset_build(self, addr: torch.Tensor, power: torch.Tensor, set_of: Optional[torch.Tensor], n_sets: int,
                      stream=None):

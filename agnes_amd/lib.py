@@ -79,6 +79,8 @@ def load():
         "agnes_valset_build": ([P, P, C.c_uint32, P, P, C.c_uint64, C.c_uint32, P, P, P, P, P,
                                 C.POINTER(C.c_uint64), P], C.c_int),
         "agnes_valset_find": ([P, P, C.c_uint32, P, C.c_uint32, P, P, C.c_uint64, P, P], C.c_int),
+        "agnes_wire_ingest": ([P, P, C.c_uint64, P, C.c_uint32, C.c_uint32, P, C.c_uint32, C.c_int64, C.c_uint32,
+                               P, P, P, P, P, P, P], C.c_int),
         "agnes_apply_msgs": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P, P, P], C.c_int),
         "agnes_edge_offsets": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P], C.c_int),
         "agnes_edges": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P], C.c_int),

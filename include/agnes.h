@@ -483,6 +483,49 @@ int agnes_valset_find(agnes_ctx* ctx, const uint8_t* sorted_addr, uint32_t addr_
                       void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Wire format and signature verification.  The reference has
+ * neither: its README (README.md:8-14, 36-41) leaves the wire format and the
+ * signature check to the consumer, and Validator carries the public key the
+ * votes are checked against (validators.rs:4-8, 15-17: address() = public_key).
+ * A signed vote is one 104-byte little-endian record: the 40 sign-bytes
+ * (magic .. pad) followed by the Ed25519 signature R || S over them (RFC 8032).
+ * ------------------------------------------------------------------------- */
+#define AGNES_WIRE_MAGIC 0x31564741u /* "AGV1" */
+#define AGNES_WIRE_SIGNED_BYTES 40u
+typedef struct agnes_wire_vote {
+    uint32_t magic;     /* AGNES_WIRE_MAGIC                                   */
+    uint32_t instance;  /* the instance id of the batch the vote belongs to  */
+    int64_t height;     /* State.height (state_machine.rs:8)                  */
+    int64_t round;      /* Vote.round (lib.rs:24)                             */
+    uint32_t validator; /* index into the instance's validator set           */
+    uint32_t value;     /* value_id, AGNES_NIL = nil (Vote.value: Option<Value>) */
+    uint8_t type;       /* 0 prevote, 1 precommit (VoteType, lib.rs:15-19)    */
+    uint8_t pad[7];     /* zero                                               */
+    uint8_t sig[64];    /* Ed25519 R || S over bytes 0 .. 39                  */
+} agnes_wire_vote;
+enum {
+    AGNES_WIRE_OK = 0,
+    AGNES_WIRE_BAD_FORMAT = 1,    /* magic, type > 1, pad != 0, round outside [0, max_rounds) */
+    AGNES_WIRE_BAD_VALIDATOR = 2, /* no such set / validator for the instance                */
+    AGNES_WIRE_BAD_SIGNATURE = 3, /* S >= L, the key decodes to no point, or [S]B - [k]A != R */
+    AGNES_WIRE_BAD_HEIGHT = 4     /* height != the batch's height                             */
+};
+/* agnes_wire_ingest: decode and verify n records into the tally's SoA columns, one
+ * record per lane.  The key of record i is pubkeys[(set * n_vals + validator) * 32 ..]
+ * with set = instance_set[instance] (instance < n_instances, else BAD_VALIDATOR) or,
+ * without instance_set, instance % n_sets.  Signature check: RFC 8032 §5.1.7 in the
+ * cofactorless form of OpenSSL 3.0 (reject S >= L; decode A per §5.1.3; accept iff
+ * encode([S]B - [k]A) == R, k = SHA-512(R || A || sign-bytes) mod L).  Out, in record
+ * order: instance, value, validator as decoded; round (low byte) and type for an
+ * accepted record, round 0 and type 0xFF (coded INVALID by agnes_tally) for any
+ * other; verdict[i] = AGNES_WIRE_*.  All pointers DEVICE; records 8-B aligned.
+ * Asynchronous on `stream`. */
+int agnes_wire_ingest(agnes_ctx* ctx, const agnes_wire_vote* records, uint64_t n, const uint8_t* pubkeys,
+                      uint32_t n_sets, uint32_t n_vals, const uint32_t* instance_set, uint32_t n_instances,
+                      int64_t height, uint32_t max_rounds, uint32_t* instance, uint8_t* round, uint8_t* type,
+                      uint32_t* value, uint32_t* validator, uint8_t* verdict, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Native multi-GPU driver: one context, stream and host thread
  * per device; a HOST batch is cut into contiguous instance ranges balanced by
  * votes (instances are independent: no collective on the data path), each range
