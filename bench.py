@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import struct
 import os
 import sys
 import time
@@ -86,6 +87,10 @@ WORKLOADS = {
                          dup_permille=100, equiv_permille=100),
                 power=(abi.POWER_ZIPF, 1, 1_000_000, 1), mode=abi.MODE_DEDUP, flags=0,
                 max_rounds=1, scaling="strong", one_instance=True, segments=1024),
+    # signed wire records -> verified SoA columns (not a BASELINE config)
+    "wire": dict(desc="wire ingest: 104-byte signed vote records (Ed25519, OpenSSL-made fixture records "
+                      "replicated to 2^20 per GPU, 48 of every 92 valid) -> verified SoA columns",
+                 records=1 << 20, scaling="weak", wire=True),
 }
 
 
@@ -225,6 +230,8 @@ def main():
 
     w = WORKLOADS[args.config]
     eng = Engine(local)
+    if w.get("wire"):
+        return bench_wire(args, w, eng, rank, world)
     if w.get("one_instance"):
         return bench_one_instance(args, w, eng, rank, world)
     shard = adist.make_shard(w["gen"], rank, world, strong=w["scaling"] == "strong")
@@ -498,6 +505,132 @@ def bench_one_instance(args, w, eng, rank, world):
             out["cpu_check_equal"] = bool(np.array_equal(codes[: hi - lo].cpu().numpy(), want[lo:hi]))
         print(json.dumps(out), flush=True)
     if world > 1:
+        dist.destroy_process_group()
+
+
+
+def openssl_verifier():
+    """Ed25519 verification by the host's OpenSSL 3 libcrypto (EVP_DigestVerify) over
+    ctypes: the CPU baseline of the wire config (ctypes releases the GIL, so one
+    Python thread per CPU verifies in parallel)."""
+    import ctypes as C
+    import ctypes.util
+    name = ctypes.util.find_library("crypto") or "libcrypto.so.3"
+    lc = C.CDLL(name)
+    lc.EVP_PKEY_new_raw_public_key.restype = C.c_void_p
+    lc.EVP_PKEY_new_raw_public_key.argtypes = [C.c_int, C.c_void_p, C.c_char_p, C.c_size_t]
+    lc.EVP_MD_CTX_new.restype = C.c_void_p
+    lc.EVP_MD_CTX_free.argtypes = [C.c_void_p]
+    lc.EVP_MD_CTX_reset.argtypes = [C.c_void_p]
+    lc.EVP_DigestVerifyInit.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    lc.EVP_DigestVerify.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]
+    lc.EVP_PKEY_free.argtypes = [C.c_void_p]
+    EVP_PKEY_ED25519 = 1087
+
+    def verify_many(items):
+        ctx = lc.EVP_MD_CTX_new()
+        keys = {}
+        out = []
+        for pub, msg, sig in items:
+            k = keys.get(pub)
+            if k is None:
+                k = keys[pub] = lc.EVP_PKEY_new_raw_public_key(EVP_PKEY_ED25519, None, pub, 32)
+            lc.EVP_MD_CTX_reset(ctx)  # a one-shot Ed25519 verify finalizes the context
+            lc.EVP_DigestVerifyInit(ctx, None, None, None, k)
+            out.append(lc.EVP_DigestVerify(ctx, sig, 64, msg, len(msg)) == 1)
+        for k in keys.values():
+            lc.EVP_PKEY_free(k)
+        lc.EVP_MD_CTX_free(ctx)
+        return out
+    return verify_many, name
+
+
+def bench_wire(args, w, eng, rank, world):
+    """--config wire: agnes_wire_ingest over 2^20 signed records per
+    GPU (weak scaling), records resident in HBM; value = records verified and decoded
+    per second over all ranks."""
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "wire_ed25519.json")))
+    recs = [bytes.fromhex(r) for r in g["records"]]
+    pubs = b"".join(bytes.fromhex(p) for p in g["pubkeys"])
+    n = w["records"]
+    reps = (n + len(recs) - 1) // len(recs)
+    host = np.frombuffer(b"".join(recs) * reps, dtype=np.uint8).reshape(-1, abi.WIRE_BYTES)[:n].copy()
+    dev = eng.device
+    rt = torch.from_numpy(host).to(dev)
+    kt = torch.from_numpy(np.frombuffer(pubs, dtype=np.uint8).copy()).to(dev)
+    offsets = torch.tensor([0, n], dtype=torch.int64, device=dev)
+
+    def step():
+        return eng.wire_ingest(rt, kt, 1, g["n_vals"], g["height"], 4, offsets)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    eng.kernel_timing(True)
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    ktimes = eng.kernel_times()
+    eng.kernel_timing(False)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        b, verdict = step()
+    torch.cuda.synchronize()
+    elapsed = adist.max_over_ranks(time.perf_counter() - t0)
+    total = adist.sum_over_ranks(n)
+    if rank == 0:
+        launches, tot = ktimes["wire_ingest"]
+        avg = tot / max(launches, 1)
+        v = verdict.cpu().numpy()
+        want_ok = np.tile(np.array(g["openssl_verifies"], dtype=bool), reps)[:n]
+        ab = 151 * n  # record 104 + key 32 in, 14-B columns + verdict out
+        out = {
+            "metric": "wire_records_verified_per_sec", "value": total * args.steps / elapsed,
+            "unit": "records/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "int32/int64 (GF(2^255-19) limbs)",
+            "data": "OpenSSL-signed fixture records (tests/golden/wire_ed25519.json) replicated",
+            "config": {"workload": w["desc"], "config": "wire", "records_per_gpu": n},
+            "roofline": {"bound": "hbm", "achieved": ab / (avg * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": ab / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "agnes::wire::ingest_kernel", "kernel_avg_ms": avg,
+                         "note": "VALU bound (one Ed25519 verification per lane, ~4.6k field products); "
+                                 "the HBM fraction is reported only for the contract"},
+            "gpu_verdicts_equal_openssl": bool(np.array_equal(v == abi.WIRE_OK, want_ok)),
+        }
+        if not args.no_cpu_baseline:
+            import concurrent.futures as cf
+            verify_many, libname = openssl_verifier()
+            cpu = host_cpu()
+            # the CPUs the cgroup grants (a quota below the affinity count would only
+            # add GIL contention between the ctypes calls)
+            threads = max(1, min(cpu["affinity"], int(cpu["cgroup_cpu_quota"] or cpu["affinity"])))
+            per = 2000
+            items = [(bytes.fromhex(g["pubkeys"][struct.unpack_from("<I", r, 24)[0]]), r[:40], r[40:])
+                     for r in recs]
+            work = [items * (per // len(items) + 1)][0][:per]
+            best = None
+            for _ in range(3):
+                t0 = time.perf_counter()
+                with cf.ThreadPoolExecutor(threads) as ex:
+                    res = list(ex.map(verify_many, [work] * threads))
+                dt = time.perf_counter() - t0
+                best = dt if best is None else min(best, dt)
+            cpu_ok = res[0][: len(items)] == list(map(bool, g["openssl_verifies"]))
+            out["cpu_baseline"] = {"value": per * threads / best, "unit": "records/s", "cores": threads,
+                                   "kind": "port", "host": cpu,
+                                   "sample": f"{per} fixture records per thread on {threads} threads, "
+                                             f"Ed25519 by {libname} EVP_DigestVerify via ctypes (an "
+                                             "independent implementation; the reference verifies nothing), "
+                                             "best of 3"}
+            out["cpu_check_equal"] = bool(cpu_ok)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
 
 
