@@ -734,68 +734,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                     const uint32_t x0 = roles(eA.x, eA.y, r8[0], c0, actA), x1 = roles(eB.x, eB.y, r8[1], c1, actB);
                     if (ballot((x0 | x1) != 0u)) {
                         const uint32_t pos0 = rc + o8, pos1 = pos0 + 4u; /* stream-relative */
-                        /* P1 / C relative to each unit: behind it (-1) when its quorum was crossed
-                         * before the unit, else the unit's first candidate byte (4: none).  The
-                         * Prevote step ends at P1 or at C, whichever comes first (a P1 after the
-                         * commit never happens); the unit holding the instance's P1 / C records it. */
-                        auto geom = [&](uint32_t x, uint32_t crossedP, uint32_t crossedC, uint32_t pos, uint32_t* rk,
-                                        int32_t& dP, int32_t& dC, bool& p1ok) {
-                            const uint32_t pm = x & (X_P1 * 0x01010101u), cm = x & (X_C * 0x01010101u);
-                            const int32_t bP = pm ? (int32_t)((uint32_t)__builtin_ctz(pm) >> 3) : 4;
-                            const int32_t bC = cm ? (int32_t)((uint32_t)__builtin_ctz(cm) >> 3) : 4;
-                            dC = crossedC ? -1 : bC;
-                            const int32_t p = crossedP ? -1 : bP;
-                            p1ok = p < dC;
-                            dP = p1ok ? p : dC;
-                            if (!crossedC && bC < 4) rk[R_C] = pos + (uint32_t)bC;
-                            if (!crossedP && p1ok && bP < 4) rk[R_P1] = pos + (uint32_t)bP;
-                        };
                         /* (an earlier chunk's P1 / C: in the record -- a round absent from this
                          * chunk has no crossing bit) */
                         const uint2 qA = *reinterpret_cast<const uint2*>(rA + R_P1);
                         const uint2 qB = *reinterpret_cast<const uint2*>(rB + R_P1);
-                        int32_t dPA, dCA, dPB, dCB;
-                        bool okA, okB;
-                        geom(x0, (cf & 1u) | (qA.x != NONE ? 1u : 0u), (cf & 2u) | (qA.y != NONE ? 1u : 0u), pos0, rA,
-                             dPA, dCA, okA);
-                        geom(x1, (cf & 4u) | (qB.x != NONE ? 1u : 0u), (cf & 8u) | (qB.y != NONE ? 1u : 0u), pos1, rB,
-                             dPB, dCB, okB);
                         const uint32_t nn0 = ~mark_bytes(nb0 << 3), nn1 = ~mark_bytes(nb1 << 3); /* non-nil votes */
-                        /* TimeoutPrevote before P1 (:196), TimeoutPrecommit before C (:208); valid:
+                        /* One unit, every mask straight from its role bits.  P1 and C are behind the
+                         * unit when their quorum was crossed before it (crossedP / crossedC), else at
+                         * its first candidate byte (none: past it).  The Prevote step ends at P1 or
+                         * at C, whichever comes first (a P1 after the commit never happens).
+                         *   alive  bytes before C         pre  bytes before the Prevote step ends
+                         *   atC    C's byte               atP  P1's byte (when P1 precedes C)
+                         * TimeoutPrevote before P1 (:196), TimeoutPrecommit before C (:208), the
+                         * precommit at P1 (:197-198), the Decision at C (:211); valid candidates:
                          * non-nil PolkaValues at State.round from P1 on (or from the start, entering
-                         * in Precommit), before C (:198, :202) */
-                        auto base_msg = [&](uint32_t x, uint32_t pre, uint32_t alive, uint32_t vall, uint32_t nnb,
-                                            uint32_t& vc) -> uint32_t {
+                         * in Precommit), before C (:198, :202).  The unit holding the instance's P1 /
+                         * C records its position. */
+                        auto unit = [&](uint32_t x, bool crossedP, bool crossedC, uint32_t pos, uint32_t* rk,
+                                        uint32_t vall, uint32_t nnb, uint32_t& atP, uint32_t& atC,
+                                        uint32_t& vc) -> uint32_t {
+                            const uint32_t pm = x & (X_P1 * 0x01010101u), cm = x & (X_C * 0x01010101u);
+                            const uint32_t lp = pm & (0u - pm);        /* bit 0 of the first P1 candidate byte */
+                            const uint32_t lc = (cm & (0u - cm)) >> 1; /* ... of the first commit candidate byte */
+                            const uint32_t preR = lp - 1u, aliveR = lc - 1u; /* 0xFF below them (none: all) */
+                            const bool p1ok = !crossedP && !crossedC && preR < aliveR;
+                            const uint32_t alive = crossedC ? 0u : aliveR;
+                            const uint32_t pre = (crossedP || crossedC) ? 0u : min(preR, aliveR);
+                            atC = crossedC ? 0u : (lc << 8) - lc;
+                            atP = p1ok ? (lp << 8) - lp : 0u;
+                            if (!crossedC && lc) rk[R_C] = pos + ((uint32_t)__builtin_ctz(lc) >> 3);
+                            if (p1ok) rk[R_P1] = pos + ((uint32_t)__builtin_ctz(lp) >> 3);
                             vc = x & alive & (~pre | vall) & nnb & (X_PV * 0x01010101u);
-                            return (x & ((pre & (X_TP * 0x01010101u)) | (alive & (X_TC * 0x01010101u)))) << 2;
+                            uint32_t msg = (x & ((pre & (X_TP * 0x01010101u)) | (alive & (X_TC * 0x01010101u)))) << 2;
+                            msg |= atP & ((AGNES_VMSG_PRECOMMIT_NIL << AGNES_CODE_MSG_SHIFT) * 0x01010101u +
+                                          (x & (X_PV * 0x01010101u)));
+                            msg |= atC & ((AGNES_VMSG_DECISION << AGNES_CODE_MSG_SHIFT) * 0x01010101u);
+                            return msg;
                         };
-                        uint32_t v0, v1, aP0 = 0, aC0 = 0, aP1 = 0, aC1 = 0;
-                        const bool inA = (uint32_t)dPA < 4u || (uint32_t)dCA < 4u;
-                        const bool inB = (uint32_t)dPB < 4u || (uint32_t)dCB < 4u;
-                        if (!ballot(inA || inB)) { /* no P1 or C inside any unit: whole-unit masks */
-                            c0 |= base_msg(x0, dPA >= 4 ? 0xFFFFFFFFu : 0u, dCA >= 4 ? 0xFFFFFFFFu : 0u, eA.z, nn0, v0);
-                            c1 |= base_msg(x1, dPB >= 4 ? 0xFFFFFFFFu : 0u, dCB >= 4 ? 0xFFFFFFFFu : 0u, eB.z, nn1, v1);
-                        } else {
-                            /* lo_bytes(d) = 0xFF in the bytes below d, d clamped to 0..4 */
-                            auto lo_bytes = [](int32_t d) -> uint32_t {
-                                const uint32_t k = (uint32_t)min(max(d, 0), 4);
-                                return (uint32_t)((0xFFFFFFFFull << (8u * k)) >> 32);
-                            };
-                            auto unit = [&](uint32_t x, int32_t dP, int32_t dC, bool p1ok, uint32_t vall, uint32_t nnb,
-                                            uint32_t& atP, uint32_t& atC, uint32_t& vc) -> uint32_t {
-                                const uint32_t alive = lo_bytes(dC), pre = lo_bytes(dP);
-                                atP = p1ok ? lo_bytes(dP + 1) ^ pre : 0u; /* the P1 vote's byte */
-                                atC = lo_bytes(dC + 1) ^ alive;         /* the commit vote's byte */
-                                /* precommit(r, v) / (r, None) at P1 (:197-198); Decision at C (:211) */
-                                uint32_t msg = base_msg(x, pre, alive, vall, nnb, vc);
-                                msg |= atP & ((AGNES_VMSG_PRECOMMIT_NIL << AGNES_CODE_MSG_SHIFT) * 0x01010101u +
-                                              (x & (X_PV * 0x01010101u)));
-                                msg |= atC & ((AGNES_VMSG_DECISION << AGNES_CODE_MSG_SHIFT) * 0x01010101u);
-                                return msg;
-                            };
-                            c0 |= unit(x0, dPA, dCA, okA, eA.z, nn0, aP0, aC0, v0);
-                            c1 |= unit(x1, dPB, dCB, okB, eB.z, nn1, aP1, aC1, v1);
-                        }
+                        uint32_t v0, v1, aP0, aC0, aP1, aC1;
+                        c0 |= unit(x0, (cf & 1u) || qA.x != NONE, (cf & 2u) || qA.y != NONE, pos0, rA, eA.z, nn0, aP0,
+                                   aC0, v0);
+                        c1 |= unit(x1, (cf & 4u) || qB.x != NONE, (cf & 8u) || qB.y != NONE, pos1, rB, eB.z, nn1, aP1,
+                                   aC1, v1);
                         const uint32_t lk0 = aP0 & (x0 << 3) & 0x80808080u, lk1 = aP1 & (x1 << 3) & 0x80808080u;
                         if (ballot((lk0 | lk1 | aC0 | aC1 | v0 | v1) != 0u)) { /* the lanes with a State write */
                             /* the value of byte b of a unit's votes (registers) */
