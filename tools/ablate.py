@@ -53,6 +53,9 @@ VARIANTS = {
     "lanenow_w4": lambda t: _lane_now(t).replace("amdgpu_waves_per_eu(3)", "amdgpu_waves_per_eu(4)"),
     "nosm": [("if (ballot((x0 | x1) != 0u)) {", "if (false) {")],
     "noroles": [("if (SM) {\n                    uint32_t* const rA", "if (false) {\n                    uint32_t* const rA")],
+    "k4nowrite2": [("if (ballot((lk0 | lk1 | aC0 | aC1 | v0 | v1) != 0u)) {", "if (false) {")],
+    "k4nomsg": [("                        c0 |= unit(x0,", "                        (void)unit(x0,"),
+                ("                        c1 |= unit(x1,", "                        (void)unit(x1,")],
     "nophase2": [("""                        uint32_t l = sv + sn > ta ? 1u : 0u;
                         l = sn > tn ? 2u : l;
                         l = sv > tv ? 3u : l;""", "                        uint32_t l = (sv ^ sn ^ (uint32_t)tv ^ (uint32_t)tn ^ (uint32_t)ta) & 3u;")],
