@@ -123,6 +123,8 @@ def gather_edges(recs: torch.Tensor, group=None) -> list:
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return [recs]
     world = dist.get_world_size(group)
+    if recs.is_cuda and dist.get_backend(group) != "nccl":  # gloo: host buffers
+        return [p.to(recs.device) for p in gather_edges(recs.cpu(), group)]
     flat = recs.contiguous().view(torch.uint8).reshape(recs.shape[0], -1) if recs.numel() else \
         torch.zeros((0, 16), dtype=torch.uint8, device=recs.device)
     rec = flat.shape[1]

@@ -223,10 +223,17 @@ def main():
     rank, world, local = adist.env()
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    # one rank per GPU; a rehearsal of the N > 1 path on a one-GPU box runs its ranks
+    # on the same device over gloo (AGNES_BENCH_BACKEND=gloo: RCCL needs a GPU per rank)
+    backend = os.environ.get("AGNES_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     w = WORKLOADS[args.config]
     eng = Engine(local)
