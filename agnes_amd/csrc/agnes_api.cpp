@@ -469,7 +469,7 @@ int agnes_wire_ingest(agnes_ctx* c, const agnes_wire_vote* records, uint64_t n, 
     if (n && (!records || !instance || !round || !type || !value || !validator || !verdict)) return AGNES_E_INVALID;
     if (n && n_sets && n_vals && !pubkeys) return AGNES_E_INVALID;
     if (((uintptr_t)records & 7u) || ((uintptr_t)pubkeys & 15u)) return AGNES_E_INVALID;
-    if (n > (1ull << 40)) return AGNES_E_UNSUPPORTED;
+    if (n > (1ull << 36)) return AGNES_E_UNSUPPORTED; /* (n + 255) / 256 blocks fit the grid */
     AGNES_TRY(hipSetDevice(c->device));
     const hipStream_t st = (hipStream_t)stream;
     AGNES_ORDER(c, st);

@@ -518,8 +518,8 @@ enum {
  * encode([S]B - [k]A) == R, k = SHA-512(R || A || sign-bytes) mod L).  Out, in record
  * order: instance, value, validator as decoded; round (low byte) and type for an
  * accepted record, round 0 and type 0xFF (coded INVALID by agnes_tally) for any
- * other; verdict[i] = AGNES_WIRE_*.  All pointers DEVICE; records 8-B aligned.
- * Asynchronous on `stream`. */
+ * other; verdict[i] = AGNES_WIRE_*.  All pointers DEVICE; records 8-B and pubkeys
+ * 16-B aligned (else AGNES_E_INVALID); n <= 2^36.  Asynchronous on `stream`. */
 int agnes_wire_ingest(agnes_ctx* ctx, const agnes_wire_vote* records, uint64_t n, const uint8_t* pubkeys,
                       uint32_t n_sets, uint32_t n_vals, const uint32_t* instance_set, uint32_t n_instances,
                       int64_t height, uint32_t max_rounds, uint32_t* instance, uint8_t* round, uint8_t* type,
