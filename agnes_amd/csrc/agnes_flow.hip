@@ -59,7 +59,7 @@ constexpr uint32_t SMALLB = 4u; /* batch size of the work queue's tail          
  * locked and decision values go straight into the staged States when P1 / C are
  * found (the vote's value is still in registers). */
 constexpr uint32_t R_Q2 = 0, R_PBASE = 1, R_NV = 2, R_EQ8 = 3, R_SMASK = 4, R_EQ = 5, R_VALL = 6, R_STEP = 7, R_P1 = 8,
-                   R_C = 9, R_DF = 10, RECW = 12;
+                   R_C = 9, R_DF = 10, R_DR = 11, RECW = 12;
 constexpr uint32_t F_LOCK = 0x100u;
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 
@@ -317,7 +317,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
             uint32_t fl = (sp[13] & ~0xFFu) | step;
             if (df & F_LOCK) { sp[4] = sp[2]; sp[5] = sp[3]; fl |= 1u << 8; } /* (P1 precedes any C) */
             if (vv) { sp[6] = sp[2]; sp[7] = sp[3]; sp[11] = (uint32_t)vv; fl |= 1u << 16; }
-            if (cc != NONE) { sp[8] = df & 0xFFu; sp[9] = 0u; fl |= 1u << 24; }
+            if (cc != NONE) { sp[8] = rk[R_DR]; sp[9] = 0u; fl |= 1u << 24; }
             sp[13] = fl;
         }
         __builtin_amdgcn_wave_barrier();
@@ -383,6 +383,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                     rk[R_P1] = NONE;
                     rk[R_C] = NONE;
                     rk[R_DF] = 0u;
+                    rk[R_DR] = 0u;
                     if (SM) vtab[lane] = 0ull;
                 }
                 if (SM && smf) { /* the State machine's view of each instance (state_machine.rs:184) */
@@ -750,9 +751,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                          * non-nil PolkaValues at State.round from P1 on (or from the start, entering
                          * in Precommit), before C (:198, :202).  The unit holding the instance's P1 /
                          * C records its position. */
-                        auto unit = [&](uint32_t x, bool crossedP, bool crossedC, uint32_t pos, uint32_t* rk,
-                                        uint32_t vall, uint32_t nnb, uint32_t& atP, uint32_t& atC,
-                                        uint32_t& vc) -> uint32_t {
+                        /* the value of byte b of unit u's votes (registers) */
+                        auto vsel = [&](uint32_t u, uint32_t b) -> uint32_t {
+                            const uint32_t* const vv = value + 4u * u;
+                            const uint32_t lo = (b & 1u) ? vv[1] : vv[0], hi = (b & 1u) ? vv[3] : vv[2];
+                            return (b & 2u) ? hi : lo;
+                        };
+                        auto unit = [&](uint32_t u, uint32_t x, bool crossedP, bool crossedC, uint32_t pos, uint32_t* rk,
+                                        uint32_t* sx, uint32_t r4, uint32_t vall, uint32_t nnb, uint32_t& vc) -> uint32_t {
                             const uint32_t pm = x & (X_P1 * 0x01010101u), cm = x & (X_C * 0x01010101u);
                             const uint32_t lp = pm & (0u - pm);        /* bit 0 of the first P1 candidate byte */
                             const uint32_t lc = (cm & (0u - cm)) >> 1; /* ... of the first commit candidate byte */
@@ -760,10 +766,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                             const bool p1ok = !crossedP && !crossedC && preR < aliveR;
                             const uint32_t alive = crossedC ? 0u : aliveR;
                             const uint32_t pre = (crossedP || crossedC) ? 0u : min(preR, aliveR);
-                            atC = crossedC ? 0u : (lc << 8) - lc;
-                            atP = p1ok ? (lp << 8) - lp : 0u;
-                            if (!crossedC && lc) rk[R_C] = pos + ((uint32_t)__builtin_ctz(lc) >> 3);
-                            if (p1ok) rk[R_P1] = pos + ((uint32_t)__builtin_ctz(lp) >> 3);
+                            const uint32_t atC = crossedC ? 0u : (lc << 8) - lc;
+                            const uint32_t atP = p1ok ? (lp << 8) - lp : 0u;
+                            /* the unit holding C: its position, the decision's value and round (:211) */
+                            if (!crossedC && lc) {
+                                const uint32_t b = (uint32_t)__builtin_ctz(lc) >> 3;
+                                rk[R_C] = pos + b;
+                                sx[12] = vsel(u, b);
+                                if (!R1) rk[R_DR] = (r4 >> (8u * b)) & 0xFFu;
+                            }
+                            /* the unit holding P1: its position; a PolkaValue locks (:198) */
+                            if (p1ok) {
+                                const uint32_t b = (uint32_t)__builtin_ctz(lp) >> 3;
+                                rk[R_P1] = pos + b;
+                                if ((x >> (8u * b)) & X_PV) {
+                                    rk[R_DF] = F_LOCK;
+                                    sx[10] = vsel(u, b);
+                                }
+                            }
                             vc = x & alive & (~pre | vall) & nnb & (X_PV * 0x01010101u);
                             uint32_t msg = (x & ((pre & (X_TP * 0x01010101u)) | (alive & (X_TC * 0x01010101u)))) << 2;
                             msg |= atP & ((AGNES_VMSG_PRECOMMIT_NIL << AGNES_CODE_MSG_SHIFT) * 0x01010101u +
@@ -771,40 +791,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                             msg |= atC & ((AGNES_VMSG_DECISION << AGNES_CODE_MSG_SHIFT) * 0x01010101u);
                             return msg;
                         };
-                        uint32_t v0, v1, aP0, aC0, aP1, aC1;
-                        c0 |= unit(x0, (cf & 1u) || qA.x != NONE, (cf & 2u) || qA.y != NONE, pos0, rA, eA.z, nn0, aP0,
-                                   aC0, v0);
-                        c1 |= unit(x1, (cf & 4u) || qB.x != NONE, (cf & 8u) || qB.y != NONE, pos1, rB, eB.z, nn1, aP1,
-                                   aC1, v1);
-                        const uint32_t lk0 = aP0 & (x0 << 3) & 0x80808080u, lk1 = aP1 & (x1 << 3) & 0x80808080u;
-                        if (ballot((lk0 | lk1 | aC0 | aC1 | v0 | v1) != 0u)) { /* the lanes with a State write */
-                            /* the value of byte b of a unit's votes (registers) */
-                            auto vsel = [&](uint32_t u, uint32_t b) -> uint32_t {
-                                const uint32_t* const vv = value + 4u * u;
-                                const uint32_t lo = (b & 1u) ? vv[1] : vv[0], hi = (b & 1u) ? vv[3] : vv[2];
-                                return (b & 2u) ? hi : lo;
-                            };
-                            uint32_t* const sA = reinterpret_cast<uint32_t*>(sbh + 64u * kA);
-                            uint32_t* const sB = reinterpret_cast<uint32_t*>(sbh + 64u * kB);
-                            if (lk0) { /* locked (:198) */
-                                atomicOr(rA + R_DF, F_LOCK);
-                                sA[10] = vsel(0u, (uint32_t)__builtin_ctz(lk0) >> 3);
-                            }
-                            if (lk1) {
-                                atomicOr(rB + R_DF, F_LOCK);
-                                sB[10] = vsel(1u, (uint32_t)__builtin_ctz(lk1) >> 3);
-                            }
-                            if (aC0) { /* the decision (:211) */
-                                const uint32_t b = (uint32_t)__builtin_ctz(aC0) >> 3;
-                                atomicOr(rA + R_DF, (r8[0] >> (8u * b)) & 0xFFu);
-                                sA[12] = vsel(0u, b);
-                            }
-                            if (aC1) {
-                                const uint32_t b = (uint32_t)__builtin_ctz(aC1) >> 3;
-                                atomicOr(rB + R_DF, (r8[1] >> (8u * b)) & 0xFFu);
-                                sB[12] = vsel(1u, b);
-                            }
-                            if (v0) { /* valid (:198, :202): the last candidate */
+                        uint32_t* const sA = reinterpret_cast<uint32_t*>(sbh + 64u * kA);
+                        uint32_t* const sB = reinterpret_cast<uint32_t*>(sbh + 64u * kB);
+                        uint32_t v0, v1;
+                        c0 |= unit(0u, x0, (cf & 1u) || qA.x != NONE, (cf & 2u) || qA.y != NONE, pos0, rA, sA, r8[0],
+                                   eA.z, nn0, v0);
+                        c1 |= unit(1u, x1, (cf & 4u) || qB.x != NONE, (cf & 8u) || qB.y != NONE, pos1, rB, sB, r8[1],
+                                   eB.z, nn1, v1);
+                        if (ballot((v0 | v1) != 0u)) { /* valid (:198, :202): the last candidate */
+                            if (v0) {
                                 const uint32_t b = (31u - (uint32_t)__builtin_clz(v0)) >> 3;
                                 atomicMax(vtab + kA, ((unsigned long long)(pos0 + b + 1u) << 32) | vsel(0u, b));
                             }
