@@ -40,18 +40,20 @@ KERNEL_BYTES_PER_VOTE = {
     "tally_stream": 15,
     "tally_fast": 15,
     "tally_wide": 15,
-    "apply_codes": 2,    # code + round u8 in (messages written back sparsely)
+    "apply_codes": 2,    # code + round u8 in (+ the message bytes written back)
     "dedup_first": 10,   # C5 DEDUP: instance, validator u32 + round, type u8 in (+ 8 B atomic per key)
     "dedup_mask": 11,    # the same in, the masked type u8 out
 }
 KERNEL_SYMBOLS = {
+    # template parameters: PC (power table in LDS), SM (State machine), R1 (one round);
+    # c2 runs flow<true, true, true>, c3 flow<false, true, false> (rocprofv3 names them)
     "flow": "agnes::flow::flow<PC, SM, R1>",
     "sweep": "agnes::sweep::sweep<PC, SM, false>",
     "sweep_walk": "agnes::sweep::sweep<PC, SM, true>",
     "tally_stream": "agnes::stream::tally_stream<false, *>",
     "tally_fast": "agnes::fast::tally_fast<...>",
     "tally_wide": "agnes::tally_kernel<true, ...>",
-    "apply_codes": "agnes::apply::apply_codes<false>",
+    "apply_codes": "agnes::apply::apply_codes<RoundSkip>",
 }
 
 WORKLOADS = {
