@@ -29,6 +29,12 @@ VARIANTS = {
                      abi.FLAG_STATE_MACHINE, 1),
     "c3_sm": (dict(n_instances=250_000, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300),
               (abi.POWER_UNIFORM, 1, 1000, 1024), abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 4),
+    "c3_1set": (dict(n_instances=250_000, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300),
+                (abi.POWER_UNIFORM, 1, 1000, 1), abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 4),
+    "c3_r1": (dict(n_instances=625_000, n_vals=150, rounds_min=1, rounds_max=1, nil_permille=300),
+              (abi.POWER_UNIFORM, 1, 1000, 1024), abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 4),
+    "c3_r1only": (dict(n_instances=625_000, n_vals=150, rounds_min=1, rounds_max=1, nil_permille=300),
+                  (abi.POWER_UNIFORM, 1, 1000, 1024), abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 1),
     "c4_full": (dict(n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4,
                      nil_permille=300, dup_permille=100, equiv_permille=100, higher_permille=50),
                 (abi.POWER_ZIPF, 1, 1_000_000, 1024), abi.MODE_DEDUP,
