@@ -38,6 +38,7 @@ struct agnes_ctx {
     uint32_t list_cap = 0;
     uint64_t* d_scan = nullptr; /* edge-offset scan: block totals */
     uint64_t scan_cap = 0;
+    int32_t* d_edtab = nullptr; /* Ed25519 fixed-base table (agnes_wire_ingest), built on first use */
 };
 
 namespace {
@@ -231,6 +232,7 @@ void agnes_ctx_destroy(agnes_ctx* c) {
     if (c->d_err) (void)hipFree(c->d_err);
     if (c->d_list) (void)hipFree(c->d_list);
     if (c->d_scan) (void)hipFree(c->d_scan);
+    if (c->d_edtab) (void)hipFree(c->d_edtab);
     if (c->order_ev) (void)hipEventDestroy(c->order_ev);
     delete c;
 }
@@ -473,8 +475,12 @@ int agnes_wire_ingest(agnes_ctx* c, const agnes_wire_vote* records, uint64_t n, 
     AGNES_TRY(hipSetDevice(c->device));
     const hipStream_t st = (hipStream_t)stream;
     AGNES_ORDER(c, st);
+    if (!c->d_edtab) { /* the fixed-base table: once per context, on the caller's stream */
+        AGNES_TRY(hipMalloc(&c->d_edtab, agnes_wire_table_bytes()));
+        AGNES_TRY(agnes_launch_wire_table(c->d_edtab, st));
+    }
     agnes_wire_args a{records, n, pubkeys, n_sets, n_vals, instance_set, n_instances, max_rounds, height,
-                      instance, value, validator, round, type, verdict};
+                      instance, value, validator, round, type, verdict, c->d_edtab};
     AgnesKt kt("wire_ingest", st);
     return status_of(agnes_launch_wire_ingest(&a, st));
 }

@@ -17,9 +17,11 @@
  *            every product operand stays below 2^26.x (no int64 overflow);
  *   points   extended twisted-Edwards (X : Y : Z : T), the unified a = -1
  *            addition (also the doubling), complete on the curve;
- *   scalars  [S]B + [k](-A) by one joint double-and-add from bit 255 (Shamir),
- *            branch-free: the addend {identity, B, -A, B - A} is selected per
- *            lane, so lanes with different bits do not diverge;
+ *   scalars  [S]B from a fixed-base table (64 rows of j 16^i B, Niels form, built
+ *            once per context: 64 mixed additions, no doubling) and [k](-A) by
+ *            2-bit windows (two doublings + one addition per window), branch-free:
+ *            the addend {O, -A, -2A, -3A} is selected per lane, so lanes with
+ *            different bits do not diverge;
  *   hash     SHA-512 of the 104-byte R || A || M: one compression.
  * Host-compilable as plain C++ (tools/ed25519_host.cpp defines the HIP
  * qualifiers away) so the arithmetic can be unit-tested without a GPU.
@@ -473,18 +475,78 @@ AGNES_ED void sha512_short(uint8_t out[64], const uint8_t* msg, uint32_t len) {
 
 /* ---- verification ---- */
 
-/* the base point B: y = 4/5, x even (RFC 8032 §5.1) */
-AGNES_ED bool ge_base(ge& b) {
-    uint8_t s[32];
-    s[0] = 0x58;
+/* the base point B: y = 4/5, x even (RFC 8032 §5.1); limbs from tools/ed25519_consts.py */
+AGNES_ED void ge_base(ge& b) {
+    const int32_t bx[10] = {52811034, 25909283, 16144682, 17082669, 27570973, 30858332, 40966398, 8378388, 20764389, 8758491};
+    const int32_t by[10] = {40265304, 26843545, 13421772, 20132659, 26843545, 6710886, 53687091, 13421772, 40265318, 26843545};
+    const int32_t bt[10] = {28827043, 27438313, 39759291, 244362, 8635006, 11264893, 19351346, 13413597, 16611511, 27139452};
 #pragma unroll
-    for (int i = 1; i < 32; ++i) s[i] = 0x66;
-    return ge_frombytes(b, s);
+    for (int i = 0; i < 10; ++i) {
+        b.X.v[i] = bx[i];
+        b.Y.v[i] = by[i];
+        b.T.v[i] = bt[i];
+    }
+    fe_set(b.Z, 1);
+}
+
+/* a point in affine "Niels" form: y + x, y - x, 2 d x y (identity: 1, 1, 0) */
+struct ge_niels {
+    fe ypx, ymx, xy2d;
+};
+/* r = p + q, q affine (madd-2008-hwcd-3, a = -1): 7 products */
+AGNES_ED void ge_madd(ge& r, const ge& p, const ge_niels& q) {
+    fe a, b, c, d, e, f, g, h;
+    fe_sub(a, p.Y, p.X);
+    fe_mul(a, a, q.ymx);
+    fe_add(b, p.Y, p.X);
+    fe_mul(b, b, q.ypx);
+    fe_mul(c, p.T, q.xy2d);
+    fe_add(d, p.Z, p.Z);
+    fe_sub(e, b, a);
+    fe_sub(f, d, c);
+    fe_add(g, d, c);
+    fe_add(h, b, a);
+    fe_mul(r.X, e, f);
+    fe_mul(r.Y, g, h);
+    fe_mul(r.T, e, h);
+    fe_mul(r.Z, f, g);
+}
+
+/* the fixed-base table: row i (0..63) holds j 16^i B for j = 0..15 in Niels form,
+ * 16 x 3 x 10 int32 (agnes_wire.hip builds it once per context, one thread a row) */
+constexpr int BASE_ROW_WORDS = 16 * 3 * 10;
+AGNES_ED void build_base_row(int i, int32_t* out) {
+    ge bi, acc;
+    ge_base(bi);
+    for (int k = 0; k < 4 * i; ++k) ge_dbl(bi, bi);
+    ge_identity(acc);
+    fe d2;
+    fe_2d(d2);
+    for (int j = 0; j < 16; ++j) {
+        fe zi, x, y, s, dd, m;
+        fe_invert(zi, acc.Z);
+        fe_mul(x, acc.X, zi);
+        fe_mul(y, acc.Y, zi);
+        fe_add(s, y, x);
+        fe_sub(dd, y, x);
+        fe_mul(m, x, y);
+        fe_mul(m, m, d2);
+        for (int l = 0; l < 10; ++l) {
+            out[(j * 3 + 0) * 10 + l] = s.v[l];
+            out[(j * 3 + 1) * 10 + l] = dd.v[l];
+            out[(j * 3 + 2) * 10 + l] = m.v[l];
+        }
+        ge_add(acc, acc, bi, d2);
+    }
 }
 
 /* RFC 8032 §5.1.7, cofactorless (OpenSSL 3.0 ED25519_verify): sig = R || S over
- * msg (len <= 47: R || A || msg fits one SHA-512 block) with public key pub */
-AGNES_ED bool verify(const uint8_t pub[32], const uint8_t* msg, uint32_t len, const uint8_t sig[64]) {
+ * msg (len <= 47: R || A || msg fits one SHA-512 block) with public key pub.
+ * [S]B = sum over the 64 nibbles s_i of S of the table entry s_i 16^i B (no
+ * doubling); [k](-A) by 2-bit windows from the top (two doublings and one
+ * addition of {O, -A, -2A, -3A} per window, chosen per lane by selects). */
+AGNES_ED bool verify(const uint8_t pub[32], const uint8_t* msg, uint32_t len, const uint8_t sig[64],
+                     const int32_t* base_table) {
     if (!sc_canonical(sig + 32)) return false;
     ge A;
     if (!ge_frombytes(A, pub)) return false;
@@ -497,39 +559,55 @@ AGNES_ED bool verify(const uint8_t pub[32], const uint8_t* msg, uint32_t len, co
     for (uint32_t i = 0; i < len; ++i) hin[64 + i] = msg[i];
     sha512_short(h, hin, 64u + len);
     sc_reduce(k, h);
-    /* addends: 1 = B, 2 = -A, 3 = B - A */
-    ge Bp, nA, BnA;
-    ge_base(Bp);
-    fe_neg(nA.X, A.X);
-    nA.Y = A.Y;
-    nA.Z = A.Z;
-    fe_neg(nA.T, A.T);
     fe d2;
     fe_2d(d2);
-    ge_add(BnA, Bp, nA, d2);
+    /* [S]B */
+    const uint8_t* S = sig + 32;
+    ge P;
+    ge_identity(P);
+    for (int i = 0; i < 64; ++i) {
+        const uint32_t nib = (S[i >> 1] >> (4 * (i & 1))) & 15u;
+        const int32_t* e = base_table + (i * 16 + (int)nib) * 30;
+        ge_niels q;
+#pragma unroll
+        for (int l = 0; l < 10; ++l) {
+            q.ypx.v[l] = e[l];
+            q.ymx.v[l] = e[10 + l];
+            q.xy2d.v[l] = e[20 + l];
+        }
+        ge_madd(P, P, q);
+    }
+    /* [k](-A) */
+    ge n1, n2, n3;
+    fe_neg(n1.X, A.X);
+    n1.Y = A.Y;
+    n1.Z = A.Z;
+    fe_neg(n1.T, A.T);
+    ge_dbl(n2, n1);
+    ge_add(n3, n2, n1, d2);
     ge Q;
     ge_identity(Q);
-    const uint8_t* S = sig + 32;
-    for (int i = 255; i >= 0; --i) {
+    for (int i = 252; i >= 0; i -= 2) { /* windows (i + 1, i); k < 2^253: bits 253.. are zero */
         ge_dbl(Q, Q);
-        const uint32_t sb = (S[i >> 3] >> (i & 7)) & 1u, kb = (k[i >> 3] >> (i & 7)) & 1u;
-        const uint32_t sel = sb | (kb << 1);
+        ge_dbl(Q, Q);
+        const uint32_t dgt = (k[i >> 3] >> (i & 7)) & 3u; /* (i even: the pair never straddles a byte) */
         ge T;
         ge_identity(T);
-        fe_select(T.X, T.X, Bp.X, sel == 1u);
-        fe_select(T.Y, T.Y, Bp.Y, sel == 1u);
-        fe_select(T.Z, T.Z, Bp.Z, sel == 1u);
-        fe_select(T.T, T.T, Bp.T, sel == 1u);
-        fe_select(T.X, T.X, nA.X, sel == 2u);
-        fe_select(T.Y, T.Y, nA.Y, sel == 2u);
-        fe_select(T.Z, T.Z, nA.Z, sel == 2u);
-        fe_select(T.T, T.T, nA.T, sel == 2u);
-        fe_select(T.X, T.X, BnA.X, sel == 3u);
-        fe_select(T.Y, T.Y, BnA.Y, sel == 3u);
-        fe_select(T.Z, T.Z, BnA.Z, sel == 3u);
-        fe_select(T.T, T.T, BnA.T, sel == 3u);
+        fe_select(T.X, T.X, n1.X, dgt == 1u);
+        fe_select(T.Y, T.Y, n1.Y, dgt == 1u);
+        fe_select(T.Z, T.Z, n1.Z, dgt == 1u);
+        fe_select(T.T, T.T, n1.T, dgt == 1u);
+        fe_select(T.X, T.X, n2.X, dgt == 2u);
+        fe_select(T.Y, T.Y, n2.Y, dgt == 2u);
+        fe_select(T.Z, T.Z, n2.Z, dgt == 2u);
+        fe_select(T.T, T.T, n2.T, dgt == 2u);
+        fe_select(T.X, T.X, n3.X, dgt == 3u);
+        fe_select(T.Y, T.Y, n3.Y, dgt == 3u);
+        fe_select(T.Z, T.Z, n3.Z, dgt == 3u);
+        fe_select(T.T, T.T, n3.T, dgt == 3u);
         ge_add(Q, Q, T, d2);
     }
+    ge_add(Q, Q, P, d2);
     uint8_t rc[32];
     ge_tobytes(rc, Q);
     uint32_t diff = 0;

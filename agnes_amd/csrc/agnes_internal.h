@@ -118,8 +118,11 @@ struct agnes_wire_args {
     int64_t height;
     uint32_t *instance, *value, *validator;
     uint8_t *round, *type, *verdict;
+    const int32_t* base_table; /* agnes_launch_wire_table's output */
 };
 hipError_t agnes_launch_wire_ingest(const agnes_wire_args* a, hipStream_t st);
+size_t agnes_wire_table_bytes(void);
+hipError_t agnes_launch_wire_table(int32_t* table, hipStream_t st);
 hipError_t agnes_launch_gen(const agnes_gen_params* p, const uint64_t* d_offsets, uint64_t n_votes,
                             uint32_t* instance, uint8_t* round, uint8_t* type, uint32_t* value,
                             uint32_t* validator, hipStream_t stream);

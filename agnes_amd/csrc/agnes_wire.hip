@@ -5,9 +5,10 @@
  * instance, height and validator a network message names; the key is the
  * validator's (validators.rs:4-8, 15-17).
  *
- * One record per lane: an Ed25519 verification is ~4.6k field products of
- * integer multiply-adds with no data shared between votes, so the kernel is
- * VALU bound and simply needs every lane busy (agnes_ed25519.h).  The record and
+ * One record per lane: an Ed25519 verification is ~4k field products of integer
+ * multiply-adds with no data shared between votes (the fixed-base table, 123 KB,
+ * is read from L2), so the kernel is VALU bound and simply needs every lane busy
+ * (agnes_ed25519.h).  The record and
  * the key are read once (136 B per vote), the columns written once (14 B + the
  * verdict byte).
  */
@@ -67,7 +68,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(agnes_wire_args a) {
             const uint32_t kw[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
 #pragma unroll
             for (int b = 0; b < 32; ++b) pub[b] = (uint8_t)(kw[b >> 2] >> (8 * (b & 3)));
-            if (!ed::verify(pub, rec, AGNES_WIRE_SIGNED_BYTES, rec + AGNES_WIRE_SIGNED_BYTES))
+            if (!ed::verify(pub, rec, AGNES_WIRE_SIGNED_BYTES, rec + AGNES_WIRE_SIGNED_BYTES, a.base_table))
                 verdict = AGNES_WIRE_BAD_SIGNATURE;
         }
     }
@@ -80,8 +81,21 @@ __global__ __launch_bounds__(256) void ingest_kernel(agnes_wire_args a) {
     a.verdict[i] = (uint8_t)verdict;
 }
 
+/* the fixed-base table: row i = j 16^i B, j = 0..15, one thread a row */
+__global__ __launch_bounds__(64) void table_kernel(int32_t* tab) {
+    const int i = (int)threadIdx.x;
+    if (i < 64) ed::build_base_row(i, tab + i * ed::BASE_ROW_WORDS);
+}
+
 } // namespace wire
 } // namespace agnes
+
+size_t agnes_wire_table_bytes(void) { return 64u * agnes::ed::BASE_ROW_WORDS * sizeof(int32_t); }
+
+hipError_t agnes_launch_wire_table(int32_t* table, hipStream_t st) {
+    hipLaunchKernelGGL(agnes::wire::table_kernel, dim3(1), dim3(64), 0, st, table);
+    return hipGetLastError();
+}
 
 hipError_t agnes_launch_wire_ingest(const agnes_wire_args* a, hipStream_t st) {
     if (a->n == 0) return hipSuccess;

@@ -607,36 +607,37 @@ def bench_wire(args, w, eng, rank, world):
             "roofline": {"bound": "hbm", "achieved": ab / (avg * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": ab / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
                          "kernel": "agnes::wire::ingest_kernel", "kernel_avg_ms": avg,
-                         "note": "VALU bound (one Ed25519 verification per lane, ~4.6k field products); "
+                         "note": "VALU bound (one Ed25519 verification per lane, ~4k field products); "
                                  "the HBM fraction is reported only for the contract"},
             "gpu_verdicts_equal_openssl": bool(np.array_equal(v == abi.WIRE_OK, want_ok)),
         }
         if not args.no_cpu_baseline:
-            import concurrent.futures as cf
-            verify_many, libname = openssl_verifier()
+            # the host's OpenSSL Ed25519 verify rate over every CPU the cgroup grants
+            # (`openssl speed -multi`: one process per CPU, OpenSSL's own timing loop),
+            # and OpenSSL's verdicts on the fixture records through libcrypto (check)
+            import subprocess
             cpu = host_cpu()
-            # the CPUs the cgroup grants (a quota below the affinity count would only
-            # add GIL contention between the ctypes calls)
-            threads = max(1, min(cpu["affinity"], int(cpu["cgroup_cpu_quota"] or cpu["affinity"])))
-            per = 2000
-            items = [(bytes.fromhex(g["pubkeys"][struct.unpack_from("<I", r, 24)[0]]), r[:40], r[40:])
-                     for r in recs]
-            work = [items * (per // len(items) + 1)][0][:per]
-            best = None
-            for _ in range(3):
-                t0 = time.perf_counter()
-                with cf.ThreadPoolExecutor(threads) as ex:
-                    res = list(ex.map(verify_many, [work] * threads))
-                dt = time.perf_counter() - t0
-                best = dt if best is None else min(best, dt)
-            cpu_ok = res[0][: len(items)] == list(map(bool, g["openssl_verifies"]))
-            out["cpu_baseline"] = {"value": per * threads / best, "unit": "records/s", "cores": threads,
-                                   "kind": "port", "host": cpu,
-                                   "sample": f"{per} fixture records per thread on {threads} threads, "
-                                             f"Ed25519 by {libname} EVP_DigestVerify via ctypes (an "
-                                             "independent implementation; the reference verifies nothing), "
-                                             "best of 3"}
-            out["cpu_check_equal"] = bool(cpu_ok)
+            procs = max(1, min(cpu["affinity"], int(cpu["cgroup_cpu_quota"] or cpu["affinity"])))
+            rate = None
+            try:
+                r = subprocess.run(["openssl", "speed", "-seconds", "3", "-multi", str(procs), "ed25519"],
+                                   capture_output=True, text=True, timeout=120)
+                for line in r.stdout.splitlines():
+                    if "Ed25519" in line:
+                        rate = float(line.split()[-1])
+            except (OSError, subprocess.SubprocessError, ValueError):
+                rate = None
+            verify_many, libname = openssl_verifier()
+            items = [(bytes.fromhex(g["pubkeys"][struct.unpack_from("<I", r_, 24)[0]]), r_[:40], r_[40:])
+                     for r_ in recs]
+            out["cpu_check_equal"] = verify_many(items) == list(map(bool, g["openssl_verifies"]))
+            if rate is not None:
+                out["cpu_baseline"] = {"value": rate, "unit": "records/s", "cores": procs, "kind": "port",
+                                       "host": cpu,
+                                       "sample": f"`openssl speed -seconds 3 -multi {procs} ed25519` verify/s "
+                                                 "(OpenSSL 3's Ed25519 verification, one process per granted "
+                                                 "CPU; an independent implementation: the reference verifies "
+                                                 "nothing)"}
         print(json.dumps(out), flush=True)
     if world > 1:
         import torch.distributed as dist

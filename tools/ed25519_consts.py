@@ -13,3 +13,11 @@ def limbs(x):
 
 for name, x in (("d", D), ("2d", 2 * D % P), ("sqrtm1", SQRT_M1)):
     print(name, ", ".join(str(v) for v in limbs(x)))
+
+# the base point B (y = 4/5, x even), extended coordinates with Z = 1
+import sys
+sys.path.insert(0, __import__("os").path.join(__import__("os").path.dirname(__file__), ".."))
+from oracle import ed25519_ref as E  # noqa: E402
+bx, by = E.B[0] % P, E.B[1] % P
+for name, x in (("bx", bx), ("by", by), ("bt", bx * by % P)):
+    print(name, ", ".join(str(v) for v in limbs(x)))

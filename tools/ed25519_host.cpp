@@ -6,9 +6,15 @@
 #define __forceinline__ inline
 #include "../agnes_amd/csrc/agnes_ed25519.h"
 using namespace agnes::ed;
+static int32_t g_tab[64 * BASE_ROW_WORDS];
+static bool g_tab_ok = false;
 extern "C" {
 int ed_verify(const uint8_t* pub, const uint8_t* msg, uint32_t len, const uint8_t* sig) {
-    return verify(pub, msg, len, sig) ? 1 : 0;
+    if (!g_tab_ok) {
+        for (int i = 0; i < 64; ++i) build_base_row(i, g_tab + i * BASE_ROW_WORDS);
+        g_tab_ok = true;
+    }
+    return verify(pub, msg, len, sig, g_tab) ? 1 : 0;
 }
 void ed_sc_reduce(const uint8_t* in, uint8_t* out) { sc_reduce(out, in); }
 void ed_fe_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) {
