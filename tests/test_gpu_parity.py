@@ -429,6 +429,45 @@ def test_deferred_instances_and_set_fallback(eng, route, mode, flags):
     assert_same(g, o)
 
 
+def _with_invalid(hb, seed, n_vals, max_rounds, permille=30):
+    """hb with a sprinkle of invalid votes: round >= max_rounds, validator >= n_vals,
+    type outside {Prevote, Precommit} (round_votes.rs has no such votes; the engine
+    counts and skips them)."""
+    rng = np.random.default_rng(seed)
+    n = hb.n_votes
+    k = rng.random(n) < permille / 1000.0
+    which = rng.integers(0, 3, n)
+    hb.round[k & (which == 0)] = max_rounds
+    hb.validator[k & (which == 1)] = n_vals + 3
+    hb.type[k & (which == 2)] = 5
+    return hb
+
+
+def test_invalid_counts_across_routes_and_calls(eng):
+    """The queued routes publish the invalid count from the LIST kernel's last wave
+    and leave the counters zeroed for the next call (no memset nodes); the other
+    routes reset on the host.  One ctx, a sequence mixing them, every count and code
+    against the checker: a stale or unreset counter shows as a wrong count."""
+    hb = _with_invalid(_ragged_batch(61, 5000, 9, 3, [0, 4, 8, 40, 200]), 61, 9, 3)
+    hbd = _with_invalid(_ragged_batch(62, 3000, 13, 3, [8, 40, 200, 1200]), 62, 13, 3)
+    hbd.instance_set = None
+    p_small = ol.gen_power(61, 2, 9, abi.POWER_UNIFORM, 1, 30)
+    p_big = ol.gen_power(62, 3, 13, abi.POWER_UNIFORM, 1 << 20, 1 << 21)
+    seq = [("auto", hb, p_small, abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE),
+           ("auto", hb, p_small, abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE),
+           ("wide", hb, p_small, abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE),
+           ("auto", hbd, p_big, abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE),
+           ("split", hbd, p_big, abi.MODE_DEDUP, abi.FLAG_STATE_MACHINE | abi.FLAG_ROUND_SKIP),
+           ("auto", hb, p_small, abi.MODE_REFERENCE, 0),
+           ("wide", hbd, p_big, abi.MODE_DEDUP, abi.FLAG_STATE_MACHINE),
+           ("auto", hb, p_small, abi.MODE_DEDUP, abi.FLAG_STATE_MACHINE | abi.FLAG_ROUND_SKIP),
+           ("auto", hb, p_small, abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE)]
+    for route, b, pw, mode, flags in seq:
+        g, o = run_both(eng, abi.config(mode, flags | ROUTES[route], 3), b, pw, None, _start_states(b.n_instances))
+        assert o[2] > 0
+        assert_same(g, o)
+
+
 def test_epoch_table_recycling(eng):
     """DEDUP/RoundSkip tables tag entries with per-instance epochs; with few
     epoch bits (AGNES_FLAG_EPOCH_BITS(30)) the tables are cleared every 3 instances."""
