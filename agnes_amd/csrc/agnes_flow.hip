@@ -489,10 +489,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                                                   : (t8[1] & 0xFEFEFEFEu) | ((r8[1] | ((r8[1] & 0x7F7F7F7Fu) + RK)) & 0x80808080u);
                     const uint32_t mA = max(max(val[0], val[1]), max(val[2], val[3]));
                     const uint32_t mB = max(max(val[4], val[5]), max(val[6], val[7]));
-                    const bool okA = bad0 == 0u && mA < recA.z && inst[0] == idA && inst[1] == idA && inst[2] == idA &&
-                                     inst[3] == idA;
-                    const bool okB = bad1 == 0u && mB < recB.z && inst[4] == idB && inst[5] == idB && inst[6] == idB &&
-                                     inst[7] == idB;
+                    /* a unit names its instance: the OR of the four ids XOR the id is zero (three
+                     * bitwise ops, not four compares whose lane masks are rebuilt as bits) */
+                    const uint32_t dA = (inst[0] ^ idA) | (inst[1] ^ idA) | (inst[2] ^ idA) | (inst[3] ^ idA);
+                    const uint32_t dB = (inst[4] ^ idB) | (inst[5] ^ idB) | (inst[6] ^ idB) | (inst[7] ^ idB);
+                    const bool okA = (bad0 | dA) == 0u && mA < recA.z;
+                    const bool okB = (bad1 | dB) == 0u && mB < recB.z;
                     all_ok = !ballot((actA && !okA) || (actB && !okB));
                     okb0 = actA ? 0xFFFFFFFFu : 0u;
                     okb1 = actB ? 0xFFFFFFFFu : 0u;
