@@ -399,6 +399,11 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
                 an[1] += an[0]; an[2] += an[1]; an[3] += an[2];
                 const uint32_t iv = scan(av[3]), in_ = scan(an[3]);
                 const uint32_t cv = ld_carry ? vw[K] : 0u, cn = ld_carry ? vn[K] : 0u;
+                /* a quiet key: even the bucket's running sums after its last vote of the
+                 * chunk stay at or below q2, so every vote of it is Init (code NONE, already
+                 * in code[]) -- the common case for the few early next-round votes, and for a
+                 * round's first chunk.  Uniform; the sums stay below 2^31 in this domain. */
+                if (rfl(cv + cn) + rdl(iv, 63u) + rdl(in_, 63u) > I.q2) {
                 /* sum > q2  <=>  lane-local prefix > q2 - carry - exclusive wave prefix */
                 const int32_t tv = (int32_t)(I.q2 - cv - (iv - av[3]));
                 const int32_t tn = (int32_t)(I.q2 - cn - (in_ - an[3]));
@@ -421,6 +426,7 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
                                           : (qn ? AGNES_CODE_POLKA_NIL : (qa ? AGNES_CODE_POLKA_ANY : AGNES_CODE_NONE));
                         code[s] = ((inb >> s) & 1u) ? ev : code[s];
                     }
+                }
                 }
                 if (st_carry && lane == 63u) {
                     vw[K] = cv + iv;
@@ -450,10 +456,12 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
                     as[1] += as[0]; as[2] += as[1]; as[3] += as[2];
                     const uint32_t is = scan(as[3]);
                     const uint32_t cs = ld_carry ? skw[kr] : 0u;
-                    const int32_t ts = (int32_t)(I.q1 - cs - (is - as[3]));
+                    if (rfl(cs) + rdl(is, 63u) > I.q1) { /* else quiet: no vote of the round crosses +1/3 */
+                        const int32_t ts = (int32_t)(I.q1 - cs - (is - as[3]));
 #pragma unroll
-                    for (uint32_t s = 0; s < VPL; ++s)
-                        if (((inb >> s) & 1u) && (int32_t)as[s] > ts) code[s] |= AGNES_CODE_SKIP;
+                        for (uint32_t s = 0; s < VPL; ++s)
+                            if (((inb >> s) & 1u) && (int32_t)as[s] > ts) code[s] |= AGNES_CODE_SKIP;
+                    }
                     if (st_carry && lane == 63u) skw[kr] = cs + is;
                     __builtin_amdgcn_wave_barrier();
                 }
