@@ -81,7 +81,7 @@ WORKLOADS = {
                     "stream, split over ranks and per rank over segments; one all_gather of partial tallies",
                gen=dict(n_instances=1, n_vals=1_000_000, rounds_min=1, rounds_max=1, nil_permille=200),
                power=(abi.POWER_ZIPF, 1, 1_000_000, 1), mode=abi.MODE_REFERENCE, flags=0,
-               max_rounds=1, scaling="strong", one_instance=True, segments=1024),
+               max_rounds=1, scaling="strong", one_instance=True, segments=2048),
     "c5d": dict(desc="C5 in DEDUP mode: 1 instance x 1M validators (Zipf power), 10% duplicates + 10% "
                      "equivocations; one all_reduce(MIN) of first-seen indices + one all_gather of "
                      "partial tallies",
@@ -220,6 +220,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--segments", type=int, default=0,
+                    help="c5/c5d: segments per GPU (one wave each; default: the workload's)")
     args = ap.parse_args()
 
     rank, world, local = adist.env()
@@ -410,7 +412,7 @@ def bench_one_instance(args, w, eng, rank, world):
         tmask = torch.empty(max(hi - lo, 1), dtype=torch.uint8, device=eng.device)
         batch = dataclasses.replace(batch, type=tmask)
 
-    segs = max(1, min(w["segments"], max(1, (hi - lo) // 4)))
+    segs = max(1, min(args.segments or w["segments"], max(1, (hi - lo) // 4)))
     off = torch.from_numpy(adist.segment_offsets(hi - lo, segs).view(np.int64)).to(eng.device)
 
     def tc(one, o, counts):  # on the current stream: a graph capture's while capturing
