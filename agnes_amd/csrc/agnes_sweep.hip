@@ -1,20 +1,14 @@
 /*
- * agnes_sweep.hip — the fused hot path for REFERENCE batches without RoundSkip
- * (BASELINE C2/C3): ingest -> weight gather -> ordered tally -> quorum -> event
+ * agnes_sweep.hip — the walk kernel of the REFERENCE route without RoundSkip
+ * (BASELINE C2/C3): the instances the flow kernel (agnes_flow.hip) hands off
+ * through the walk list (unaligned offsets, long instances, power sets outside
+ * the flow domain): ingest -> weight gather -> ordered tally -> quorum -> event
  * -> State::apply, ONE pass over the votes (consensus_executor.rs:61-69).
  *
- * Two instantiations of one kernel body:
- *   STREAM  a work queue hands out batches of up to SB consecutive instances.  A
- *           batch whose offsets are multiples of 4 and whose instances are all in
- *           the stream domain (u32 power set, len * maxpow < 2^30, maxpow < 2^22)
- *           is walked as ONE vote stream in 256-vote chunks (lane l = votes
- *           4l..4l+3, so a lane never straddles an instance); the instances a
- *           chunk straddles are its segments.  Any other batch goes to the walk
- *           list (its States copied through unchanged).
- *   WALK    the walk list, statically split over the waves: each instance is a
- *           stream of its own starting at its first vote rounded down to 4 (the
- *           votes before it masked); an instance whose sums may reach 2^31 goes to
- *           the i64 LIST kernel.
+ * The walk list is statically split over the waves: each instance is a stream of
+ * its own, in 256-vote chunks (lane l = votes 4l..4l+3), starting at its first
+ * vote rounded down to 4 (the votes before it masked); an instance whose sums may
+ * reach 2^31 goes to the i64 LIST kernel.
  * The vote columns arrive by non-temporal LDS-DMA one chunk ahead; every address
  * is a uniform 64-bit base plus a 32-bit lane offset (saddr forms: no 64-bit
  * vector arithmetic per chunk).
@@ -44,10 +38,9 @@
  *        vote before C (the label of a later nil PolkaValue vote is that value,
  *        round_votes.rs:50-54), so no label is ever searched.
  *
- * States: read from states_in (staged in LDS by DMA when the batch starts),
- * updated through per-instance shadow records, written to states_out when the
- * batch ends; batches sent to the walk list are copied through unchanged (the
- * WALK and LIST kernels then work in place on states_out).
+ * States: in place in states_out (the flow kernel copied the walked instances'
+ * States through), staged in LDS by DMA when an instance starts, updated through
+ * per-instance shadow records, written back when it ends.
  */
 #include "agnes_fast.h"
 
@@ -57,7 +50,6 @@ using namespace agnes::fast;
 
 constexpr uint32_t SB = 16u;    /* instances per batch (header offsets in lanes 0..SB) */
 constexpr uint32_t HI = 32u;    /* header lanes HI + k: per-instance data of instance k */
-constexpr uint32_t SMALLB = 4u; /* batch size of the work queue's tail                  */
 constexpr uint32_t REC = 32u;   /* bytes of an instance record                          */
 /* instance record words: quorum threshold, row base in the power table, validators
  * of its set (0: the set does not exist), State view (State.round if in 0..255 else
@@ -134,7 +126,7 @@ struct Hdr {
     uint32_t ready;  /* phase 2 done                                                    */
 };
 
-template <bool PC, bool SM, bool WALK>
+template <bool PC, bool SM>
 __global__ __launch_bounds__(256) void sweep(agnes_tally_args a, uint32_t lds_per_wave) {
     const uint32_t lane = lane_id();
     const uint32_t wave = rfl(threadIdx.x >> 6);
@@ -156,38 +148,26 @@ __global__ __launch_bounds__(256) void sweep(agnes_tally_args a, uint32_t lds_pe
     const uint32_t cw = 4u * R; /* one carry copy: vw[2R] then vn[2R] */
     uint32_t* const itab = reinterpret_cast<uint32_t*>(base + PF_BYTES + carry_bytes(R));
     unsigned char* const sb = base + PF_BYTES + carry_bytes(R) + SB * REC;
-    /* WALK works in place: the STREAM kernel copied the walked instances' States */
-    const agnes_state* const st_in = (!WALK && a.states_in) ? a.states_in : a.states;
+    /* in place: the flow kernel copied the walked instances' States */
+    const agnes_state* const st_in = a.states;
     uint32_t cpar = 0;
     uint64_t pf_at = ~0ull;
     uint32_t bad = 0;
     /* r < R <=> ((r & 0x7F) + 128 - R) < 128 and r < 128 (R <= 15) */
     const uint32_t RK = (128u - R) * 0x01010101u;
 
-    /* ---- work: STREAM batches from the queue, WALK entries of the walk list ---- */
-    const uint32_t qn = gridDim.x < QN ? gridDim.x : QN;
-    const uint32_t qk = blockIdx.x % qn;
-    uint32_t* const ctr = a.list_count + 1u + qk;
-    const uint64_t NB = (uint64_t)(n / SB) * 7u / 8u;
-    uint32_t wl = 0, wend = 0; /* WALK: this wave's slice of the walk list */
-    if (WALK) {
+    /* ---- work: this wave's slice of the walk list, one instance at a time ---- */
+    uint32_t wl = 0, wend = 0;
+    {
         const uint32_t L = rfl(*(volatile uint32_t*)(a.list_count + AGNES_WALK_COUNT));
         const uint32_t W = gridDim.x * AGNES_WAVES_PER_BLOCK, gw = blockIdx.x * AGNES_WAVES_PER_BLOCK + wave;
         wl = (uint32_t)((uint64_t)L * gw / W);
         wend = (uint32_t)((uint64_t)L * (gw + 1u) / W);
     }
     auto range_of = [&](uint32_t t, uint32_t& s0, uint32_t& e0) {
-        if (WALK) {
-            const uint32_t e = wl + t;
-            s0 = e < wend ? rfl(a.walk[e]) : n;
-            e0 = e < wend ? s0 + 1u : n;
-            return;
-        }
-        const uint64_t b = (uint64_t)t * qn + qk;
-        const uint64_t s = b < NB ? b * SB : NB * SB + (b - NB) * SMALLB;
-        const uint64_t e = s + (b < NB ? SB : SMALLB);
-        s0 = s < n ? (uint32_t)s : n;
-        e0 = e < n ? (uint32_t)e : n;
+        const uint32_t e = wl + t;
+        s0 = e < wend ? rfl(a.walk[e]) : n;
+        e0 = e < wend ? s0 + 1u : n;
     };
     /* header phase 1: offsets and sets */
     auto hdr1 = [&](Hdr& h) {
@@ -216,7 +196,7 @@ __global__ __launch_bounds__(256) void sweep(agnes_tally_args a, uint32_t lds_pe
         const uint64_t ob = u64of(shfl(h.olo, k), shfl(h.ohi, k));
         const uint64_t oe = u64of(shfl(h.olo, k + 1u), shfl(h.ohi, k + 1u));
         const uint64_t len = oe > ob ? oe - ob : 0ull;
-        bool f31 = false, f30 = false;
+        bool f31 = false;
         uint32_t q2 = 0;
         if (il) {
             const uint32_t set = h.olo;
@@ -224,27 +204,17 @@ __global__ __launch_bounds__(256) void sweep(agnes_tally_args a, uint32_t lds_pe
                 const agnes_set_info si = a.sets[set];
                 const uint64_t wmax = len * (uint64_t)si.maxpow; /* no sum of the instance exceeds it */
                 f31 = si.fast && len < (1ull << 30) && wmax < (1ull << 31);
-                f30 = f31 && wmax < (1ull << 30) && si.maxpow < (1u << 22);
                 /* 3s > 2t <=> s > q2; a q2 >= wmax is never crossed, so min(q2, wmax) */
                 const uint64_t qq = (uint64_t)si.q2 < wmax ? (uint64_t)si.q2 : wmax;
                 q2 = (uint32_t)(qq < 0x7FFFFFFFull ? qq : 0x7FFFFFFFull);
             } else {
-                f31 = f30 = len < (1ull << 30); /* no such set: every vote INVALID */
+                f31 = len < (1ull << 30); /* no such set: every vote INVALID */
             }
         }
         h.q2 = q2;
         const uint32_t full = (uint32_t)((1ull << m) - 1ull);
         h.f31 = (uint32_t)(ballot(f31) >> HI) & full;
-        const uint32_t f30m = (uint32_t)(ballot(f30) >> HI) & full;
-        if (WALK) {
-            h.stream = m == 1u && h.f31 == 1u;
-        } else {
-            const uint64_t Ol = u64of(h.olo, h.ohi);
-            const uint64_t On = u64of(shfl(h.olo, lane + 1u), shfl(h.ohi, lane + 1u));
-            const bool badl = lane <= m && (((h.olo & 3u) != 0u) || (lane < m && On < Ol));
-            const uint64_t O0 = u64of(rdl(h.olo, 0u), rdl(h.ohi, 0u)), Om = u64of(rdl(h.olo, m), rdl(h.ohi, m));
-            h.stream = m > 0u && !ballot(badl) && f30m == full && Om - O0 < (1ull << 30);
-        }
+        h.stream = m == 1u && h.f31 == 1u;
         h.ready = 1;
     };
     /* the batch's States into LDS (64 B each, lane l's 16 B at 16 l) */
@@ -270,9 +240,7 @@ __global__ __launch_bounds__(256) void sweep(agnes_tally_args a, uint32_t lds_pe
     uint32_t dc_code = 0, dc_pos = 0; /* dc_pos: byte mask of the lane's votes to store */
     auto flush = [&]() {
         if (dc_at != ~0ull) {
-            if (!WALK) {
-                if (dc_pos) sstore4(a.codes + dc_at, p0, dc_code);
-            } else if (dc_pos == 0xFFFFFFFFu) {
+            if (dc_pos == 0xFFFFFFFFu) {
                 sstore4(a.codes + dc_at, p0, dc_code);
             } else if (dc_pos) {
 #pragma unroll
@@ -286,13 +254,9 @@ __global__ __launch_bounds__(256) void sweep(agnes_tally_args a, uint32_t lds_pe
     Hdr H, N;
     uint32_t tq = 0; /* lane 0: slot of the batch after N (atomic in flight) */
     {
-        uint32_t t = 0;
-        if (!WALK && lane == 0) t = atomicAdd(ctr, 2u);
-        t = rdl(t, 0u);
-        range_of(t, H.s0, H.e0);
-        range_of(t + 1u, N.s0, N.e0);
-        if (!WALK && lane == 0) tq = atomicAdd(ctr, 1u);
-        else if (WALK) tq = 2u;
+        range_of(0u, H.s0, H.e0);
+        range_of(1u, N.s0, N.e0);
+        tq = 2u;
     }
     if (H.s0 >= H.e0) return;
     hdr1(H);
@@ -304,12 +268,7 @@ __global__ __launch_bounds__(256) void sweep(agnes_tally_args a, uint32_t lds_pe
         const uint32_t m = H.e0 - H.s0;
         bool smf = SM; /* the State views are not yet set up from the staged States */
         if (!H.stream) {
-            if (!WALK) { /* not one vote stream: the walk list */
-                uint32_t w0 = 0;
-                if (lane == 0) w0 = atomicAdd(a.list_count + AGNES_WALK_COUNT, m);
-                w0 = rdl(w0, 0u);
-                if (lane < m) a.walk[w0 + lane] = H.s0 + lane;
-            } else if (lane == 0) { /* sums may reach 2^31: the i64 LIST kernel */
+            if (lane == 0) { /* sums may reach 2^31: the i64 LIST kernel */
                 if (rdl(H.olo, 1u) != rdl(H.olo, 0u) || rdl(H.ohi, 1u) != rdl(H.ohi, 0u))
                     a.list[atomicAdd(a.list_count, 1u)] = H.s0;
             }
@@ -329,16 +288,15 @@ __global__ __launch_bounds__(256) void sweep(agnes_tally_args a, uint32_t lds_pe
             }
             /* the stream: starts relative to its first chunk */
             const uint64_t O0 = u64of(rdl(H.olo, 0u), rdl(H.ohi, 0u));
-            const uint64_t S0 = WALK ? (O0 & ~3ull) : O0;
+            const uint64_t S0 = O0 & ~3ull;
             const uint32_t s0lo = (uint32_t)S0;
-            const uint32_t lo0 = (uint32_t)O0 - s0lo; /* WALK: votes before the instance in its first chunk */
+            const uint32_t lo0 = (uint32_t)O0 - s0lo; /* votes before the instance in its first chunk */
             const uint32_t Lend = rdl(H.olo, m) - s0lo;
             const uint32_t rl = lane == 0u ? 0u : H.olo - s0lo;
             const uint32_t rn = shfl(rl, lane + 1u);
             const uint64_t NE = ballot(lane < m && rn > rl);
             const uint32_t relv = lane <= m ? rl : 0x7FFFFFFFu;
             const uint64_t mm64 = (1ull << m) - 1ull;
-            bool fresh = true;
 
             for (uint32_t rc = 0; rc < Lend; rc += CHUNK) {
                 const uint64_t c = S0 + rc;
@@ -383,8 +341,8 @@ __global__ __launch_bounds__(256) void sweep(agnes_tally_args a, uint32_t lds_pe
                 const uint32_t* const rk = itab + 8u * kln;
                 const uint4 rec = *reinterpret_cast<const uint4*>(rk); /* q2, pbase, nv of its set, smw */
                 /* the lane's votes in the stream (byte mask) */
-                uint32_t posb = p0 < hi_r ? 0xFFFFFFFFu : 0u;
-                if (WALK) {
+                uint32_t posb;
+                {
                     const uint32_t bh = hi_r > p0 ? (hi_r - p0 < 4u ? hi_r - p0 : 4u) : 0u;
                     const uint32_t bl = lo_r > p0 ? (lo_r - p0 < 4u ? lo_r - p0 : 4u) : 0u;
                     posb = below_bytes(bh) & ~below_bytes(bl);
@@ -424,16 +382,9 @@ __global__ __launch_bounds__(256) void sweep(agnes_tally_args a, uint32_t lds_pe
                     const uint32_t rt_bad = R == 1u ? (t4 & 0xFEFEFEFEu) | r4
                                                     : (t4 & 0xFEFEFEFEu) | ((r4 | ((r4 & 0x7F7F7F7Fu) + RK)) & 0x80808080u);
                     key4 = ((r4 << 1) & 0xFEFEFEFEu) | t4;
-                    if (!WALK) {
-                        const uint32_t vmax = max(max(val[0], val[1]), max(val[2], val[3]));
-                        const bool lane_ok = rt_bad == 0u && vmax < rec.z && inst[0] == id && inst[1] == id &&
-                                             inst[2] == id && inst[3] == id;
-                        all_ok = !ballot(!lane_ok && posb != 0u);
-                    } else {
-                        all_ok = false;
-                    }
+                    all_ok = false; /* the exact per-vote checks */
                     okb = posb;
-                    if (!all_ok) { /* the exact per-vote checks */
+                    {
                         okb = 0;
 #pragma unroll
                         for (uint32_t s = 0; s < VPL; ++s) {
@@ -465,14 +416,11 @@ __global__ __launch_bounds__(256) void sweep(agnes_tally_args a, uint32_t lds_pe
                 /* a gather from HBM retires before the DMA below is issued: a wait on it
                  * behind the DMA would wait for the DMA too (in-order vmcnt) */
                 if (!PC) asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
-                if (!WALK && fresh && !N.ready && N.s0 < N.e0) hdr2(N);
-                fresh = false;
                 /* the next chunk by LDS-DMA (this stream's, or the next batch's first),
                  * then the previous chunk's codes */
                 {
                     uint64_t nc = ~0ull;
                     if (rc + CHUNK < Lend) nc = c + CHUNK;
-                    else if (!WALK && N.s0 < N.e0 && N.ready && N.stream) nc = u64of(rdl(N.olo, 0u), rdl(N.ohi, 0u));
                     if (nc != ~0ull && nc + CHUNK <= NV) {
                         dma_chunk(nc);
                         pf_at = nc;
@@ -672,8 +620,7 @@ __global__ __launch_bounds__(256) void sweep(agnes_tally_args a, uint32_t lds_pe
         H = N;
         dma_states(H);
         range_of(rdl(tq, 0u), N.s0, N.e0); /* the batch after, grabbed one batch ago */
-        if (!WALK && lane == 0) tq = atomicAdd(ctr, 1u);
-        else if (WALK) tq += 1u;
+        tq += 1u;
         hdr1(N);
     }
     flush();
@@ -691,13 +638,13 @@ bool agnes_sweep_supported(const agnes_tally_args* a) {
     return a->max_rounds <= 15u; /* keys round * 2 + type < 31: one bit each in a u32 */
 }
 
-template <bool SM, bool WALK>
+template <bool SM>
 static hipError_t launch_sweep_k(const agnes_tally_args* a, int num_cus, hipStream_t st) {
     const uint32_t n = a->vb.n_instances;
     if (n == 0) return hipSuccess;
     using agnes::sweep::sweep;
-    const void* fns[2] = {reinterpret_cast<const void*>(&sweep<false, SM, WALK>),
-                          reinterpret_cast<const void*>(&sweep<true, SM, WALK>)};
+    const void* fns[2] = {reinterpret_cast<const void*>(&sweep<false, SM>),
+                          reinterpret_cast<const void*>(&sweep<true, SM>)};
     const uint32_t lpw = agnes::sweep::lds_bytes(SM, a->max_rounds);
     const uint64_t wave_lds = (uint64_t)lpw * AGNES_WAVES_PER_BLOCK;
     const uint64_t pcb = agnes::align16(4ull * a->n_sets * a->n_vals);
@@ -738,30 +685,27 @@ static hipError_t launch_sweep_k(const agnes_tally_args* a, int num_cus, hipStre
         if (e != hipSuccess) return e;
     }
     const uint64_t ncu = (uint64_t)(num_cus > 0 ? num_cus : 256);
-    /* STREAM: enough waves for the batches, at most the resident grid; WALK: one
-     * block per CU (the walk list is a fallback, usually empty) */
+    /* one block per CU (the walk list is a fallback, usually empty) */
     uint64_t blocks = ((uint64_t)n + 4u * AGNES_WAVES_PER_BLOCK - 1u) / (4u * AGNES_WAVES_PER_BLOCK);
-    const uint64_t cap = WALK ? ncu : ncu * (uint64_t)o->per_cu;
+    const uint64_t cap = ncu;
     if (blocks > cap) blocks = cap;
     if (blocks == 0) blocks = 1;
     if (o->pc)
-        hipLaunchKernelGGL((sweep<true, SM, WALK>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
+        hipLaunchKernelGGL((sweep<true, SM>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
     else
-        hipLaunchKernelGGL((sweep<false, SM, WALK>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
+        hipLaunchKernelGGL((sweep<false, SM>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
     return hipGetLastError();
 }
 
 hipError_t agnes_launch_sweep(const agnes_tally_args* a, int num_cus, hipStream_t st) {
     const bool sm = (a->flags & AGNES_FLAG_STATE_MACHINE) != 0 && a->states != nullptr;
+    if (!agnes_flow_supported(a)) return hipErrorInvalidValue; /* max_rounds <= 15 always fits */
     hipError_t e;
-    if (agnes_flow_supported(a)) { /* flow streams; every other batch to the walk list */
+    { /* flow streams; every other batch to the walk list */
         AgnesKt kt("flow", st);
         e = agnes_launch_flow(a, num_cus, st);
-    } else {
-        AgnesKt kt("sweep", st);
-        e = sm ? launch_sweep_k<true, false>(a, num_cus, st) : launch_sweep_k<false, false>(a, num_cus, st);
     }
     if (e != hipSuccess) return e;
     AgnesKt kt("sweep_walk", st);
-    return sm ? launch_sweep_k<true, true>(a, num_cus, st) : launch_sweep_k<false, true>(a, num_cus, st);
+    return sm ? launch_sweep_k<true>(a, num_cus, st) : launch_sweep_k<false>(a, num_cus, st);
 }

@@ -14,8 +14,6 @@ from . import abi
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, "libagnes_amd.so")
-if os.environ.get("AGNES_LIB"):  # development: an in-tree experiment build (agnes_amd/_exp/)
-    LIB_PATH = os.path.join(ROOT, os.environ["AGNES_LIB"])
 HEADER = os.path.join(ROOT, "include", "agnes.h")
 
 _STATUS = {abi.E_INVALID: "AGNES_E_INVALID", abi.E_UNSUPPORTED: "AGNES_E_UNSUPPORTED",

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import struct
 import os
 import sys
@@ -36,8 +37,6 @@ BYTES_PER_VOTE = 15            # 14 B canonical SoA in + 1 B code out (BASELINE.
 # algorithmic bytes per vote of each engine kernel (names: agnes_kernel_times)
 KERNEL_BYTES_PER_VOTE = {
     "flow": 15,          # instance, value, validator u32 + round, type u8 in; code u8 out
-    "sweep": 15,
-    "tally_stream": 15,
     "tally_fast": 15,
     "tally_wide": 15,
     "apply_codes": 2,    # code + round u8 in (+ the message bytes written back)
@@ -48,9 +47,7 @@ KERNEL_SYMBOLS = {
     # template parameters: PC (power table in LDS), SM (State machine), R1 (one round);
     # c2 runs flow<true, true, true>, c3 flow<false, true, false> (rocprofv3 names them)
     "flow": "agnes::flow::flow<PC, SM, R1>",
-    "sweep": "agnes::sweep::sweep<PC, SM, false>",
-    "sweep_walk": "agnes::sweep::sweep<PC, SM, true>",
-    "tally_stream": "agnes::stream::tally_stream<false, *>",
+    "sweep_walk": "agnes::sweep::sweep<PC, SM>",
     "tally_fast": "agnes::fast::tally_fast<...>",
     "tally_wide": "agnes::tally_kernel<true, ...>",
     "apply_codes": "agnes::apply::apply_codes<RoundSkip>",
@@ -135,6 +132,14 @@ def host_cpu() -> dict:
             "cgroup_cpu_quota": quota}
 
 
+def cpu_threads(cpu: dict) -> int:
+    """Threads the CPU legs use: the CPUs this process may run on, capped by the
+    cgroup CPU quota (a box may show 256 CPUs in its affinity mask and grant 16)."""
+    n = max(1, cpu["affinity"])
+    q = cpu.get("cgroup_cpu_quota")
+    return max(1, min(n, math.ceil(q))) if q else n
+
+
 def cpu_baseline(eng, cfg, batch, power, states0, set_of_instance):
     """The checker (oracle/, scalar C, one pthread per CPU this process may use,
     over instances) on the same batch; best of 5."""
@@ -149,7 +154,7 @@ def cpu_baseline(eng, cfg, batch, power, states0, set_of_instance):
     hb = ol.HostBatch(h["instance"][:nv], h["round"][:nv], h["type"][:nv], h["value"][:nv],
                       h["validator"][:nv], off.copy(), set_of_instance[:limit].copy())
     cpu = host_cpu()
-    threads = max(1, cpu["affinity"])
+    threads = cpu_threads(cpu)
     best = None
     for _ in range(5):
         t0 = time.perf_counter()
@@ -622,7 +627,7 @@ def bench_wire(args, w, eng, rank, world):
             # and OpenSSL's verdicts on the fixture records through libcrypto (check)
             import subprocess
             cpu = host_cpu()
-            procs = max(1, min(cpu["affinity"], int(cpu["cgroup_cpu_quota"] or cpu["affinity"])))
+            procs = cpu_threads(cpu)
             rate = None
             try:
                 r = subprocess.run(["openssl", "speed", "-seconds", "3", "-multi", str(procs), "ed25519"],

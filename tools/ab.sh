@@ -9,7 +9,7 @@ fi
 summ() { python3 -c "import json,sys; d=json.loads(open('$1').read().strip().splitlines()[-1]); print('$2', round(d['ms_per_step'],4), round(d['roofline'].get('path_frac') or 0,3), {k:round(v['avg_ms'],4) for k,v in d['kernels'].items()})"; }
 for r in $(seq ${REPS:-2}); do
   for c in ${CFGS:-c2}; do
-    AGNES_LIB=agnes_amd/_exp/lib_base.so timeout -k 10 200 python3 bench.py --config $c --no-cpu-baseline > gpurun_out/ab_base_$c.json 2> gpurun_out/ab_base_$c.err || { tail -20 gpurun_out/ab_base_$c.err; exit 1; }
+    timeout -k 10 200 python3 tools/withlib.py agnes_amd/_exp/lib_base.so bench.py --config $c --no-cpu-baseline > gpurun_out/ab_base_$c.json 2> gpurun_out/ab_base_$c.err || { tail -20 gpurun_out/ab_base_$c.err; exit 1; }
     summ gpurun_out/ab_base_$c.json "base $c"
     timeout -k 10 200 python3 bench.py --config $c --no-cpu-baseline > gpurun_out/ab_new_$c.json 2> gpurun_out/ab_new_$c.err || { tail -20 gpurun_out/ab_new_$c.err; exit 1; }
     summ gpurun_out/ab_new_$c.json "new  $c"

@@ -2,7 +2,7 @@
 """Ablation builds of the flow kernel (development tool): each variant is
 agnes_flow.hip with one text substitution (timing only: the results are wrong by
 design), linked with the other engine objects into agnes_amd/_exp/lib_<name>.so.
-Run on the GPU box with  AGNES_LIB=agnes_amd/_exp/lib_<name>.so python tools/kbench.py ...
+Run on the GPU box with  python tools/withlib.py agnes_amd/_exp/lib_<name>.so tools/kbench.py ...
 
 usage: tools/ablate.py build   |   tools/ablate.py list"""
 import os
