@@ -28,13 +28,13 @@ struct agnes_ctx {
     agnes_set_info* d_sets = nullptr;
     uint32_t n_sets = 0;
     uint32_t n_vals = 0;
-    unsigned long long* d_err = nullptr;
+    unsigned long long* d_err = nullptr; /* the invalid-vote count, then AGNES_QUEUE_WORDS work-queue
+                                            counters (agnes_internal.h): one memset per call */
     hipStream_t last_stream = nullptr;
     bool used = false;               /* a call has enqueued work on last_stream */
     hipEvent_t order_ev = nullptr;   /* orders a call on another stream after it */
     bool all_fast = false;     /* every set inside the u32 fast domain */
-    uint32_t* d_list = nullptr; /* [list_cap] deferred instances, [list_cap] walk list, then
-                                   AGNES_QUEUE_WORDS counters (agnes_internal.h) */
+    uint32_t* d_list = nullptr; /* [list_cap] deferred instances, [list_cap] walk list */
     uint32_t list_cap = 0;
     uint64_t* d_scan = nullptr; /* edge-offset scan: block totals */
     uint64_t scan_cap = 0;
@@ -215,12 +215,12 @@ int agnes_ctx_create(int device, agnes_ctx** out) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
         cus > 0)
         c->num_cus = cus;
-    hipError_t e = hipMalloc(&c->d_err, sizeof(unsigned long long));
+    hipError_t e = hipMalloc(&c->d_err, AGNES_COUNTER_BYTES);
     if (e != hipSuccess) {
         delete c;
         return status_of(e);
     }
-    (void)hipMemset(c->d_err, 0, sizeof(unsigned long long));
+    (void)hipMemset(c->d_err, 0, AGNES_COUNTER_BYTES);
     *out = c;
     return AGNES_OK;
 }
@@ -302,15 +302,16 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     AGNES_ORDER(c, st);
     const bool wide_all = b->weight != nullptr || carry != nullptr || !sets_fast;
     if (!wide_all && (!c->d_list || c->list_cap < b->n_instances)) {
-        /* [list_cap] deferred instances | [list_cap] walk list | counters */
+        /* [list_cap] deferred instances | [list_cap] walk list */
         AGNES_TRY(hipStreamSynchronize(st));
         if (c->d_list) (void)hipFree(c->d_list);
         c->d_list = nullptr;
         c->list_cap = 0;
-        AGNES_TRY(hipMalloc(&c->d_list, (2 * (size_t)b->n_instances + AGNES_QUEUE_WORDS) * sizeof(uint32_t)));
+        AGNES_TRY(hipMalloc(&c->d_list, (2 * (size_t)b->n_instances + 1) * sizeof(uint32_t)));
         c->list_cap = b->n_instances;
     }
-    AGNES_TRY(hipMemsetAsync(c->d_err, 0, sizeof(unsigned long long), st));
+    /* the invalid count and the work-queue counters: one memset */
+    AGNES_TRY(hipMemsetAsync(c->d_err, 0, wide_all ? sizeof(unsigned long long) : AGNES_COUNTER_BYTES, st));
     agnes_tally_args a;
     std::memset(&a, 0, sizeof(a));
     a.vb = *b;
@@ -342,7 +343,7 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     a.n_invalid = c->d_err;
     a.list = c->d_list;
     a.walk = c->d_list ? c->d_list + (size_t)c->list_cap : nullptr;
-    a.list_count = c->d_list ? c->d_list + 2 * (size_t)c->list_cap : nullptr;
+    a.list_count = c->d_list ? reinterpret_cast<uint32_t*>(c->d_err + 1) : nullptr;
     /* DEDUP / RoundSkip tables tag entries with (instance epoch, local vote index):
      * the local index of any vote is < n_votes, so it needs bit_length(n_votes - 1) bits */
     if (cfg->mode == AGNES_MODE_DEDUP || (cfg->flags & AGNES_FLAG_ROUND_SKIP)) {

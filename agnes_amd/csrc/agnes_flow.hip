@@ -38,6 +38,8 @@
  *        (in this domain a nil PolkaValue's label is the last non-nil one's,
  *        round_votes.rs:50-54, and P1 / C are crossed by non-nil votes).
  */
+#include <type_traits>
+
 #include "agnes_fast.h"
 
 namespace agnes {
@@ -47,8 +49,10 @@ using namespace agnes::fast;
 constexpr uint32_t LV = 8u, CH = 64u * LV; /* votes per lane, per chunk */
 /* DMA slot: each column of the chunk as a contiguous image */
 constexpr uint32_t F_INST = 0, F_VALUE = 2048, F_VAL = 4096, F_ROUND = 6144, F_TYPE = 6656, F_BYTES = 7168;
-constexpr uint32_t FB = 16u;    /* instances per batch (header offsets in lanes 0..FB) */
-constexpr uint32_t HI = 32u;    /* header lanes HI + k: per-instance data of instance k */
+/* instances per batch: header offsets in lanes 0..FB, per-instance data in lane k.  A
+ * batch's stream ends in a partial chunk, so the bigger the batch the fewer idle lanes
+ * (C2: 16 instances = 3,200 votes in 7 chunks, 32 = 6,400 in 13) */
+constexpr uint32_t FB = 32u;
 constexpr uint32_t SMALLB = 4u; /* batch size of the work queue's tail                  */
 /* instance record, 12 words: quorum threshold, power-row base, validators of its set
  * (0: no such set); the State machine's view: the roles its step keeps (one byte per
@@ -135,14 +139,15 @@ __device__ __forceinline__ void sstore8(void* base, uint32_t voff, uint32_t d0, 
 
 /* a batch: instances [s0, e0).  Its header is built in three stages, each one
  * chunk apart so that its loads land behind the chunk DMA's wait: (1) offsets
- * (lanes 0..m, clamped to n_votes) and sets (lanes HI + k) requested; (2) lengths
+ * (lanes 0..m, clamped to n_votes) and sets (lanes k < m) requested; (2) lengths
  * and the checks on the offsets, the sets' constants requested; (3) the quorum
  * thresholds and whether the batch is one flow stream. */
 struct Hdr {
     uint32_t s0, e0;
-    uint32_t olo, ohi;  /* lanes 0..m: offset; lane HI + k: set (in olo)        */
-    uint32_t q2, mp;    /* lane HI + k: set q2, maxpow; after stage 3 q2 = threshold */
-    uint32_t fa, ln;    /* lane HI + k: set fast flag (2: no such set), length   */
+    uint32_t olo, ohi;  /* lanes 0..m: offset                                     */
+    uint32_t hs;        /* lane k < m: the power set of instance k                */
+    uint32_t q2, mp;    /* lane k: set q2, maxpow; after stage 3 q2 = threshold   */
+    uint32_t fa, ln;    /* lane k: set fast flag (2: no such set), length         */
     uint32_t stage;     /* 1, 2, 3 (ready)                                       */
     uint32_t stream;    /* stage 2: the offsets pass; stage 3: walked by this kernel */
 };
@@ -181,7 +186,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
     const uint32_t qn = gridDim.x < QN ? gridDim.x : QN;
     const uint32_t qk = blockIdx.x % qn;
     uint32_t* const ctr = a.list_count + 1u + qk;
-    const uint64_t NB = (uint64_t)(n / FB) * 7u / 8u;
+    const uint64_t NB = (uint64_t)(n / FB) * 15u / 16u;
     auto range_of = [&](uint32_t t, uint32_t& s0, uint32_t& e0) {
         const uint64_t b = (uint64_t)t * qn + qk;
         const uint64_t s = b < NB ? b * FB : NB * FB + (b - NB) * SMALLB;
@@ -191,32 +196,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
     };
     auto hdr1 = [&](Hdr& h) { /* stage 1: offsets and sets requested */
         const uint32_t m = h.e0 - h.s0;
-        uint32_t lo = 0, hi = 0;
+        uint32_t lo = 0, hi = 0, hs = 0;
         if (m > 0u && lane <= m) {
             const uint64_t o = a.vb.offsets[h.s0 + lane];
             const uint64_t oc = o < NV ? o : NV;
             lo = (uint32_t)oc;
             hi = (uint32_t)(oc >> 32);
-        } else if (lane >= HI && lane < HI + m) {
-            const uint32_t k = h.s0 + lane - HI;
-            lo = a.vb.instance_set ? a.vb.instance_set[k] : (ns ? k % ns : 0u);
+        }
+        if (lane < m) {
+            const uint32_t k = h.s0 + lane;
+            hs = a.vb.instance_set ? a.vb.instance_set[k] : (ns ? k % ns : 0u);
         }
         h.olo = lo;
         h.ohi = hi;
+        h.hs = hs;
         h.stage = 1;
         h.stream = 0;
     };
     auto hdr2 = [&](Hdr& h) { /* stage 2: lengths, offset checks; set constants requested */
         const uint32_t m = h.e0 - h.s0;
-        const bool il = lane >= HI && lane < HI + m;
-        const uint32_t k = il ? lane - HI : 0u;
-        const uint64_t ob = u64of(shfl(h.olo, k), shfl(h.ohi, k));
-        const uint64_t oe = u64of(shfl(h.olo, k + 1u), shfl(h.ohi, k + 1u));
-        const uint64_t len = oe > ob ? oe - ob : 0ull;
+        const bool il = lane < m;
+        const uint64_t ob = u64of(h.olo, h.ohi);
+        const uint64_t oe = u64of(shfl(h.olo, lane + 1u), shfl(h.ohi, lane + 1u));
+        const uint64_t len = il && oe > ob ? oe - ob : 0ull;
         h.ln = len < (1ull << 31) ? (uint32_t)len : (1u << 31);
         uint32_t q2 = 0, mp = 0, fa = 2;
-        if (il && h.olo < ns) {
-            const agnes_set_info* const si = a.sets + h.olo;
+        if (il && h.hs < ns) {
+            const agnes_set_info* const si = a.sets + h.hs;
             q2 = si->q2;
             mp = si->maxpow;
             fa = si->fast;
@@ -224,16 +230,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
         h.q2 = q2;
         h.mp = mp;
         h.fa = fa;
-        const uint64_t Ol = u64of(h.olo, h.ohi);
-        const uint64_t On = u64of(shfl(h.olo, lane + 1u), shfl(h.ohi, lane + 1u));
-        const bool badl = (lane <= m && (h.olo & 3u) != 0u) || (lane < m && On < Ol);
+        const bool badl = (lane <= m && (h.olo & 3u) != 0u) || (lane < m && oe < ob);
         const uint64_t O0 = u64of(rdl(h.olo, 0u), rdl(h.ohi, 0u)), Om = u64of(rdl(h.olo, m), rdl(h.ohi, m));
         h.stream = m > 0u && !ballot(badl) && Om - O0 < (1ull << 30);
         h.stage = 2;
     };
     auto hdr3 = [&](Hdr& h) { /* stage 3: quorum thresholds; a flow stream or the walk list */
         const uint32_t m = h.e0 - h.s0;
-        const bool il = lane >= HI && lane < HI + m;
+        const bool il = lane < m;
         bool fl = true;
         uint32_t q2 = 0;
         if (il) {
@@ -256,8 +260,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
     auto dma_states = [&](const Hdr& h, uint32_t par) { /* the batch's States into LDS (64 B each) */
         const uint32_t m = h.e0 - h.s0;
         if (!SM || m == 0u) return;
-        glds16(reinterpret_cast<const unsigned char*>(st_in + h.s0) + 16u * (lane < 4u * m ? lane : 0u),
-               sb + par * (FB * 64u));
+        const unsigned char* const g = reinterpret_cast<const unsigned char*>(st_in + h.s0);
+        glds16(g + 16u * (lane < 4u * m ? lane : 0u), sb + par * (FB * 64u));
+        if (m > 16u) glds16(g + 16u * (64u + lane < 4u * m ? 64u + lane : 0u), sb + par * (FB * 64u) + 1024u);
     };
     auto dma_chunk = [&](uint64_t c, uint32_t lo, uint32_t lim) { /* the chunk's votes lo..lim into the slot */
         __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): the slot's LDS reads are done */
@@ -321,7 +326,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
             sp[13] = fl;
         }
         __builtin_amdgcn_wave_barrier();
-        if (lane < 4u * mm) reinterpret_cast<uint4*>(a.states + s0)[lane] = *reinterpret_cast<const uint4*>(sbp + o16);
+        for (uint32_t j = lane; j < 4u * mm; j += 64u)
+            reinterpret_cast<uint4*>(a.states + s0)[j] = *reinterpret_cast<const uint4*>(sbp + 16u * j);
     };
 
     Hdr H, N;
@@ -353,8 +359,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
         } else {
             /* the instance records' constants (written at the first chunk's top, once the
              * batch before has been finalized from its records) */
-            const uint32_t q2k = shfl(H.q2, HI + lane);
-            const uint32_t setk = shfl(H.olo, HI + lane);
+            const uint32_t q2k = H.q2;
+            const uint32_t setk = H.hs;
             /* the stream: instance starts relative to its first vote */
             const uint64_t S0 = u64of(rdl(H.olo, 0u), rdl(H.ohi, 0u));
             const uint32_t s0lo = (uint32_t)S0;
@@ -424,8 +430,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                 const bool actA = o8 >= lo_r && o8 < hi_r, actB = o8 + 4u >= lo_r && o8 + 4u < hi_r;
                 uint32_t kA = k0, kB = k0, sA = 0, klast = k0, slast = 0;
                 bool split = false;
+                uint64_t SA = 0, SBm = 0; /* units A / B (lane bits) that start an instance */
                 if (multi) {
-                    uint64_t SA = 0, SBm = 0;
                     uint32_t segw = k0, D = 0;
                     while (bk) {
                         const uint32_t k = (uint32_t)__builtin_ctzll(bk);
@@ -560,44 +566,70 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                 }
                 flush(); /* the previous chunk's codes */
 
-                /* ---- K2 + K3: one pass per round present ---- */
+                /* ---- K2 + K3 ---- */
                 uint32_t* const A = crow + cpar * cw;
                 uint32_t* const B = crow + (cpar ^ 1u) * cw;
-                if (lastc) { /* row B: the executors the last segment carries into the next chunk */
-                    const bool keep = !multi && cont0;
+                /* per-vote bucket shifts as bytes, no per-vote masks: type * 32 (the
+                 * precommit half of the accumulator) | nil * 16 */
+                const uint32_t ts0c = (t8[0] & 0x01010101u) << 5, ts1c = (t8[1] & 0x01010101u) << 5;
+                const uint32_t sh0c = ts0c | nb0, sh1c = ts1c | nb1;
+                /* Several rounds (!R1): when every unit holds one round and, inside the chunk,
+                 * an instance's rounds only increase, the segments are the (instance, round)
+                 * RUNS, each one executor (RoundVotes of that round, round_votes.rs:74-97) with
+                 * its carry-in from the previous chunk's row (no run of the chunk revisits a
+                 * round), and one pass tallies every round (`runs`).  Otherwise one pass per
+                 * round present, the other rounds' votes masked.  (Generated streams hold an
+                 * instance's rounds in order: C3's chunks take one pass.) */
+                bool runs = false;
+                uint32_t uA = 0, uB = 0, sAr = sA;
+                bool splitr = split, multir = multi;
+                uint64_t SAr = 0, SBr = 0;
+                if (!R1 && all_ok && lo_r == 0u && hi_r == CH) {
+                    uA = r8[0] & 0xFFu;
+                    uB = r8[1] & 0xFFu;
+                    const uint32_t pA = shfl(uB, lane - 1u); /* the unit before unit A (lane 0: none) */
+                    const bool iA = ((SA >> lane) & 1ull) != 0ull, iB = ((SBm >> lane) & 1ull) != 0ull;
+                    const bool rsA = lane != 0u && !iA && uA != pA, rsB = !iB && uB != uA;
+                    const bool badr = r8[0] != uA * 0x01010101u || r8[1] != uB * 0x01010101u ||
+                                      (rsA && uA < pA) || (rsB && uB < uA);
+                    if (!ballot(badr)) {
+                        runs = true;
+                        SAr = SA | ballot(rsA);
+                        SBr = SBm | ballot(rsB);
+                        multir = (SAr | SBr) != 0ull;
+                        splitr = ((SBr >> lane) & 1ull) != 0ull;
+                        /* unit A's run starts at the last run start at or before it: a unit A of a
+                         * lane <= mine or a unit B of a lane < mine (that lane's last-segment
+                         * prefix is its unit B alone) */
+                        const uint64_t mA = SAr & ((2ull << lane) - 1ull), mB = SBr & ((1ull << lane) - 1ull);
+                        const uint32_t la = mA ? 63u - (uint32_t)__builtin_clzll(mA) : 0u;
+                        const uint32_t lb = mB ? 63u - (uint32_t)__builtin_clzll(mB) : 0u;
+                        sAr = la > lb ? la : lb;
+                    }
+                }
+                if (lastc) { /* row B: the executors the last instance carries into the next chunk */
+                    const bool keep = cont0 && klast == k0 && (runs || !multi);
                     for (uint32_t k = lane; k < cw; k += 64u) B[k] = keep ? A[k] : 0u;
                     __builtin_amdgcn_wave_barrier();
                 }
                 const bool cA = cont0 && kA == k0;   /* unit A continues the previous chunk's instance */
                 const bool cL = cont0 && klast == k0; /* so does the last segment */
-                /* per-vote bucket shifts as bytes, no per-vote masks: type * 32 (the
-                 * precommit half of the accumulator) | nil * 16 */
-                const uint32_t ts0c = (t8[0] & 0x01010101u) << 5, ts1c = (t8[1] & 0x01010101u) << 5;
-                const uint32_t sh0c = ts0c | nb0, sh1c = ts1c | nb1;
-                uint32_t rset = 1u;
-                if (R > 1u) { /* the rounds present among the votes that checked in */
-                    uint32_t rb = 0;
-#pragma unroll
-                    for (uint32_t s = 0; s < LV; ++s) {
-                        const uint32_t ok = ((s < 4u ? okb0 : okb1) >> (8u * (s & 3u))) & 1u;
-                        rb |= ok << ((r8[s >> 2] >> (8u * (s & 3u))) & 15u);
-                    }
-                    rset = wave_or(rb);
-                }
                 uint32_t lv0 = 0, lv1 = 0; /* levels 0..3, byte s & 3 of unit s >> 2 */
                 /* (State machine) quorums crossed before each unit: bit 0 / 2 the prevote nil or
                  * value one at State.round (P1 is then behind the unit A / B), bit 1 / 3 a precommit
                  * value one (C behind it) -- the sums only grow, so a unit's first candidate is
                  * the instance's first exactly when its bit is clear */
                 uint32_t cf = 0;
-                while (rset) {
-                    const uint32_t r = (uint32_t)__builtin_ctz(rset);
-                    rset &= rset - 1u;
+                /* one tally pass: the round r's votes (ONE: every round, each unit in its run) */
+                auto pass = [&](auto one_t, uint32_t r) {
+                    constexpr bool ONE = decltype(one_t)::value;
+                    const uint32_t sAx = ONE ? sAr : sA;
+                    const bool splitx = ONE ? splitr : split, multix = ONE ? multir : multi;
                     uint32_t sh0 = sh0c, sh1 = sh1c, ts0 = ts0c, ts1 = ts1c;
                     if (!R1) asm volatile("" : "+v"(sh0), "+v"(sh1), "+v"(ts0), "+v"(ts1)); /* extracts stay per pass */
                     /* 0xFF in the bytes of this round's votes */
-                    const uint32_t rm0 = R > 1u ? mark_bytes(zero_marks(r8[0] ^ (r * 0x01010101u))) : 0xFFFFFFFFu;
-                    const uint32_t rm1 = R > 1u ? mark_bytes(zero_marks(r8[1] ^ (r * 0x01010101u))) : 0xFFFFFFFFu;
+                    const uint32_t rm0 = (R > 1u && !ONE) ? mark_bytes(zero_marks(r8[0] ^ (r * 0x01010101u))) : 0xFFFFFFFFu;
+                    const uint32_t rm1 = (R > 1u && !ONE) ? mark_bytes(zero_marks(r8[1] ^ (r * 0x01010101u))) : 0xFFFFFFFFu;
                     /* lane-serial prefix of the round's four buckets, 16-bit fields:
                      * prevote value | prevote nil << 16 | precommit value << 32 | precommit nil << 48;
                      * Dw: the vote's own type's half after it */
@@ -607,38 +639,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                     for (uint32_t s = 0; s < LV; ++s) {
                         const uint32_t bs = 8u * (s & 3u);
                         uint32_t ws = w[s];
-                        if (R > 1u) ws &= (uint32_t)__builtin_amdgcn_sbfe((int32_t)(s < 4u ? rm0 : rm1), bs, 8u);
+                        if (R > 1u && !ONE) ws &= (uint32_t)__builtin_amdgcn_sbfe((int32_t)(s < 4u ? rm0 : rm1), bs, 8u);
                         P += (uint64_t)ws << __builtin_amdgcn_ubfe(s < 4u ? sh0 : sh1, bs, 8u);
                         if (s == 3u) P3 = P;
                         Dw[s] = (uint32_t)(P >> __builtin_amdgcn_ubfe(s < 4u ? ts0 : ts1, bs, 8u));
                     }
-                    /* the lane's last segment (unit B alone when it starts an instance) */
-                    const uint64_t T = split ? P - P3 : P;
+                    /* the lane's last segment (unit B alone when it starts a segment) */
+                    const uint64_t T = splitx ? P - P3 : P;
                     const uint32_t Tvp = (uint32_t)T & 0xFFFFu, Tnp = (uint32_t)T >> 16;
                     const uint32_t Tvc = (uint32_t)(T >> 32) & 0xFFFFu, Tnc = (uint32_t)(T >> 48);
                     const uint32_t Ivp = scan(Tvp), Inp = scan(Tnp), Ivc = scan(Tvc), Inc = scan(Tnc);
                     const uint32_t Evp = Ivp - Tvp, Enp = Inp - Tnp, Evc = Ivc - Tvc, Enc = Inc - Tnc;
                     /* carried executors of the instance continuing from the previous chunk
-                     * (keys 2r prevote, 2r + 1 precommit; uniform LDS reads) */
+                     * (keys 2r prevote, 2r + 1 precommit): uniform LDS reads per pass, or (ONE)
+                     * each unit's own round's */
                     const uint32_t K = 2u * r;
                     uint32_t cvp = 0, cnp = 0, cvc = 0, cnc = 0;
-                    if (cont0) {
+                    if (ONE) {
+                        if (cA) {
+                            const uint2 cv = *reinterpret_cast<const uint2*>(A + 2u * uA);
+                            const uint2 cn = *reinterpret_cast<const uint2*>(A + 2u * R + 2u * uA);
+                            cvp = cv.x; cvc = cv.y; cnp = cn.x; cnc = cn.y;
+                        }
+                    } else if (cont0) {
                         cvp = A[K];
                         cvc = A[K + 1u];
                         cnp = A[2u * R + K];
                         cnc = A[2u * R + K + 1u];
                     }
-                    /* unit A's running sums before the lane: scan - (scan at its instance's
+                    /* unit A's running sums before the lane: scan - (scan at its segment's
                      * first lane) + carry */
                     uint32_t bvp = Evp, bnp = Enp, bvc = Evc, bnc = Enc;
-                    if (multi) { /* every lane runs the shuffles */
-                        const uint32_t xvp = shfl(Evp, sA), xnp = shfl(Enp, sA), xvc = shfl(Evc, sA), xnc = shfl(Enc, sA);
+                    if (multix) { /* every lane runs the shuffles */
+                        const uint32_t xvp = shfl(Evp, sAx), xnp = shfl(Enp, sAx), xvc = shfl(Evc, sAx), xnc = shfl(Enc, sAx);
                         bvp -= xvp;
                         bnp -= xnp;
                         bvc -= xvc;
                         bnc -= xnc;
                     }
-                    if (cA) {
+                    if (ONE || cA) {
                         bvp += cvp;
                         bnp += cnp;
                         bvc += cvc;
@@ -650,16 +689,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                     const uint32_t qA = recA.x;
                     uint64_t TVa = u64of(qA - bvp, qA - bvc), TNa = u64of(qA - bnp, qA - bnc);
                     uint64_t TAa = u64of(qA - bvp - bnp, qA - bvc - bnc);
-                    /* unit B: unit A's thresholds, or (split) its own instance from 0: the lane
-                     * prefix there includes unit A's part, P3 */
+                    /* unit B: unit A's thresholds, or (split) its own segment from its carry-in
+                     * (a new instance: none): the lane prefix there includes unit A's part, P3 */
                     uint64_t TVb = TVa, TNb = TNa, TAb = TAa;
-                    if (multi && split) {
+                    const uint32_t p3vp = (uint32_t)P3 & 0xFFFFu, p3np = (uint32_t)P3 >> 16;
+                    const uint32_t p3vc = (uint32_t)(P3 >> 32) & 0xFFFFu, p3nc = (uint32_t)(P3 >> 48);
+                    uint32_t dvp = 0, dnp = 0, dvc = 0, dnc = 0; /* (ONE) unit B's carry-in */
+                    if (multix && splitx) {
+                        if (ONE && cont0 && kB == k0) {
+                            const uint2 cv = *reinterpret_cast<const uint2*>(A + 2u * uB);
+                            const uint2 cn = *reinterpret_cast<const uint2*>(A + 2u * R + 2u * uB);
+                            dvp = cv.x; dvc = cv.y; dnp = cn.x; dnc = cn.y;
+                        }
                         const uint32_t qB = recB.x;
-                        const uint32_t p3vp = (uint32_t)P3 & 0xFFFFu, p3np = (uint32_t)P3 >> 16;
-                        const uint32_t p3vc = (uint32_t)(P3 >> 32) & 0xFFFFu, p3nc = (uint32_t)(P3 >> 48);
-                        TVb = u64of(qB + p3vp, qB + p3vc);
-                        TNb = u64of(qB + p3np, qB + p3nc);
-                        TAb = u64of(qB + p3vp + p3np, qB + p3vc + p3nc);
+                        TVb = u64of(qB + p3vp - dvp, qB + p3vc - dvc);
+                        TNb = u64of(qB + p3np - dnp, qB + p3nc - dnc);
+                        TAb = u64of(qB + p3vp + p3np - dvp - dnp, qB + p3vc + p3nc - dvc - dnc);
                     }
                     /* per vote: is_quorum on its own type's sums, precedence as a level */
                     uint32_t l0 = 0, l1 = 0;
@@ -679,35 +724,71 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                     }
                     if (SM) {
                         /* unit A: its running sums before the lane exceed q2 <=> the threshold on the
-                         * lane prefix is negative; unit B (same instance): the prefix through vote 3
-                         * exceeds it; a split lane's unit B starts its instance (nothing before) */
-                        const bool eA_ = R1 || r == recA.w, eB_ = R1 || r == recB.w;
-                        const uint32_t p3vp = (uint32_t)P3 & 0xFFFFu, p3np = (uint32_t)P3 >> 16;
-                        const uint32_t p3vc = (uint32_t)(P3 >> 32) & 0xFFFFu;
+                         * lane prefix is negative; unit B (same segment): the prefix through vote 3
+                         * exceeds it; a split lane's unit B starts its segment (a round run's carry-in
+                         * past q2 was crossed in an earlier chunk: in the record).  (ONE: C crossed
+                         * in another run of the instance is found by K4's ballots.) */
+                        const bool eA_ = R1 || (ONE ? uA : r) == recA.w, eB_ = R1 || (ONE ? uB : r) == recB.w;
                         const int32_t tvp = (int32_t)(uint32_t)TVa, tnp = (int32_t)(uint32_t)TNa;
                         const int32_t tvc = (int32_t)(uint32_t)(TVa >> 32);
                         cf |= (eA_ && (tvp < 0 || tnp < 0)) ? 1u : 0u;
                         cf |= tvc < 0 ? 2u : 0u;
-                        if (!split) {
+                        if (!splitx) {
                             cf |= (eB_ && ((int32_t)p3vp > tvp || (int32_t)p3np > tnp)) ? 4u : 0u;
                             cf |= (int32_t)p3vc > tvc ? 8u : 0u;
                         }
                     }
                     lv0 |= l0 & rm0;
                     lv1 |= l1 & rm1;
-                    if (lastc) { /* the last segment's executors after the chunk (lane 0 writes) */
-                        const uint32_t nvp = rdl(Ivp, 63u) - rdl(Evp, slast) + (cL ? cvp : 0u);
-                        const uint32_t nnp = rdl(Inp, 63u) - rdl(Enp, slast) + (cL ? cnp : 0u);
-                        const uint32_t nvc = rdl(Ivc, 63u) - rdl(Evc, slast) + (cL ? cvc : 0u);
-                        const uint32_t nnc = rdl(Inc, 63u) - rdl(Enc, slast) + (cL ? cnc : 0u);
-                        if (lane == 0u) {
-                            B[K] = nvp;
-                            B[K + 1u] = nvc;
-                            B[2u * R + K] = nnp;
-                            B[2u * R + K + 1u] = nnc;
+                    if (lastc) {
+                        if (ONE) { /* every run of the last instance: its executors at the run's end
+                                    * (the lane holding its last unit writes) */
+                            const bool endA = splitx, endB = lane == 63u || ((SAr >> (lane + 1u)) & 1ull) != 0ull;
+                            if (endA && kA == klast) {
+                                *reinterpret_cast<uint2*>(B + 2u * uA) = make_uint2(bvp + p3vp, bvc + p3vc);
+                                *reinterpret_cast<uint2*>(B + 2u * R + 2u * uA) = make_uint2(bnp + p3np, bnc + p3nc);
+                            }
+                            if (endB && kB == klast) {
+                                const uint32_t evp = splitx ? dvp + Tvp : bvp + ((uint32_t)P & 0xFFFFu);
+                                const uint32_t enp = splitx ? dnp + Tnp : bnp + ((uint32_t)P >> 16);
+                                const uint32_t evc = splitx ? dvc + Tvc : bvc + ((uint32_t)(P >> 32) & 0xFFFFu);
+                                const uint32_t enc = splitx ? dnc + Tnc : bnc + (uint32_t)(P >> 48);
+                                *reinterpret_cast<uint2*>(B + 2u * uB) = make_uint2(evp, evc);
+                                *reinterpret_cast<uint2*>(B + 2u * R + 2u * uB) = make_uint2(enp, enc);
+                            }
+                        } else { /* the last segment's executors after the chunk (lane 0 writes) */
+                            const uint32_t nvp = rdl(Ivp, 63u) - rdl(Evp, slast) + (cL ? cvp : 0u);
+                            const uint32_t nnp = rdl(Inp, 63u) - rdl(Enp, slast) + (cL ? cnp : 0u);
+                            const uint32_t nvc = rdl(Ivc, 63u) - rdl(Evc, slast) + (cL ? cvc : 0u);
+                            const uint32_t nnc = rdl(Inc, 63u) - rdl(Enc, slast) + (cL ? cnc : 0u);
+                            if (lane == 0u) {
+                                B[K] = nvp;
+                                B[K + 1u] = nvc;
+                                B[2u * R + K] = nnp;
+                                B[2u * R + K + 1u] = nnc;
+                            }
                         }
                     }
                     __builtin_amdgcn_wave_barrier();
+                };
+                if (R1) {
+                    pass(std::false_type{}, 0u);
+                } else if (runs) {
+                    pass(std::true_type{}, 0u);
+                } else {
+                    /* the rounds present among the votes that checked in, one pass each */
+                    uint32_t rb = 0;
+#pragma unroll
+                    for (uint32_t s = 0; s < LV; ++s) {
+                        const uint32_t ok = ((s < 4u ? okb0 : okb1) >> (8u * (s & 3u))) & 1u;
+                        rb |= ok << ((r8[s >> 2] >> (8u * (s & 3u))) & 15u);
+                    }
+                    uint32_t rset = wave_or(rb);
+                    while (rset) {
+                        const uint32_t r = (uint32_t)__builtin_ctz(rset);
+                        rset &= rset - 1u;
+                        pass(std::false_type{}, r);
+                    }
                 }
                 if (lastc) cpar ^= 1u;
                 /* to_event by (type, level); INVALID for a vote that checked out */
@@ -795,10 +876,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                         };
                         uint32_t* const sA = reinterpret_cast<uint32_t*>(sbh + 64u * kA);
                         uint32_t* const sB = reinterpret_cast<uint32_t*>(sbh + 64u * kB);
+                        uint32_t cfx = cf;
+                        if (!R1 && runs) {
+                            /* C is the first PrecommitValue of ANY round (:211): crossed before a unit
+                             * when an earlier unit of its instance in this chunk holds a commit
+                             * candidate (another run's sums are not in the unit's own pass) */
+                            const uint64_t XA = ballot((x0 & (X_C * 0x01010101u)) != 0u);
+                            const uint64_t XB = ballot((x1 & (X_C * 0x01010101u)) != 0u);
+                            /* the instance's first unit in the chunk: its last start at or before unit A */
+                            const uint64_t iAm = SA & ((2ull << lane) - 1ull), iBm = SBm & ((1ull << lane) - 1ull);
+                            const uint32_t fa = iAm ? 2u * (63u - (uint32_t)__builtin_clzll(iAm)) : 0u;
+                            const uint32_t fb = iBm ? 2u * (63u - (uint32_t)__builtin_clzll(iBm)) + 1u : 0u;
+                            const uint32_t ui = fa > fb ? fa : fb;
+                            const uint64_t below = (1ull << lane) - 1ull;
+                            const uint64_t fromA = ~((1ull << ((ui + 1u) >> 1)) - 1ull), fromB = ~((1ull << (ui >> 1)) - 1ull);
+                            const bool xcA = ((XA & fromA & below) | (XB & fromB & below)) != 0ull;
+                            const bool xcB = ((SBm >> lane) & 1ull) == 0ull && (xcA || ((XA >> lane) & 1ull) != 0ull);
+                            cfx |= (xcA ? 2u : 0u) | (xcB ? 8u : 0u);
+                        }
                         uint32_t v0, v1;
-                        c0 |= unit(0u, x0, (cf & 1u) || qA.x != NONE, (cf & 2u) || qA.y != NONE, pos0, rA, sA, r8[0],
+                        c0 |= unit(0u, x0, (cfx & 1u) || qA.x != NONE, (cfx & 2u) || qA.y != NONE, pos0, rA, sA, r8[0],
                                    eA.z, nn0, v0);
-                        c1 |= unit(1u, x1, (cf & 4u) || qB.x != NONE, (cf & 8u) || qB.y != NONE, pos1, rB, sB, r8[1],
+                        c1 |= unit(1u, x1, (cfx & 4u) || qB.x != NONE, (cfx & 8u) || qB.y != NONE, pos1, rB, sB, r8[1],
                                    eB.z, nn1, v1);
                         if (ballot((v0 | v1) != 0u)) { /* valid (:198, :202): the last candidate */
                             if (v0) {
@@ -825,8 +924,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
         if (SM && m && H.stream) {
             if (smf) { /* no vote: the States as they came */
                 dma_wait();
-                if (lane < 4u * m)
-                    reinterpret_cast<uint4*>(a.states + H.s0)[lane] = *reinterpret_cast<const uint4*>(sbh + o16);
+                for (uint32_t j = lane; j < 4u * m; j += 64u)
+                    reinterpret_cast<uint4*>(a.states + H.s0)[j] = *reinterpret_cast<const uint4*>(sbh + 16u * j);
             } else {
                 finalize(m, H.s0, sbh);
             }

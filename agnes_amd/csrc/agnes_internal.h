@@ -152,12 +152,13 @@ hipError_t agnes_launch_dedup_reject(const uint8_t* type_masked, uint64_t n, uin
 #define AGNES_WAVES_PER_BLOCK 4
 /* list_count[0] counts the deferred (i64 LIST) list; list_count[1 .. AGNES_QUEUE_N] are
  * the u32 kernels' work-queue counters; list_count[AGNES_WALK_COUNT] counts the sweep's
- * walk list and list_count[AGNES_WALK_QUEUE] is the walk kernel's queue counter; all
- * zeroed before each launch */
+ * walk list and list_count[AGNES_WALK_QUEUE] is the walk kernel's queue counter; they
+ * follow the u64 invalid-vote count in one device block, zeroed by one memset per call */
 #define AGNES_QUEUE_N 256
 #define AGNES_WALK_COUNT (AGNES_QUEUE_N + 1)
 #define AGNES_WALK_QUEUE (AGNES_QUEUE_N + 2)
 #define AGNES_QUEUE_WORDS (AGNES_QUEUE_N + 4)
+#define AGNES_COUNTER_BYTES (8 + AGNES_QUEUE_WORDS * 4)
 #define AGNES_MAX_LDS_PER_WAVE (36 * 1024)
 
 #endif

@@ -1286,12 +1286,8 @@ static hipError_t launch_mode(const agnes_tally_args* a, uint32_t lpw, int num_c
         AgnesKt kt("tally_wide", st);
         return launch_k<true, MODE, SKIP, SM, false>(a, lpw, num_cus, st);
     }
-    hipError_t e;
+    hipError_t e = hipSuccess; /* (the work-queue counters were zeroed with the invalid count) */
     {
-        AgnesKt kt("queue_reset", st);
-        e = hipMemsetAsync(a->list_count, 0, AGNES_QUEUE_WORDS * sizeof(uint32_t), st);
-    }
-    if (e == hipSuccess) {
         /* REFERENCE without RoundSkip: the fused sweep (tally + State machine in one
          * pass over the votes, agnes_sweep.hip).  DEDUP / RoundSkip: the per-instance
          * kernel, with the State machine either fused or in the one-instance-per-lane

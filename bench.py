@@ -165,7 +165,28 @@ def cpu_baseline(eng, cfg, batch, power, states0, set_of_instance):
             "host": cpu,
             "sample": f"first {limit} instances ({nv} votes) of the same batch, "
                       f"oracle/agnes_oracle.c orc_tally_mt on {threads} threads, best of 5",
-            "codes_prefix": codes, "states_prefix": st}
+            "codes_prefix": codes, "states_prefix": st, "_sample": (hb, states0[:limit])}
+
+
+def records_check(cfg, hb, power, states0, codes, ev_offs, ev_recs, ed_offs, ed_recs):
+    """The GPU's event and edge records of the CPU-baseline sample (the first instances
+    of the batch) against the checker's, every record.  Test infrastructure only: runs
+    after the timed region."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as ol
+    t0 = time.perf_counter()
+    n = hb.n_instances
+    threads = cpu_threads(host_cpu())
+    _, _, _, o_offs, o_ev = ol.events(cfg, hb, power, None, states0, threads=threads)
+    g_offs = ev_offs[: n + 1].cpu().numpy().view(np.uint64)
+    g_ev = ev_recs[: int(g_offs[-1])].cpu().numpy().reshape(-1).view(abi.VOTE_EVENT_DTYPE)
+    ev_ok = bool(np.array_equal(g_offs, o_offs) and g_ev.tobytes() == o_ev.tobytes())
+    o_doffs, o_ed = ol.edges(cfg, hb, codes)
+    g_doffs = ed_offs[: n + 1].cpu().numpy().view(np.uint64)
+    g_ed = ed_recs[: int(g_doffs[-1])].cpu().numpy().reshape(-1).view(abi.EDGE_DTYPE)
+    ed_ok = bool(np.array_equal(g_doffs, o_doffs) and g_ed.tobytes() == o_ed.tobytes())
+    return {"instances": n, "votes": hb.n_votes, "events": len(o_ev), "events_equal": ev_ok,
+            "edges": len(o_ed), "edges_equal": ed_ok, "seconds": time.perf_counter() - t0}
 
 
 def edge_summary(eng, cfg, batch, codes, reps: int = 5):
@@ -184,7 +205,7 @@ def edge_summary(eng, cfg, batch, codes, reps: int = 5):
     eng.kernel_timing(False)
     nv, ni, ne = batch.n_votes, batch.n_instances, recs.shape[0]
     ab = {"edge_count": 3 * nv + 24 * ni, "edge_scan": 16 * ni, "edge_emit": 3 * nv + 16 * ni + 16 * ne}
-    res = {"edges": int(ne), "edges_per_vote": ne / max(nv, 1), "_records": recs}
+    res = {"edges": int(ne), "edges_per_vote": ne / max(nv, 1), "_records": recs, "_offsets": offs}
     for name, (launches, total) in kt.items():
         avg = total / max(launches, 1)
         res[name] = {"avg_ms": avg, "algorithmic_bytes": ab.get(name),
@@ -208,13 +229,11 @@ def event_stream(eng, cfg, batch, codes, reps: int = 3):
     eng.kernel_timing(False)
     nv, ni, ne = batch.n_votes, batch.n_instances, recs.shape[0]
     ab = {"event_count": nv + 16 * ni, "event_scan": 16 * ni, "event_emit": 7 * nv + 8 * ni + 24 * ne}
-    res = {"events": int(ne), "events_per_vote": ne / max(nv, 1)}
+    res = {"events": int(ne), "events_per_vote": ne / max(nv, 1), "_records": recs, "_offsets": offs}
     for name, (launches, total) in kt.items():
         avg = total / max(launches, 1)
         res[name] = {"avg_ms": avg, "algorithmic_bytes": ab.get(name),
                      "GBps": ab[name] / (avg * 1e-3) / 1e9 if name in ab and avg > 0 else None}
-    del offs, recs
-    torch.cuda.empty_cache()
     return res
 
 
@@ -317,10 +336,13 @@ def main():
 
     events = event_stream(eng, cfg, batch, codes)
     edges = edge_summary(eng, cfg, batch, codes)
+    ev_offs, ev_recs = events.pop("_offsets"), events.pop("_records")
+    ed_offs = edges.pop("_offsets")
     if world > 1:  # every rank's edge records to every rank (RCCL), outside the timed region
         edges["all_gather"] = adist.gather_edges_timed(edges.pop("_records"))
+        ed_recs = None
     else:
-        edges.pop("_records")
+        ed_recs = edges.pop("_records")
 
     if rank == 0:
         ms_per_step = elapsed * 1e3 / args.steps
@@ -381,11 +403,17 @@ def main():
             cb = cpu_baseline(eng, cfg, batch, power, st0_host, set_of)
             cprefix = cb.pop("codes_prefix")
             sprefix = cb.pop("states_prefix")
+            hb, st_s = cb.pop("_sample")
             # the GPU's codes and States of the last step against the checker's
             g_codes = codes[: len(cprefix)].cpu().numpy()
             g_states = states_to_host(states)[: len(sprefix)]
-            out["cpu_check_equal"] = bool(np.array_equal(g_codes, cprefix)
-                                          and np.array_equal(g_states.view(np.uint8), sprefix.view(np.uint8)))
+            ok_codes = bool(np.array_equal(g_codes, cprefix)
+                            and np.array_equal(g_states.view(np.uint8), sprefix.view(np.uint8)))
+            # ... and the emitted records of the same sample: the stream-compacted events
+            # and the edge summaries (checker: orc_tally_labels + orc_events, orc_edges)
+            out["cpu_check"] = records_check(cfg, hb, power, st_s, cprefix, ev_offs, ev_recs, ed_offs, ed_recs)
+            out["cpu_check"]["codes_states_equal"] = ok_codes
+            out["cpu_check_equal"] = ok_codes and out["cpu_check"]["events_equal"] and out["cpu_check"]["edges_equal"]
             out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)
     if world > 1:

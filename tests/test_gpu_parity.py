@@ -548,3 +548,47 @@ def test_routes_valid_from_input(eng, route):
     g, o = run_both(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE | ROUTES[route], 2), hb, power,
                     None, st)
     assert_same(g, o)
+
+
+# ------------------------------------------------ several rounds in one pass (flow)
+
+def _reorder(hb, key):
+    """The batch with each instance's votes stably reordered by key (per vote)."""
+    order = np.lexsort((np.arange(hb.n_votes), key, hb.instance))
+    return ol.batch_from_lists(hb.instance[order], hb.round[order], hb.type[order], hb.value[order],
+                               hb.validator[order], hb.offsets.copy(), hb.instance_set)
+
+
+def _round_states(n, R, seed):
+    """Prevote / Precommit / NewRound States at rounds 0 .. R-1, so that the eqr-guarded
+    arms (state_machine.rs:196-209) fire in every round's run."""
+    st = _start_states(n, seed=seed)
+    st["round"] = np.random.default_rng(seed).integers(0, R, n)
+    return st
+
+
+@pytest.mark.parametrize("order", ["increasing", "decreasing", "revisit", "unaligned"])
+def test_round_runs(eng, order):
+    """The flow kernel tallies a chunk whose instances hold several rounds in one pass
+    when every 4-vote unit holds one round and each instance's rounds increase inside
+    the chunk (the (instance, round) runs are the segments); otherwise one pass per
+    round.  4 validators x 2 types = 8 votes per round (unit-aligned round runs, many
+    runs and commits per 512-vote chunk); 'unaligned' has 3 validators (6 votes per
+    round: units straddle rounds)."""
+    n_vals = 3 if order == "unaligned" else 4
+    p = abi.gen_params(seed=77, n_instances=6000, n_vals=n_vals, rounds_min=1, rounds_max=8,
+                       nil_permille=200)
+    hb = ol.gen_batch(p)
+    if order == "decreasing":
+        hb = _reorder(hb, -hb.round.astype(np.int64))
+    elif order == "revisit":
+        hb = _reorder(hb, (hb.round.astype(np.int64) % 2) * 16 + hb.round)
+    power = ol.gen_power(77, 3, n_vals, abi.POWER_UNIFORM, 1, 20)
+    cfg = abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 8)
+    st = _round_states(p.n_instances, 8, 5)
+    g, o = run_both(eng, cfg, hb, power, None, st)
+    assert_same(g, o)
+    assert g[1]["decided"].sum() > 100
+    cfg0 = abi.config(abi.MODE_REFERENCE, 0, 8)
+    g, o = run_both(eng, cfg0, hb, power)
+    assert_same(g, o)
