@@ -8,7 +8,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 NIL = 0xFFFFFFFF
 
 OK, E_INVALID, E_UNSUPPORTED, E_DEVICE, E_NOMEM, E_NODEVICE = 0, -1, -2, -3, -4, -5
@@ -136,6 +136,8 @@ FOLD_RESET, FOLD_APPLY, FOLD_CARRY_ZERO_NONE, FOLD_ZERO_LABELS, FOLD_TOTAL_ZERO_
 VOTE_EVENT_DTYPE = np.dtype([("vote", "<u8"), ("instance", "<u4"), ("value", "<u4"), ("round", "u1"),
                              ("kind", "u1"), ("message", "u1"), ("pad", "u1", (5,))])  # agnes_vote_event
 assert VOTE_EVENT_DTYPE.itemsize == 24
+# agnes_multi_exchange modes (include/agnes.h)
+MULTI_EXCHANGE_AUTO, MULTI_EXCHANGE_HOST, MULTI_EXCHANGE_RCCL = 0, 1, 2
 VOTE_COUNT_DTYPE = np.dtype([("value_w", "<i8"), ("nil_w", "<i8"), ("value", "<u4"),
                              ("reserved", "<u4")])  # agnes_vote_count
 MULTI_STATS_DTYPE = np.dtype([("device", "<u4"), ("i0", "<u4"), ("i1", "<u4"), ("pad", "<u4"),

@@ -21,7 +21,7 @@ OUT = os.path.join(PKG_DIR, "libagnes_amd.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("AGNES_ARCH", "gfx950")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", f"--offload-arch={ARCH}"]
-LDFLAGS = ["-shared", "-fPIC", f"--offload-arch={ARCH}"]
+LDFLAGS = ["-shared", "-fPIC", f"--offload-arch={ARCH}", "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
 
 
 def _mtime(p: str) -> float:

@@ -11,12 +11,29 @@
  * offsets rebased to 0, and its instance column rebased to the range
  * (instance - i0: the engine's batch contract numbers a batch's instances from 0),
  * by one small kernel after the copy.
+ *
+ * C5 (agnes_multi_tally_one): ONE instance's stream cut into consecutive slices, one
+ * per device in device order -- the path's one real exchange step (SURVEY.md
+ * §8(e)).  A vote's event needs the exact running sums before it (round_votes.rs:
+ * 48-67, driven per vote by vote_executor.rs:20-23), so every device tallies its
+ * slice twice around an exchange of the slice totals (the agnes_amd/dist.py
+ * tally_one_instance protocol, natively): pass A partials -> ALL-GATHER of the
+ * slice totals -> the fold of the slices before each device -> pass B.  DEDUP adds an
+ * ALL-REDUCE(MIN) of the first-vote table before the tally, the State machine an
+ * ALL-REDUCE(MIN) of the P1 / C positions and an ALL-REDUCE(MAX) of the valid
+ * candidate / decision round.  The exchanges run over RCCL (ncclCommInitAll over
+ * the devices, one communicator rank per device: xGMI between MI355X GPUs) when
+ * the devices are distinct, else through pinned host memory (several contexts on
+ * one GPU, the single-GPU tests).
  */
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <chrono>
+#include <condition_variable>
 #include <cstdint>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <thread>
 #include <vector>
@@ -46,6 +63,28 @@ struct Dev {
     agnes_ctx* ctx = nullptr;
     hipStream_t st = nullptr;
     Bufs b;
+    uint64_t* eoff = nullptr; /* the range's edge offsets (agnes_multi_edge_offsets) */
+    uint64_t etotal = 0;
+    uint64_t v0 = 0; /* the range's first vote in the last agnes_multi_tally's batch */
+};
+
+/* a reusable barrier of the driver's host threads (one per device) */
+struct Barrier {
+    std::mutex mu;
+    std::condition_variable cv;
+    uint32_t n = 0, arrived = 0;
+    uint64_t gen = 0;
+    void wait() {
+        std::unique_lock<std::mutex> lk(mu);
+        const uint64_t g = gen;
+        if (++arrived == n) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return gen != g; });
+        }
+    }
 };
 
 } // namespace multi
@@ -54,6 +93,15 @@ struct Dev {
 struct agnes_multi {
     std::vector<agnes::multi::Dev> dev;
     uint32_t n_sets = 0; /* of the uploaded power table */
+    uint32_t n_vals = 0;
+    uint32_t xmode = AGNES_MULTI_EXCHANGE_AUTO;
+    std::vector<ncclComm_t> comms; /* one rank per device (RCCL exchanges), created on first use */
+    agnes::multi::Barrier bar;
+    std::vector<unsigned char*> stage; /* pinned host staging of the host exchange, per device */
+    std::vector<uint64_t> stage_cap;
+    /* the last agnes_multi_tally's ranges (for agnes_multi_edge_offsets / _edges) */
+    std::vector<uint32_t> cut;
+    bool have_ranges = false;
 };
 
 namespace {
@@ -110,6 +158,7 @@ int run_range(Dev& d, uint32_t n_sets, const agnes_config* cfg, const agnes_vote
     MTRY(hipSetDevice(d.device));
     const uint32_t m = i1 - i0;
     const uint64_t v0 = hb->offsets[i0], v1 = hb->offsets[i1], nv = v1 - v0;
+    d.v0 = v0;
     const bool sm = (cfg->flags & AGNES_FLAG_STATE_MACHINE) && states;
     int rc = grow(d.b, nv, m);
     if (rc != AGNES_OK) return rc;
@@ -179,6 +228,294 @@ int run_range(Dev& d, uint32_t n_sets, const agnes_config* cfg, const agnes_vote
     return AGNES_OK;
 }
 
+/* ---- the exchanges of a split instance (C5) ---------------------------------------
+ * One call per device thread, every thread the same call in the same order.  RCCL:
+ * one collective on the device's communicator rank (stream-ordered, xGMI between
+ * distinct MI355X).  Host: each thread stages its buffer in pinned memory, a barrier,
+ * the reduction (each thread combines a contiguous part of the elements), a barrier,
+ * each thread copies the result back. */
+enum XOp { X_MIN_U64, X_MIN_I64, X_MAX_I64, X_GATHER };
+
+int stage_grow(agnes_multi* m, uint32_t d, uint64_t bytes) {
+    if (m->stage_cap[d] >= bytes) return AGNES_OK;
+    if (m->stage[d]) (void)hipHostFree(m->stage[d]);
+    m->stage[d] = nullptr;
+    m->stage_cap[d] = 0;
+    MTRY(hipHostMalloc(reinterpret_cast<void**>(&m->stage[d]), bytes, hipHostMallocDefault));
+    m->stage_cap[d] = bytes;
+    return AGNES_OK;
+}
+
+/* in place on the device (count int64 / u64 elements); X_GATHER: count elements per
+ * device from send into recv (D * count, device order).  Every thread reaches every
+ * barrier, also after an error (it then reports the error). */
+int exchange(agnes_multi* m, uint32_t d, XOp op, const int64_t* send, int64_t* recv, uint64_t count) {
+    Dev& dv = m->dev[d];
+    const uint32_t D = (uint32_t)m->dev.size();
+    if (!m->comms.empty()) {
+        ncclResult_t r;
+        if (op == X_GATHER)
+            r = ncclAllGather(send, recv, count, ncclInt64, m->comms[d], dv.st);
+        else
+            r = ncclAllReduce(send, recv, count, op == X_MIN_U64 ? ncclUint64 : ncclInt64,
+                              op == X_MAX_I64 ? ncclMax : ncclMin, m->comms[d], dv.st);
+        return r == ncclSuccess ? AGNES_OK : AGNES_E_DEVICE;
+    }
+    const uint64_t bytes = 8u * count;
+    int rc = stage_grow(m, d, bytes);
+    if (rc == AGNES_OK && hipMemcpyAsync(m->stage[d], send, bytes, hipMemcpyDeviceToHost, dv.st) != hipSuccess)
+        rc = AGNES_E_DEVICE;
+    if (rc == AGNES_OK && hipStreamSynchronize(dv.st) != hipSuccess) rc = AGNES_E_DEVICE;
+    m->bar.wait(); /* every stage written */
+    for (uint32_t k = 0; k < D; ++k) /* a device whose staging failed leaves a hole: all fail */
+        if (m->stage_cap[k] < bytes) rc = rc == AGNES_OK ? AGNES_E_DEVICE : rc;
+    if (op == X_GATHER) {
+        for (uint32_t k = 0; k < D && rc == AGNES_OK; ++k)
+            if (hipMemcpyAsync(recv + k * count, m->stage[k], bytes, hipMemcpyHostToDevice, dv.st) != hipSuccess)
+                rc = AGNES_E_DEVICE;
+        if (rc == AGNES_OK && hipStreamSynchronize(dv.st) != hipSuccess) rc = AGNES_E_DEVICE;
+        m->bar.wait(); /* the stages are free again */
+        return rc;
+    }
+    if (rc == AGNES_OK) { /* this thread combines elements [e0, e1) of every stage into stage 0 */
+        const uint64_t e0 = count * d / D, e1 = count * (d + 1) / D;
+        for (uint64_t e = e0; e < e1; ++e) {
+            uint64_t acc = reinterpret_cast<const uint64_t*>(m->stage[0])[e];
+            for (uint32_t k = 1; k < D; ++k) {
+                const uint64_t x = reinterpret_cast<const uint64_t*>(m->stage[k])[e];
+                if (op == X_MIN_U64) acc = x < acc ? x : acc;
+                else if (op == X_MIN_I64) acc = (int64_t)x < (int64_t)acc ? x : acc;
+                else acc = (int64_t)x > (int64_t)acc ? x : acc;
+            }
+            reinterpret_cast<uint64_t*>(m->stage[0])[e] = acc;
+        }
+    }
+    m->bar.wait(); /* stage 0 complete */
+    if (rc == AGNES_OK && hipMemcpyAsync(recv, m->stage[0], bytes, hipMemcpyHostToDevice, dv.st) != hipSuccess)
+        rc = AGNES_E_DEVICE;
+    if (rc == AGNES_OK && hipStreamSynchronize(dv.st) != hipSuccess) rc = AGNES_E_DEVICE;
+    m->bar.wait(); /* the stages are free again */
+    return rc;
+}
+
+/* device buffers of a split-instance call */
+struct OneBufs {
+    uint32_t *inst = nullptr, *value = nullptr, *val = nullptr;
+    uint8_t *round = nullptr, *type = nullptr, *tmask = nullptr, *codes = nullptr;
+    uint64_t *segoff = nullptr, *first = nullptr, *off1 = nullptr;
+    agnes_vote_count *counts = nullptr, *mine = nullptr, *ranks = nullptr, *fin = nullptr;
+    agnes_state* state = nullptr;
+    int64_t* marks = nullptr;
+    void release() {
+        void* ps[] = {inst, value, val, round, type, tmask, codes, segoff, first, off1,
+                      counts, mine, ranks, fin, state, marks};
+        for (void* p : ps)
+            if (p) (void)hipFree(p);
+        *this = OneBufs{};
+    }
+};
+
+/* device d's slice [lo, hi) of the one instance.  Every thread runs the same sequence
+ * of exchanges: a device that failed still takes part in them (so that no thread
+ * waits forever) and reports its first error. */
+int run_one(agnes_multi* m, uint32_t d, const agnes_config* cfg, const agnes_vote_batch* hb, uint64_t lo,
+            uint64_t hi, uint32_t spd, uint8_t* codes, agnes_state* state, agnes_vote_count* counts_out,
+            agnes_multi_stats* out) {
+    Dev& dv = m->dev[d];
+    const uint32_t D = (uint32_t)m->dev.size();
+    const uint32_t R = cfg->max_rounds, K = 2u * R;
+    const bool dedup = cfg->mode == AGNES_MODE_DEDUP;
+    const bool sm = (cfg->flags & AGNES_FLAG_STATE_MACHINE) && state;
+    const uint64_t nv = hi - lo;
+    OneBufs b;
+    int rc = AGNES_OK;
+#define OTRY(expr)                                          \
+    do {                                                    \
+        if (rc == AGNES_OK) {                               \
+            const hipError_t e_ = (expr);                   \
+            if (e_ != hipSuccess) rc = status(e_);          \
+        }                                                   \
+    } while (0)
+#define OCALL(expr)                                         \
+    do {                                                    \
+        if (rc == AGNES_OK) {                               \
+            const int r_ = (expr);                          \
+            if (r_ != AGNES_OK) rc = r_;                    \
+        }                                                   \
+    } while (0)
+#define OXCH(expr)                                          \
+    do {                                                    \
+        const int r_ = (expr); /* (always: every thread) */ \
+        if (rc == AGNES_OK && r_ != AGNES_OK) rc = r_;      \
+    } while (0)
+    OTRY(hipSetDevice(dv.device));
+    const uint64_t v = nv ? nv : 4u;
+    uint32_t S = spd ? spd : 2048u;
+    if ((uint64_t)S > (nv + 3u) / 4u) S = (uint32_t)((nv + 3u) / 4u);
+    if (S == 0u) S = 1u;
+    OTRY(hipMalloc(&b.inst, 4 * v));
+    OTRY(hipMalloc(&b.value, 4 * v));
+    OTRY(hipMalloc(&b.val, 4 * v));
+    OTRY(hipMalloc(&b.round, v));
+    OTRY(hipMalloc(&b.type, v));
+    OTRY(hipMalloc(&b.codes, v));
+    OTRY(hipMalloc(&b.segoff, 8 * ((uint64_t)S + 1u)));
+    OTRY(hipMalloc(&b.off1, 16));
+    OTRY(hipMalloc(&b.counts, sizeof(agnes_vote_count) * (uint64_t)S * K));
+    OTRY(hipMalloc(&b.mine, sizeof(agnes_vote_count) * K));
+    OTRY(hipMalloc(&b.ranks, sizeof(agnes_vote_count) * K * D));
+    OTRY(hipMalloc(&b.fin, sizeof(agnes_vote_count) * K));
+    if (dedup) {
+        OTRY(hipMalloc(&b.tmask, v));
+        OTRY(hipMalloc(&b.first, 8ull * K * m->n_vals));
+    }
+    if (sm) {
+        OTRY(hipMalloc(&b.state, sizeof(agnes_state)));
+        OTRY(hipMalloc(&b.marks, 4 * sizeof(int64_t)));
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    if (nv) {
+        OTRY(hipMemcpyAsync(b.inst, hb->instance + lo, 4 * nv, hipMemcpyHostToDevice, dv.st));
+        OTRY(hipMemcpyAsync(b.round, hb->round + lo, nv, hipMemcpyHostToDevice, dv.st));
+        OTRY(hipMemcpyAsync(b.type, hb->type + lo, nv, hipMemcpyHostToDevice, dv.st));
+        OTRY(hipMemcpyAsync(b.value, hb->value + lo, 4 * nv, hipMemcpyHostToDevice, dv.st));
+        OTRY(hipMemcpyAsync(b.val, hb->validator + lo, 4 * nv, hipMemcpyHostToDevice, dv.st));
+    }
+    /* the slice's segments: balanced, multiples of 4 votes (one wave each) */
+    std::vector<uint64_t> so((size_t)S + 1u);
+    for (uint32_t k = 0; k <= S; ++k) so[k] = ((uint64_t)k * nv / S) / 4u * 4u;
+    so[S] = nv;
+    const uint64_t off1[2] = {0, nv};
+    OTRY(hipMemcpyAsync(b.segoff, so.data(), 8 * ((uint64_t)S + 1u), hipMemcpyHostToDevice, dv.st));
+    OTRY(hipMemcpyAsync(b.off1, off1, 16, hipMemcpyHostToDevice, dv.st));
+    if (sm) OTRY(hipMemcpyAsync(b.state, state, sizeof(agnes_state), hipMemcpyHostToDevice, dv.st));
+    OTRY(hipStreamSynchronize(dv.st));
+    const double h2d = ms_since(t0);
+    const auto t1 = std::chrono::steady_clock::now();
+
+    agnes_vote_batch sl{}; /* the slice as one batch (the DEDUP and State-machine passes) */
+    sl.instance = b.inst;
+    sl.round = b.round;
+    sl.type = b.type;
+    sl.value = b.value;
+    sl.validator = b.val;
+    sl.offsets = b.off1;
+    sl.n_votes = nv;
+    sl.n_instances = 1;
+    const agnes_config one{AGNES_MODE_REFERENCE, cfg->flags | AGNES_FLAG_ONE_INSTANCE, R, 0u};
+    agnes_config scfg = *cfg; /* the DEDUP / State-machine passes: instance id 0 */
+    scfg.reserved = 0u;
+    agnes_vote_batch seg = sl; /* the slice cut into segments (the carried tally) */
+    seg.offsets = b.segoff;
+    seg.n_instances = S;
+    if (dedup) { /* the first vote of every (round, type, validator) over all slices */
+        OTRY(hipMemsetAsync(b.first, 0xFF, 8ull * K * m->n_vals, dv.st));
+        OCALL(agnes_dedup_first(dv.ctx, &scfg, &sl, lo, b.first, dv.st));
+        OTRY(hipStreamSynchronize(dv.st));
+        OXCH(exchange(m, d, X_MIN_U64, reinterpret_cast<const int64_t*>(b.first), reinterpret_cast<int64_t*>(b.first),
+                      (uint64_t)K * m->n_vals));
+        OCALL(agnes_dedup_mask(dv.ctx, &scfg, &sl, lo, b.first, b.tmask, dv.st));
+        seg.type = b.tmask;
+    }
+    /* pass A: every segment from RoundVotes::new -> its partial; this slice's total */
+    OCALL(agnes_fold_counts(dv.ctx, b.counts, S, K, nullptr, nullptr, AGNES_FOLD_RESET, dv.st));
+    OCALL(agnes_tally_carried(dv.ctx, &one, &seg, b.codes, b.counts, dv.st));
+    OCALL(agnes_fold_counts(dv.ctx, b.counts, S, K, nullptr, b.mine, 0u, dv.st));
+    OTRY(hipStreamSynchronize(dv.st));
+    /* the exchange: every slice's total to every device */
+    OXCH(exchange(m, d, X_GATHER, reinterpret_cast<const int64_t*>(b.mine), reinterpret_cast<int64_t*>(b.ranks),
+                  3ull * K));
+    /* the slices before each device, then before each segment: pass B's carry-ins */
+    OCALL(agnes_fold_counts(dv.ctx, b.ranks, D, K, nullptr, b.fin,
+                            AGNES_FOLD_APPLY | AGNES_FOLD_CARRY_ZERO_NONE | AGNES_FOLD_TOTAL_ZERO_LABELS, dv.st));
+    OCALL(agnes_fold_counts(dv.ctx, b.counts, S, K, b.ranks + (uint64_t)d * K, nullptr,
+                            AGNES_FOLD_APPLY | AGNES_FOLD_ZERO_LABELS, dv.st));
+    OCALL(agnes_tally_carried(dv.ctx, &one, &seg, b.codes, b.counts, dv.st));
+    if (dedup) OCALL(agnes_dedup_reject(dv.ctx, b.tmask, nv, b.codes, dv.st));
+    if (sm) { /* P1 / C: MIN over slices; valid, decision round: MAX; the State */
+        const int64_t init[4] = {INT64_MAX, INT64_MAX, 0, 0};
+        OTRY(hipMemcpyAsync(b.marks, init, sizeof(init), hipMemcpyHostToDevice, dv.st));
+        OCALL(agnes_one_sm_scan(dv.ctx, &scfg, &sl, lo, b.codes, b.state, b.marks, dv.st));
+        OTRY(hipStreamSynchronize(dv.st));
+        OXCH(exchange(m, d, X_MIN_I64, b.marks, b.marks, 2u));
+        OCALL(agnes_one_sm_apply(dv.ctx, &scfg, &sl, lo, b.codes, b.state, b.marks, dv.st));
+        OTRY(hipStreamSynchronize(dv.st));
+        OXCH(exchange(m, d, X_MAX_I64, b.marks + 2, b.marks + 2, 2u));
+        OCALL(agnes_one_sm_finish(dv.ctx, b.marks, b.state, dv.st));
+    }
+    OTRY(hipStreamSynchronize(dv.st));
+    uint64_t bad = 0;
+    OCALL(agnes_last_error_count(dv.ctx, &bad));
+    const double tally = ms_since(t1);
+    const auto t2 = std::chrono::steady_clock::now();
+    if (nv) OTRY(hipMemcpyAsync(codes + lo, b.codes, nv, hipMemcpyDeviceToHost, dv.st));
+    if (d == 0u) {
+        if (counts_out) OTRY(hipMemcpyAsync(counts_out, b.fin, sizeof(agnes_vote_count) * K, hipMemcpyDeviceToHost, dv.st));
+        if (sm) OTRY(hipMemcpyAsync(state, b.state, sizeof(agnes_state), hipMemcpyDeviceToHost, dv.st));
+    }
+    OTRY(hipStreamSynchronize(dv.st));
+    if (out) {
+        out->device = (uint32_t)dv.device;
+        out->i0 = 0;
+        out->i1 = 1;
+        out->n_votes = nv;
+        out->n_invalid = bad;
+        out->h2d_ms = h2d;
+        out->tally_ms = tally;
+        out->d2h_ms = ms_since(t2);
+    }
+    (void)hipStreamSynchronize(dv.st);
+    b.release();
+#undef OTRY
+#undef OCALL
+#undef OXCH
+    return rc;
+}
+
+int ensure_exchange(agnes_multi* m) {
+    const uint32_t D = (uint32_t)m->dev.size();
+    if (m->stage.size() != D) {
+        m->stage.assign(D, nullptr);
+        m->stage_cap.assign(D, 0);
+    }
+    m->bar.n = D;
+    bool distinct = true;
+    for (uint32_t i = 0; i < D; ++i)
+        for (uint32_t j = i + 1; j < D; ++j)
+            if (m->dev[i].device == m->dev[j].device) distinct = false;
+    const bool want = m->xmode == AGNES_MULTI_EXCHANGE_RCCL || (m->xmode == AGNES_MULTI_EXCHANGE_AUTO && distinct && D > 1);
+    if (!want) {
+        for (ncclComm_t c : m->comms) (void)ncclCommDestroy(c);
+        m->comms.clear();
+        return AGNES_OK;
+    }
+    if (!distinct) return AGNES_E_UNSUPPORTED; /* RCCL: one communicator rank per device */
+    if (m->comms.size() == D) return AGNES_OK;
+    std::vector<int> devs(D);
+    for (uint32_t k = 0; k < D; ++k) devs[k] = m->dev[k].device;
+    m->comms.assign(D, nullptr);
+    if (ncclCommInitAll(m->comms.data(), (int)D, devs.data()) != ncclSuccess) {
+        m->comms.clear();
+        return AGNES_E_DEVICE;
+    }
+    return AGNES_OK;
+}
+
+/* the device batch of range k of the last agnes_multi_tally */
+agnes_vote_batch range_batch(const agnes_multi* m, uint32_t k, uint64_t nv) {
+    const Dev& d = m->dev[k];
+    agnes_vote_batch db{};
+    db.instance = d.b.inst;
+    db.round = d.b.round;
+    db.type = d.b.type;
+    db.value = d.b.value;
+    db.validator = d.b.val;
+    db.offsets = d.b.off;
+    db.n_instances = m->cut[k + 1] - m->cut[k];
+    db.n_votes = nv;
+    return db;
+}
+
 } // namespace
 
 extern "C" {
@@ -210,10 +547,14 @@ void agnes_multi_destroy(agnes_multi* m) {
         if (hipSetDevice(d.device) == hipSuccess) {
             if (d.st) (void)hipStreamSynchronize(d.st);
             free_bufs(d.b);
+            if (d.eoff) (void)hipFree(d.eoff);
             if (d.st) (void)hipStreamDestroy(d.st);
         }
         if (d.ctx) agnes_ctx_destroy(d.ctx);
     }
+    for (ncclComm_t c : m->comms) (void)ncclCommDestroy(c);
+    for (unsigned char* p : m->stage)
+        if (p) (void)hipHostFree(p);
     delete m;
 }
 
@@ -225,6 +566,7 @@ int agnes_multi_upload_power(agnes_multi* m, const int64_t* power, uint32_t n_se
         if (rc != AGNES_OK) return rc;
     }
     m->n_sets = n_sets;
+    m->n_vals = n_vals;
     return AGNES_OK;
 }
 
@@ -251,10 +593,139 @@ int agnes_multi_tally(agnes_multi* m, const agnes_config* cfg, const agnes_vote_
     std::vector<int> rc(D, AGNES_OK);
     std::vector<std::thread> th;
     th.reserve(D);
+    m->have_ranges = false;
     for (uint32_t k = 0; k < D; ++k)
         th.emplace_back([&, k]() {
             rc[k] = run_range(m->dev[k], m->n_sets, cfg, hb, cut[k], cut[k + 1], codes, states,
                               stats ? stats + k : nullptr);
+        });
+    for (auto& t : th) t.join();
+    for (int r : rc)
+        if (r != AGNES_OK) return r;
+    m->cut = cut;
+    m->have_ranges = true;
+    return AGNES_OK;
+}
+
+
+int agnes_multi_exchange(agnes_multi* m, uint32_t mode) {
+    if (!m || mode > AGNES_MULTI_EXCHANGE_RCCL) return AGNES_E_INVALID;
+    m->xmode = mode;
+    return ensure_exchange(m);
+}
+
+int agnes_multi_tally_one(agnes_multi* m, const agnes_config* cfg, const agnes_vote_batch* hb, uint8_t* codes,
+                          agnes_state* state, agnes_vote_count* counts, uint32_t segments_per_device,
+                          agnes_multi_stats* stats) {
+    if (!m || !cfg || !hb || !hb->offsets || hb->n_instances != 1u) return AGNES_E_INVALID;
+    if (cfg->max_rounds < 1u || (cfg->mode != AGNES_MODE_REFERENCE && cfg->mode != AGNES_MODE_DEDUP) ||
+        (cfg->flags & (AGNES_FLAG_ROUND_SKIP | AGNES_FLAG_ONE_INSTANCE | AGNES_FLAG_DISTINCT_VALUES)))
+        return AGNES_E_UNSUPPORTED;
+    if (hb->weight || hb->instance_set) return AGNES_E_UNSUPPORTED; /* the power table weighs, set 0 */
+    const uint64_t n = hb->offsets[1];
+    if (hb->offsets[0] != 0u || n > hb->n_votes) return AGNES_E_INVALID;
+    if (n && (!codes || !hb->instance || !hb->round || !hb->type || !hb->value || !hb->validator))
+        return AGNES_E_INVALID;
+    if (!m->n_vals) return AGNES_E_INVALID; /* no power table */
+    if (n > (1ull << 31)) return AGNES_E_UNSUPPORTED;
+    const int e = ensure_exchange(m);
+    if (e != AGNES_OK) return e;
+    const uint32_t D = (uint32_t)m->dev.size();
+    std::vector<int> rc(D, AGNES_OK);
+    std::vector<std::thread> th;
+    th.reserve(D);
+    for (uint32_t k = 0; k < D; ++k) {
+        /* consecutive slices in device order, boundaries on multiples of 4 votes */
+        const uint64_t lo = (n * k / D) / 4u * 4u, hi = k + 1u == D ? n : (n * (k + 1u) / D) / 4u * 4u;
+        th.emplace_back([&, k, lo, hi]() {
+            rc[k] = run_one(m, k, cfg, hb, lo, hi, segments_per_device, codes, state, counts,
+                            stats ? stats + k : nullptr);
+        });
+    }
+    for (auto& t : th) t.join();
+    for (int r : rc)
+        if (r != AGNES_OK) return r;
+    return AGNES_OK;
+}
+
+int agnes_multi_edge_offsets(agnes_multi* m, const agnes_config* cfg, uint64_t* offsets) {
+    if (!m || !cfg || !offsets) return AGNES_E_INVALID;
+    if (!m->have_ranges) return AGNES_E_INVALID; /* no agnes_multi_tally before */
+    const uint32_t D = (uint32_t)m->dev.size();
+    std::vector<int> rc(D, AGNES_OK);
+    std::vector<std::vector<uint64_t>> loc(D);
+    std::vector<std::thread> th;
+    th.reserve(D);
+    for (uint32_t k = 0; k < D; ++k)
+        th.emplace_back([&, k]() {
+            Dev& d = m->dev[k];
+            const uint32_t mi = m->cut[k + 1] - m->cut[k];
+            loc[k].assign((size_t)mi + 1u, 0u);
+            int r = hipSetDevice(d.device) == hipSuccess ? AGNES_OK : AGNES_E_DEVICE;
+            uint64_t nv = 0;
+            if (r == AGNES_OK && hipMemcpy(&nv, d.b.off + mi, 8, hipMemcpyDeviceToHost) != hipSuccess) r = AGNES_E_DEVICE;
+            if (r == AGNES_OK) {
+                if (d.eoff) (void)hipFree(d.eoff);
+                d.eoff = nullptr;
+                if (hipMalloc(&d.eoff, 8ull * (mi + 1u)) != hipSuccess) r = AGNES_E_NOMEM;
+            }
+            const agnes_vote_batch db = range_batch(m, k, nv);
+            if (r == AGNES_OK) r = agnes_edge_offsets(d.ctx, cfg, &db, d.b.codes, d.eoff, d.st);
+            if (r == AGNES_OK && hipMemcpyAsync(loc[k].data(), d.eoff, 8ull * (mi + 1u), hipMemcpyDeviceToHost, d.st) !=
+                                     hipSuccess)
+                r = AGNES_E_DEVICE;
+            if (r == AGNES_OK && hipStreamSynchronize(d.st) != hipSuccess) r = AGNES_E_DEVICE;
+            d.etotal = loc[k][mi];
+            rc[k] = r;
+        });
+    for (auto& t : th) t.join();
+    for (int r : rc)
+        if (r != AGNES_OK) return r;
+    uint64_t base = 0; /* the ranges' offsets made global, in range order */
+    for (uint32_t k = 0; k < D; ++k) {
+        const uint32_t i0 = m->cut[k], mi = m->cut[k + 1] - i0;
+        for (uint32_t j = 0; j < mi; ++j) offsets[i0 + j] = base + loc[k][j];
+        base += loc[k][mi];
+    }
+    offsets[m->cut[D]] = base;
+    return AGNES_OK;
+}
+
+int agnes_multi_edges(agnes_multi* m, const agnes_config* cfg, const uint64_t* offsets, agnes_edge* out) {
+    if (!m || !cfg || !offsets) return AGNES_E_INVALID;
+    if (!m->have_ranges) return AGNES_E_INVALID;
+    const uint32_t D = (uint32_t)m->dev.size();
+    for (uint32_t k = 0; k < D; ++k)
+        if (!m->dev[k].eoff) return AGNES_E_INVALID; /* agnes_multi_edge_offsets first */
+    if (offsets[m->cut[D]] && !out) return AGNES_E_INVALID;
+    std::vector<int> rc(D, AGNES_OK);
+    std::vector<std::thread> th;
+    th.reserve(D);
+    for (uint32_t k = 0; k < D; ++k)
+        th.emplace_back([&, k]() {
+            Dev& d = m->dev[k];
+            const uint32_t i0 = m->cut[k], mi = m->cut[k + 1] - i0;
+            const uint64_t ne = d.etotal, at = offsets[i0];
+            int r = hipSetDevice(d.device) == hipSuccess ? AGNES_OK : AGNES_E_DEVICE;
+            uint64_t nv = 0;
+            if (r == AGNES_OK && hipMemcpy(&nv, d.b.off + mi, 8, hipMemcpyDeviceToHost) != hipSuccess) r = AGNES_E_DEVICE;
+            uint64_t v0 = 0; /* the range's first vote in the host batch: offsets rebased at 0 */
+            agnes_edge* dout = nullptr;
+            if (r == AGNES_OK && ne && hipMalloc(&dout, sizeof(agnes_edge) * ne) != hipSuccess) r = AGNES_E_NOMEM;
+            const agnes_vote_batch db = range_batch(m, k, nv);
+            if (r == AGNES_OK && ne) r = agnes_edges(d.ctx, cfg, &db, d.b.codes, d.eoff, dout, d.st);
+            if (r == AGNES_OK && ne &&
+                hipMemcpyAsync(out + at, dout, sizeof(agnes_edge) * ne, hipMemcpyDeviceToHost, d.st) != hipSuccess)
+                r = AGNES_E_DEVICE;
+            if (r == AGNES_OK && hipStreamSynchronize(d.st) != hipSuccess) r = AGNES_E_DEVICE;
+            if (dout) (void)hipFree(dout);
+            v0 = d.v0;
+            if (r == AGNES_OK) /* the batch's vote and instance numbering */
+                for (uint64_t e = 0; e < ne; ++e) {
+                    out[at + e].vote += v0;
+                    out[at + e].instance += i0;
+                }
+            rc[k] = r;
         });
     for (auto& t : th) t.join();
     for (int r : rc)

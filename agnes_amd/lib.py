@@ -74,6 +74,11 @@ def load():
         "agnes_multi_destroy": ([P], None),
         "agnes_multi_upload_power": ([P, P, C.c_uint32, C.c_uint32, P], C.c_int),
         "agnes_multi_tally": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P], C.c_int),
+        "agnes_multi_tally_one": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, C.c_uint32, P],
+                                  C.c_int),
+        "agnes_multi_exchange": ([P, C.c_uint32], C.c_int),
+        "agnes_multi_edge_offsets": ([P, C.POINTER(abi.Config), P], C.c_int),
+        "agnes_multi_edges": ([P, C.POINTER(abi.Config), P, P], C.c_int),
         "agnes_valset_build": ([P, P, C.c_uint32, P, P, C.c_uint64, C.c_uint32, P, P, P, P, P,
                                 C.POINTER(C.c_uint64), P], C.c_int),
         "agnes_valset_find": ([P, P, C.c_uint32, P, C.c_uint32, P, P, C.c_uint64, P, P], C.c_int),

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AGNES_ABI_VERSION 4u
+#define AGNES_ABI_VERSION 5u
 
 /* ---------------------------------------------------------------------------
  * Status codes (reference never fails, state_machine.rs:212; these report
@@ -551,6 +551,32 @@ int agnes_multi_upload_power(agnes_multi* m, const int64_t* power, uint32_t n_se
 int agnes_multi_tally(agnes_multi* m, const agnes_config* cfg, const agnes_vote_batch* batch, uint8_t* codes,
                       agnes_state* states, agnes_multi_stats* stats);
 
+/* C5 through the native driver: ONE instance's stream (batch: HOST, n_instances ==
+ * 1, instance ids 0, the power table's set 0) cut into consecutive slices, one per
+ * device in device order, and tallied with codes identical to one stream's
+ * (VoteExecutor::apply vote by vote, vote_executor.rs:20-36, over the running
+ * VoteCount of round_votes.rs:48-67).  Each device tallies its slice twice around
+ * the path's exchange step: pass A partials -> ALL-GATHER of the
+ * slice totals -> each device's carry-in (the fold of the slices before it) -> pass
+ * B.  DEDUP mode adds an ALL-REDUCE(MIN) of the first-vote table (the first vote of
+ * each (round, type, validator) wins); AGNES_FLAG_STATE_MACHINE with `state` (HOST,
+ * one record, in/out) an ALL-REDUCE(MIN) of the P1 / C positions and an
+ * ALL-REDUCE(MAX) of the valid candidate and the decision round (agnes_one_sm_*).
+ * counts (HOST [2 * max_rounds], optional) receives the instance's executors after
+ * its last vote.  segments_per_device: waves per slice (0: 2048).  No RoundSkip,
+ * DISTINCT_VALUES, caller weights or instance sets (AGNES_E_UNSUPPORTED).
+ * Synchronous; stats (optional) one record per device (i0 = 0, i1 = 1). */
+int agnes_multi_tally_one(agnes_multi* m, const agnes_config* cfg, const agnes_vote_batch* batch, uint8_t* codes,
+                          agnes_state* state, agnes_vote_count* counts, uint32_t segments_per_device,
+                          agnes_multi_stats* stats);
+/* How agnes_multi_tally_one exchanges: AUTO = RCCL (ncclCommInitAll, one rank per
+ * device, xGMI between MI355X) when the devices are distinct and more than one, else
+ * pinned host memory; HOST; RCCL (AGNES_E_UNSUPPORTED when a device is listed twice). */
+#define AGNES_MULTI_EXCHANGE_AUTO 0u
+#define AGNES_MULTI_EXCHANGE_HOST 1u
+#define AGNES_MULTI_EXCHANGE_RCCL 2u
+int agnes_multi_exchange(agnes_multi* m, uint32_t mode);
+
 /* ---------------------------------------------------------------------------
  * Edge-triggered summary of a coded batch.
  *
@@ -587,6 +613,11 @@ int agnes_edge_offsets(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote
  * batch and codes. */
 int agnes_edges(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
                 const uint8_t* codes, const uint64_t* offsets, agnes_edge* out, void* stream);
+/* The same summary of the LAST agnes_multi_tally's batch (the native multi-GPU
+ * driver), gathered from every device into HOST arrays in the batch's own numbering:
+ * offsets [n_instances + 1] first, then out [offsets[n_instances]] records. */
+int agnes_multi_edge_offsets(agnes_multi* m, const agnes_config* cfg, uint64_t* offsets);
+int agnes_multi_edges(agnes_multi* m, const agnes_config* cfg, const uint64_t* offsets, agnes_edge* out);
 
 /* ---------------------------------------------------------------------------
  * Event stream: every Some(Event) the batch's votes produced, stream-compacted

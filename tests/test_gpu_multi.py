@@ -54,3 +54,96 @@ def test_multi_rejects():
             m.tally(abi.config(abi.MODE_REFERENCE, 0, 1), hb)
     finally:
         m.close()
+
+
+# ------------------------------------------- C5 through the native driver (tally_one)
+
+def _c5_batch(seed, n_vals, dedup, rounds=1):
+    gen = dict(n_instances=1, n_vals=n_vals, rounds_min=rounds, rounds_max=rounds, nil_permille=200)
+    if dedup:
+        gen.update(dup_permille=100, equiv_permille=100)
+    return ol.gen_batch(abi.gen_params(seed=seed, **gen))
+
+
+@pytest.mark.parametrize("n_dev", [1, 2, 3])
+@pytest.mark.parametrize("mode", [abi.MODE_REFERENCE, abi.MODE_DEDUP])
+@pytest.mark.parametrize("sm", [False, True])
+def test_multi_tally_one_equals_checker(n_dev, mode, sm):
+    """One instance's stream split over 1..3 contexts (agnes_multi_tally_one): pass A,
+    the all-gather of the slice totals, pass B (+ the DEDUP MIN and the State
+    machine's MIN / MAX exchanges) through pinned host memory; codes, the State and
+    the final executors equal one stream tallied by the checker (round_votes.rs:48-67,
+    vote_executor.rs:20-36, state_machine.rs:196-211)."""
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    n_vals = 20_000
+    hb = _c5_batch(11 + n_dev, n_vals, mode == abi.MODE_DEDUP, rounds=2)
+    power = ol.gen_power(11, 1, n_vals, abi.POWER_ZIPF, 1, 1_000_000)
+    cfg = abi.config(mode, abi.FLAG_STATE_MACHINE if sm else 0, 2)
+    st0 = abi.new_states(1, 1, abi.STEP_PREVOTE) if sm else None
+    m = MultiEngine([0] * n_dev)
+    try:
+        m.upload_power(power)
+        codes, st, counts, stats = m.tally_one(cfg, hb, st0, segments=97)
+    finally:
+        m.close()
+    want, want_st, bad = ol.tally(cfg, hb, power, None, st0)
+    if not np.array_equal(codes, want):
+        k = int(np.nonzero(codes != want)[0][0])
+        raise AssertionError(f"code {k}: gpu {codes[k]:#x} checker {want[k]:#x}")
+    if sm:
+        assert st.tobytes() == want_st.tobytes() and st["decided"][0] == 1
+    # the final executors: every counted vote's weight (REFERENCE: all; DEDUP: firsts)
+    counted = (want & 7) != abi.CODE_INVALID
+    counted &= (want & 7) != abi.CODE_REJECTED
+    w = power[0][hb.validator]
+    for r in range(2):
+        for t in range(2):
+            sel = counted & (hb.round == r) & (hb.type == t)
+            nil = hb.value == abi.NIL
+            k = 2 * r + t
+            assert counts["value_w"][k] == int(w[sel & ~nil].sum()) and counts["nil_w"][k] == int(w[sel & nil].sum())
+    assert int(stats["n_votes"].sum()) == hb.n_votes
+
+
+def test_multi_tally_one_rccl_one_rank():
+    """The RCCL exchange path (ncclCommInitAll, all_gather / all_reduce MIN / MAX)
+    with one device (a one-rank communicator: the box has one GPU)."""
+    hb = _c5_batch(5, 4096, True)
+    power = ol.gen_power(5, 1, 4096, abi.POWER_ZIPF, 1, 1_000_000)
+    cfg = abi.config(abi.MODE_DEDUP, abi.FLAG_STATE_MACHINE, 1)
+    st0 = abi.new_states(1, 1, abi.STEP_PREVOTE)
+    m = MultiEngine([0])
+    try:
+        m.exchange(abi.MULTI_EXCHANGE_RCCL)
+        m.upload_power(power)
+        codes, st, _, _ = m.tally_one(cfg, hb, st0, segments=33)
+    finally:
+        m.close()
+    want, want_st, _ = ol.tally(cfg, hb, power, None, st0)
+    assert np.array_equal(codes, want) and st.tobytes() == want_st.tobytes()
+    m = MultiEngine([0, 0])
+    try:
+        with pytest.raises(AgnesError):
+            m.exchange(abi.MULTI_EXCHANGE_RCCL)  # one rank per device
+    finally:
+        m.close()
+
+
+@pytest.mark.parametrize("n_dev", [1, 3])
+def test_multi_edges_gathered(n_dev):
+    """The edge summary of the last agnes_multi_tally, gathered from every range in
+    the batch's own numbering, equals the checker's orc_edges over the whole batch."""
+    p = abi.gen_params(seed=4, n_instances=3001, n_vals=50, rounds_min=1, rounds_max=3, nil_permille=300)
+    hb = ol.gen_batch(p)
+    power = ol.gen_power(4, 5, 50, abi.POWER_UNIFORM, 1, 100)
+    cfg = abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 3)
+    m = MultiEngine([0] * n_dev)
+    try:
+        m.upload_power(power)
+        codes, _, _ = m.tally(cfg, hb, abi.new_states(3001, 1, abi.STEP_PREVOTE))
+        offs, recs = m.edges(cfg, p.n_instances)
+    finally:
+        m.close()
+    o_offs, o_recs = ol.edges(cfg, hb, codes)
+    assert np.array_equal(offs, o_offs)
+    assert recs.tobytes() == o_recs.tobytes() and len(recs) > 3001
