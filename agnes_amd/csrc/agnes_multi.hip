@@ -402,19 +402,23 @@ int run_one(agnes_multi* m, uint32_t d, const agnes_config* cfg, const agnes_vot
     sl.offsets = b.off1;
     sl.n_votes = nv;
     sl.n_instances = 1;
-    const agnes_config one{AGNES_MODE_REFERENCE, cfg->flags | AGNES_FLAG_ONE_INSTANCE, R, 0u};
-    agnes_config scfg = *cfg; /* the DEDUP / State-machine passes: instance id 0 */
+    /* the carried tally: REFERENCE over the (masked) slice, no State machine */
+    const agnes_config one{AGNES_MODE_REFERENCE, (cfg->flags & ~AGNES_FLAG_STATE_MACHINE) | AGNES_FLAG_ONE_INSTANCE,
+                           R, 0u};
+    agnes_config scfg = *cfg; /* the State-machine passes: instance id 0 */
     scfg.reserved = 0u;
+    agnes_config dcfg = scfg; /* the DEDUP passes */
+    dcfg.flags &= ~AGNES_FLAG_STATE_MACHINE;
     agnes_vote_batch seg = sl; /* the slice cut into segments (the carried tally) */
     seg.offsets = b.segoff;
     seg.n_instances = S;
     if (dedup) { /* the first vote of every (round, type, validator) over all slices */
         OTRY(hipMemsetAsync(b.first, 0xFF, 8ull * K * m->n_vals, dv.st));
-        OCALL(agnes_dedup_first(dv.ctx, &scfg, &sl, lo, b.first, dv.st));
+        OCALL(agnes_dedup_first(dv.ctx, &dcfg, &sl, lo, b.first, dv.st));
         OTRY(hipStreamSynchronize(dv.st));
         OXCH(exchange(m, d, X_MIN_U64, reinterpret_cast<const int64_t*>(b.first), reinterpret_cast<int64_t*>(b.first),
                       (uint64_t)K * m->n_vals));
-        OCALL(agnes_dedup_mask(dv.ctx, &scfg, &sl, lo, b.first, b.tmask, dv.st));
+        OCALL(agnes_dedup_mask(dv.ctx, &dcfg, &sl, lo, b.first, b.tmask, dv.st));
         seg.type = b.tmask;
     }
     /* pass A: every segment from RoundVotes::new -> its partial; this slice's total */
