@@ -42,16 +42,37 @@ constexpr uint32_t EV_LO = AGNES_CODE_NONE | (AGNES_CODE_POLKA_ANY << 8) | (AGNE
 constexpr uint32_t EV_HI = AGNES_CODE_NONE | (AGNES_CODE_PRECOMMIT_ANY << 8) | (AGNES_CODE_NONE << 16) |
                            (AGNES_CODE_PRECOMMIT_VALUE << 24);
 
+/* DMA slot: each column of the next chunk as a contiguous image */
+constexpr uint32_t F_INST = 0, F_VALUE = 2048, F_VAL = 4096, F_ROUND = 6144, F_TYPE = 6656, F_BYTES = 7168;
+
 /* per-wave LDS: carried executors ca[2R] (all votes), cn[2R] (nil), cs[R] (distinct
- * RoundSkip weight) | DEDUP table [2R][nv] | RoundSkip table [R][nv] */
+ * RoundSkip weight) | DEDUP table [2R][nv] | RoundSkip table [R][nv] | DMA slot */
 __host__ __device__ inline void layout(uint32_t mode, bool skip, uint32_t R, uint32_t nv, uint32_t* o_fv,
-                                       uint32_t* o_fs, uint32_t* total) {
+                                       uint32_t* o_fs, uint32_t* o_slot, uint32_t* total) {
     uint32_t o = (uint32_t)align16(20ull * R);
     *o_fv = o;
     if (mode == AGNES_MODE_DEDUP) o = (uint32_t)align16(o + 8ull * R * nv);
     *o_fs = o;
     if (skip) o = (uint32_t)align16(o + 4ull * R * nv);
-    *total = o;
+    *o_slot = o;
+    *total = o + F_BYTES;
+}
+
+/* LDS-DMA, saddr form (uniform 64-bit base + 32-bit lane offset), non-temporal: the
+ * vote columns are read once */
+__device__ __forceinline__ void sdma16(const void* base, uint32_t voff, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(base), "s"(lds)
+                 : "memory");
+}
+__device__ __forceinline__ void sdma4(const void* base, uint32_t voff, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2 nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(base), "s"(lds)
+                 : "memory");
 }
 
 __device__ __forceinline__ uint32_t wave_or(uint32_t x) { /* every lane active */
@@ -79,14 +100,33 @@ __global__ __launch_bounds__(256) void sieve(agnes_tally_args a, uint32_t lds_pe
         for (uint32_t k = threadIdx.x; k < np; k += blockDim.x) pc[k] = a.power32[k];
         __syncthreads();
     }
-    uint32_t o_fv, o_fs, o_tot;
-    layout(MODE, SKIP, R, nv, &o_fv, &o_fs, &o_tot);
+    uint32_t o_fv, o_fs, o_slot, o_tot;
+    layout(MODE, SKIP, R, nv, &o_fv, &o_fs, &o_slot, &o_tot);
     unsigned char* const base = agnes_smem + a.power_cache + wave * lds_per_wave;
     uint32_t* const ca = reinterpret_cast<uint32_t*>(base); /* [2R] all-vote weight carried */
     uint32_t* const cn = ca + 2u * R;                        /* [2R] nil weight              */
     uint32_t* const cs = cn + 2u * R;                        /* [R]  distinct RoundSkip weight */
     uint32_t* const first_v = reinterpret_cast<uint32_t*>(base + o_fv);
     uint32_t* const first_s = reinterpret_cast<uint32_t*>(base + o_fs);
+    unsigned char* const slot = base + o_slot;
+    const uint32_t slotl = lds_addr(slot);
+    const uint32_t o16 = 16u * lane, o4 = 4u * lane;
+    uint64_t pf_at = ~0ull; /* the chunk held (or in flight) in the slot */
+    /* the full chunk at c into the slot (c + CH <= NV, c a multiple of 4) */
+    auto dma_chunk = [&](uint64_t c) {
+        __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): the slot's LDS reads are done */
+        sdma16(a.vb.instance + c, o16, slotl + F_INST);
+        sdma16(a.vb.instance + c + 256u, o16, slotl + F_INST + 1024u);
+        sdma16(a.vb.value + c, o16, slotl + F_VALUE);
+        sdma16(a.vb.value + c + 256u, o16, slotl + F_VALUE + 1024u);
+        sdma16(a.vb.validator + c, o16, slotl + F_VAL);
+        sdma16(a.vb.validator + c + 256u, o16, slotl + F_VAL + 1024u);
+        sdma4(a.vb.round + c, o4, slotl + F_ROUND);
+        sdma4(a.vb.round + c + 256u, o4, slotl + F_ROUND + 256u);
+        sdma4(a.vb.type + c, o4, slotl + F_TYPE);
+        sdma4(a.vb.type + c + 256u, o4, slotl + F_TYPE + 256u);
+        pf_at = c;
+    };
     if (MODE == AGNES_MODE_DEDUP) fill_u32(first_v, 2ull * R * nv, 0u, lane);
     if (SKIP) fill_u32(first_s, (uint64_t)R * nv, 0u, lane);
     const uint32_t lb = a.epoch_shift, lmask = (1u << lb) - 1u;
@@ -166,7 +206,26 @@ __global__ __launch_bounds__(256) void sieve(agnes_tally_args a, uint32_t lds_pe
                 const uint64_t j0 = c + p0;
                 /* ---- K1 ---- */
                 uint32_t inst[LV], value[LV], val[LV], r8[2], t8[2];
-                if (j0 + LV <= NV) {
+                if (pf_at == c) { /* prefetched by LDS-DMA */
+                    dma_wait();
+                    const uint32_t o32 = 32u * lane, o8 = 8u * lane;
+                    const uint4 i0 = *reinterpret_cast<const uint4*>(slot + F_INST + o32);
+                    const uint4 i1 = *reinterpret_cast<const uint4*>(slot + F_INST + o32 + 16u);
+                    const uint4 v0 = *reinterpret_cast<const uint4*>(slot + F_VALUE + o32);
+                    const uint4 v1 = *reinterpret_cast<const uint4*>(slot + F_VALUE + o32 + 16u);
+                    const uint4 d0 = *reinterpret_cast<const uint4*>(slot + F_VAL + o32);
+                    const uint4 d1 = *reinterpret_cast<const uint4*>(slot + F_VAL + o32 + 16u);
+                    const uint2 rr = *reinterpret_cast<const uint2*>(slot + F_ROUND + o8);
+                    const uint2 tt = *reinterpret_cast<const uint2*>(slot + F_TYPE + o8);
+                    inst[0] = i0.x; inst[1] = i0.y; inst[2] = i0.z; inst[3] = i0.w;
+                    inst[4] = i1.x; inst[5] = i1.y; inst[6] = i1.z; inst[7] = i1.w;
+                    value[0] = v0.x; value[1] = v0.y; value[2] = v0.z; value[3] = v0.w;
+                    value[4] = v1.x; value[5] = v1.y; value[6] = v1.z; value[7] = v1.w;
+                    val[0] = d0.x; val[1] = d0.y; val[2] = d0.z; val[3] = d0.w;
+                    val[4] = d1.x; val[5] = d1.y; val[6] = d1.z; val[7] = d1.w;
+                    r8[0] = rr.x; r8[1] = rr.y;
+                    t8[0] = tt.x; t8[1] = tt.y;
+                } else if (j0 + LV <= NV) {
                     const uint4 i0 = *reinterpret_cast<const uint4*>(a.vb.instance + j0);
                     const uint4 i1 = *reinterpret_cast<const uint4*>(a.vb.instance + j0 + 4u);
                     const uint4 v0 = *reinterpret_cast<const uint4*>(a.vb.value + j0);
@@ -212,6 +271,25 @@ __global__ __launch_bounds__(256) void sieve(agnes_tally_args a, uint32_t lds_pe
                     w[s] = ok ? w[s] : 0u;
                 }
                 bad += (uint32_t)__builtin_popcount(inm & ~okm);
+                uint32_t nilm = 0; /* bit s: a nil vote */
+#pragma unroll
+                for (uint32_t s = 0; s < LV; ++s) nilm |= (uint32_t)(value[s] == AGNES_NIL) << s;
+                /* a gather from HBM retires before the DMA below is issued (vmcnt retires in
+                 * issue order); then the next chunk: this instance's, or the next one's first */
+                if (!PC) asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]),
+                                      "v"(w[6]), "v"(w[7]));
+                {
+                    uint64_t nc = c + CH;
+                    if (nc >= end) {
+                        nc = ~0ull;
+                        if (succ() < n) {
+                            const uint64_t nb = u64of(rdl(hn, 0u), rdl(hn, 1u)), ne = u64of(rdl(hn, 2u), rdl(hn, 3u));
+                            if (ne > nb && nb < NV) nc = nb & ~3ull;
+                        }
+                    }
+                    if (nc != ~0ull && nc + CH <= NV) dma_chunk(nc);
+                    else pf_at = ~0ull;
+                }
 
                 /* first-vote tables: the earliest vote of the instance wins (DEDUP: per (round,
                  * type, validator); RoundSkip: per (round, validator)) */
@@ -228,6 +306,11 @@ __global__ __launch_bounds__(256) void sieve(agnes_tally_args a, uint32_t lds_pe
                         }
                     }
                     __builtin_amdgcn_wave_barrier();
+                    /* opaque copies: the read-back recomputes its addresses instead of keeping
+                     * the atomics' 16 addresses live (register pressure) */
+#pragma unroll
+                    for (uint32_t s = 0; s < LV; ++s) asm volatile("" : "+v"(val[s]));
+                    asm volatile("" : "+v"(r8[0]), "+v"(r8[1]), "+v"(t8[0]), "+v"(t8[1]));
                     if (MODE == AGNES_MODE_DEDUP) acc = 0u;
 #pragma unroll
                     for (uint32_t s = 0; s < LV; ++s) {
@@ -253,23 +336,21 @@ __global__ __launch_bounds__(256) void sieve(agnes_tally_args a, uint32_t lds_pe
                 while (rset) {
                     const uint32_t r = (uint32_t)__builtin_ctz(rset);
                     rset &= rset - 1u;
-                    uint64_t PA = 0, PN = 0; /* lane prefixes: prevote in the low, precommit in the high half */
-                    uint32_t PS = 0;         /* distinct-validator weight (RoundSkip) */
-                    uint32_t Da[LV], Dn[LV], Ds[LV], sh[LV];
-                    uint32_t am = 0;         /* bit s: an accepted vote of round r */
+                    uint32_t am = 0; /* bit s: an accepted vote of round r */
+#pragma unroll
+                    for (uint32_t s = 0; s < LV; ++s)
+                        am |= (uint32_t)(((acc >> s) & 1u) && byte_of(r8[s >> 2], s & 3u) == r) << s;
+                    /* the lane's totals: all-vote and nil weights per type (prevote in the low,
+                     * precommit in the high half), distinct-validator weight */
+                    uint64_t PA = 0, PN = 0;
+                    uint32_t PS = 0;
 #pragma unroll
                     for (uint32_t s = 0; s < LV; ++s) {
-                        const uint32_t rs_ = byte_of(r8[s >> 2], s & 3u);
-                        const bool m = ((acc >> s) & 1u) && rs_ == r;
-                        am |= (uint32_t)m << s;
-                        const uint32_t wm = m ? w[s] : 0u;
-                        sh[s] = (byte_of(t8[s >> 2], s & 3u) & 1u) << 5; /* 32 * type */
-                        PA += (uint64_t)wm << sh[s];
-                        PN += (uint64_t)(value[s] == AGNES_NIL ? wm : 0u) << sh[s];
+                        const uint32_t wm = ((am >> s) & 1u) ? w[s] : 0u;
+                        const uint32_t sh = (byte_of(t8[s >> 2], s & 3u) & 1u) << 5; /* 32 * type */
+                        PA += (uint64_t)wm << sh;
+                        PN += (uint64_t)(((nilm >> s) & 1u) ? wm : 0u) << sh;
                         if (SKIP) PS += ((sfirst >> s) & 1u) ? wm : 0u;
-                        Da[s] = (uint32_t)(PA >> sh[s]);
-                        Dn[s] = (uint32_t)(PN >> sh[s]);
-                        Ds[s] = PS;
                     }
                     const uint32_t Tpa = (uint32_t)PA, Tca = (uint32_t)(PA >> 32);
                     const uint32_t Tpn = (uint32_t)PN, Tcn = (uint32_t)(PN >> 32);
@@ -288,25 +369,38 @@ __global__ __launch_bounds__(256) void sieve(agnes_tally_args a, uint32_t lds_pe
                     const uint64_t TV = u64of(q2 - (bpa - bpn), q2 - (bca - bcn));
                     const uint64_t TN = u64of(q2 - bpn, q2 - bcn);
                     const uint64_t TA = u64of(q2 - bpa, q2 - bca);
+                    uint32_t csr = 0, ts = 0;
+                    if (SKIP) {
+                        csr = ld_carry ? cs[r] : 0u;
+                        ts = q1 - csr - (Is - PS);
+                    }
+                    /* per vote (the lane prefixes again, fewer live registers): is_quorum on
+                     * its own type's sums, precedence as a level; RoundSkip (3 * distinct >
+                     * total <=> distinct > q1) */
+                    uint64_t QA = 0, QN = 0;
+                    uint32_t QS = 0;
 #pragma unroll
                     for (uint32_t s = 0; s < LV; ++s) {
-                        const int32_t tv = (int32_t)(uint32_t)(TV >> sh[s]);
-                        const int32_t tn = (int32_t)(uint32_t)(TN >> sh[s]);
-                        const int32_t ta = (int32_t)(uint32_t)(TA >> sh[s]);
-                        uint32_t l = (int32_t)Da[s] > ta ? 1u : 0u;
-                        l = (int32_t)Dn[s] > tn ? 2u : l;
-                        l = (int32_t)(Da[s] - Dn[s]) > tv ? 3u : l;
+                        const uint32_t wm = ((am >> s) & 1u) ? w[s] : 0u;
+                        const uint32_t sh = (byte_of(t8[s >> 2], s & 3u) & 1u) << 5;
+                        QA += (uint64_t)wm << sh;
+                        QN += (uint64_t)(((nilm >> s) & 1u) ? wm : 0u) << sh;
+                        const uint32_t Da = (uint32_t)(QA >> sh), Dn = (uint32_t)(QN >> sh);
+                        const int32_t tv = (int32_t)(uint32_t)(TV >> sh);
+                        const int32_t tn = (int32_t)(uint32_t)(TN >> sh);
+                        const int32_t ta = (int32_t)(uint32_t)(TA >> sh);
+                        uint32_t l = (int32_t)Da > ta ? 1u : 0u;
+                        l = (int32_t)Dn > tn ? 2u : l;
+                        l = (int32_t)(Da - Dn) > tv ? 3u : l;
                         l = ((am >> s) & 1u) ? l : 0u;
                         lv[s >> 2] |= l << (8u * (s & 3u));
+                        if (SKIP) {
+                            QS += ((sfirst >> s) & 1u) ? wm : 0u;
+                            skb[s >> 2] |= (((am >> s) & 1u) && (int32_t)QS > (int32_t)ts) ? AGNES_CODE_SKIP << (8u * (s & 3u))
+                                                                                            : 0u;
+                        }
                     }
-                    if (SKIP) { /* RoundSkip: 3 * distinct > total <=> distinct > q1 */
-                        const uint32_t csr = ld_carry ? cs[r] : 0u;
-                        const int32_t ts = (int32_t)(q1 - csr - (Is - PS));
-#pragma unroll
-                        for (uint32_t s = 0; s < LV; ++s)
-                            skb[s >> 2] |= (((am >> s) & 1u) && (int32_t)Ds[s] > ts) ? AGNES_CODE_SKIP << (8u * (s & 3u)) : 0u;
-                        if (st_carry && lane == 63u) cs[r] = csr + Is;
-                    }
+                    if (SKIP && st_carry && lane == 63u) cs[r] = csr + Is;
                     if (st_carry && lane == 63u) { /* the round's executors after the chunk */
                         ca[K] = bpa + Tpa;
                         ca[K + 1u] = bca + Tca;
@@ -354,6 +448,7 @@ __global__ __launch_bounds__(256) void sieve(agnes_tally_args a, uint32_t lds_pe
         }
         hq = hn;
     }
+    dma_wait(); /* no LDS-DMA may land after the wave's LDS is handed on */
     const uint32_t nb = rdl(scan(bad), 63u);
     if (lane == 0 && nb) atomicAdd(a.n_invalid, (unsigned long long)nb);
 }
@@ -365,8 +460,8 @@ __global__ __launch_bounds__(256) void sieve(agnes_tally_args a, uint32_t lds_pe
 /* launcher                                                            */
 
 static uint32_t sieve_lds(uint32_t mode, uint32_t flags, uint32_t R, uint32_t nv) {
-    uint32_t fv, fs, tot;
-    agnes::sieve::layout(mode, (flags & AGNES_FLAG_ROUND_SKIP) != 0, R, nv, &fv, &fs, &tot);
+    uint32_t fv, fs, sl, tot;
+    agnes::sieve::layout(mode, (flags & AGNES_FLAG_ROUND_SKIP) != 0, R, nv, &fv, &fs, &sl, &tot);
     return tot;
 }
 

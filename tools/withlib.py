@@ -28,6 +28,7 @@ class _Tolerant:
 
     def __init__(self, path):
         self._L = _orig_cdll(path)
+        abi.ABI_VERSION = self._L.agnes_abi_version()  # accept the build's own ABI version
 
     def __getattr__(self, name):
         try:
@@ -42,9 +43,7 @@ class _Tolerant:
 
 
 lib.C = type("C", (), {k: getattr(C, k) for k in dir(C) if not k.startswith("__")})
-lib.C.CDLL = _Tolerant
-_L = _Tolerant(lib.LIB_PATH)
-abi.ABI_VERSION = _L.agnes_abi_version()
+lib.C.CDLL = _Tolerant  # (loaded by lib.load(): after the script imported torch and its HIP runtime)
 script = sys.argv[2]
 sys.argv = sys.argv[2:]
 sys.path.insert(0, os.path.dirname(os.path.abspath(script)))
