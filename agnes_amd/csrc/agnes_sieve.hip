@@ -256,20 +256,26 @@ __global__ __launch_bounds__(256) void sieve(agnes_tally_args a, uint32_t lds_pe
                 }
                 /* the boundary's checks: the vote names its instance, round < R, type in
                  * {0, 1}, validator in the set; in: inside [beg, end) */
-                uint32_t inm = 0, okm = 0; /* bit s */
-                uint32_t w[LV];
+                uint32_t inm = 0, okm = 0; /* bit s (bitwise tests: no per-vote branches) */
 #pragma unroll
                 for (uint32_t s = 0; s < LV; ++s) {
                     const uint32_t r = byte_of(r8[s >> 2], s & 3u), t = byte_of(t8[s >> 2], s & 3u);
-                    const bool in = p0 + s >= lo_r && p0 + s < hi_r;
-                    const bool ok = in && inst[s] == i && r < R && t <= 1u && val[s] < nvs;
-                    inm |= (uint32_t)in << s;
-                    okm |= (uint32_t)ok << s;
-                    /* K1: w = power[set][validator] (consensus_executor.rs:62-63 -> validators.rs:7) */
-                    const uint32_t idx = pbase + (ok ? val[s] : 0u);
-                    w[s] = PC ? reinterpret_cast<const uint32_t*>(agnes_smem)[idx] : a.power32[idx];
-                    w[s] = ok ? w[s] : 0u;
+                    const uint32_t in = (uint32_t)(p0 + s >= lo_r) & (uint32_t)(p0 + s < hi_r);
+                    const uint32_t ok = in & (uint32_t)(inst[s] == i) & (uint32_t)(r < R) & (uint32_t)(t <= 1u) &
+                                        (uint32_t)(val[s] < nvs);
+                    inm |= in << s;
+                    okm |= ok << s;
                 }
+                /* K1: w = power[set][validator] (consensus_executor.rs:62-63 -> validators.rs:7);
+                 * a vote that checked out reads entry 0 and weighs 0 */
+                uint32_t w[LV];
+#pragma unroll
+                for (uint32_t s = 0; s < LV; ++s) {
+                    const uint32_t idx = pbase + (((okm >> s) & 1u) ? val[s] : 0u);
+                    w[s] = PC ? reinterpret_cast<const uint32_t*>(agnes_smem)[idx] : a.power32[idx];
+                }
+#pragma unroll
+                for (uint32_t s = 0; s < LV; ++s) w[s] = ((okm >> s) & 1u) ? w[s] : 0u;
                 bad += (uint32_t)__builtin_popcount(inm & ~okm);
                 uint32_t nilm = 0; /* bit s: a nil vote */
 #pragma unroll
@@ -339,7 +345,7 @@ __global__ __launch_bounds__(256) void sieve(agnes_tally_args a, uint32_t lds_pe
                     uint32_t am = 0; /* bit s: an accepted vote of round r */
 #pragma unroll
                     for (uint32_t s = 0; s < LV; ++s)
-                        am |= (uint32_t)(((acc >> s) & 1u) && byte_of(r8[s >> 2], s & 3u) == r) << s;
+                        am |= ((acc >> s) & 1u & (uint32_t)(byte_of(r8[s >> 2], s & 3u) == r)) << s;
                     /* the lane's totals: all-vote and nil weights per type (prevote in the low,
                      * precommit in the high half), distinct-validator weight */
                     uint64_t PA = 0, PN = 0;
@@ -396,8 +402,7 @@ __global__ __launch_bounds__(256) void sieve(agnes_tally_args a, uint32_t lds_pe
                         lv[s >> 2] |= l << (8u * (s & 3u));
                         if (SKIP) {
                             QS += ((sfirst >> s) & 1u) ? wm : 0u;
-                            skb[s >> 2] |= (((am >> s) & 1u) && (int32_t)QS > (int32_t)ts) ? AGNES_CODE_SKIP << (8u * (s & 3u))
-                                                                                            : 0u;
+                            skb[s >> 2] |= ((am >> s) & 1u & (uint32_t)((int32_t)QS > (int32_t)ts)) << (8u * (s & 3u) + 3u);
                         }
                     }
                     if (SKIP && st_carry && lane == 63u) cs[r] = csr + Is;
@@ -419,10 +424,10 @@ __global__ __launch_bounds__(256) void sieve(agnes_tally_args a, uint32_t lds_pe
                     for (uint32_t s = 0; s < 4u; ++s) {
                         const uint32_t b = 4u * u + s;
                         const uint32_t sft = 8u * s;
-                        if (!((acc >> b) & 1u)) { /* not tallied */
-                            const uint32_t x = ((okm >> b) & 1u) ? AGNES_CODE_REJECTED : AGNES_CODE_INVALID;
-                            code = (code & ~(0xFFu << sft)) | (x << sft);
-                        }
+                        /* not tallied: INVALID, or REJECTED (DEDUP) */
+                        const uint32_t x = ((okm >> b) & 1u) ? AGNES_CODE_REJECTED : AGNES_CODE_INVALID;
+                        const uint32_t mk = ((acc >> b) & 1u) ? 0u : 0xFFu << sft;
+                        code = (code & ~mk) | ((x << sft) & mk);
                         inb |= ((inm >> b) & 1u) << s;
                     }
                     const uint64_t at = j0 + 4u * u;
