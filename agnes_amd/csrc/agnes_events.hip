@@ -326,6 +326,233 @@ __global__ __launch_bounds__(256) void event_emit_wave(EvArgs a) {
     }
 }
 
+/* ---- the batch-stream forms (aligned columns): a wave walks a batch of up to EB
+ * consecutive instances as ONE vote stream, so a short instance (C2: 200 votes) no
+ * longer leaves most of a pass idle, and the records leave through LDS as coalesced
+ * 8-B stores ------------------------------------------------------------------- */
+constexpr uint32_t EB = 32u; /* instances per batch (offsets in lanes 0..EB) */
+
+/* the batch's offsets in lanes 0..m (clamped to n_votes), as two halves */
+struct EvBatch {
+    uint32_t s0, m, olo, ohi;
+    uint64_t O0, Om;
+};
+__device__ __forceinline__ EvBatch ev_batch(const EvArgs& a, uint32_t b, uint32_t lane) {
+    EvBatch B;
+    const uint32_t n = a.vb.n_instances;
+    const uint64_t NV = a.vb.n_votes;
+    B.s0 = b * EB;
+    B.m = n - B.s0 < EB ? n - B.s0 : EB;
+    uint64_t o = 0;
+    if (lane <= B.m) {
+        o = a.vb.offsets[B.s0 + lane];
+        o = o < NV ? o : NV;
+    }
+    B.olo = (uint32_t)o;
+    B.ohi = (uint32_t)(o >> 32);
+    B.O0 = ((uint64_t)__builtin_amdgcn_readlane(B.ohi, 0) << 32) | (uint32_t)__builtin_amdgcn_readlane(B.olo, 0);
+    B.Om = ((uint64_t)__builtin_amdgcn_readlane(B.ohi, B.m) << 32) | (uint32_t)__builtin_amdgcn_readlane(B.olo, B.m);
+    return B;
+}
+
+/* the count pass: per instance its records (a tallied vote gives its event and its
+ * RoundSkip: code bits 0..2 in 1..5, bit 3), from the codes alone (1 B per vote) */
+__global__ __launch_bounds__(256) void event_count_stream(EvArgs a) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t n = a.vb.n_instances, NB = (n + EB - 1u) / EB;
+    const uint64_t NV = a.vb.n_votes;
+    for (uint32_t b = blockIdx.x * 4u + wave; b < NB; b += gridDim.x * 4u) {
+        const EvBatch B = ev_batch(a, b, lane);
+        const uint64_t ol = ((uint64_t)B.ohi << 32) | B.olo;
+        const uint64_t on = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * (lane + 1u)), (int)B.ohi) << 32) |
+                            (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * (lane + 1u)), (int)B.olo);
+        uint64_t cnt = 0; /* lane k < m: records of instance s0 + k */
+        /* 1024-vote chunks: lane l holds votes 16l .. 16l+15 (one 16-B load of codes) */
+        for (uint64_t c = B.O0 & ~15ull; c < B.Om; c += 1024u) {
+            const uint64_t j0 = c + 16u * lane;
+            uint32_t w4[4] = {0u, 0u, 0u, 0u};
+            if (j0 + 16u <= NV) {
+                const uint4 q = *reinterpret_cast<const uint4*>(a.codes + j0);
+                w4[0] = q.x; w4[1] = q.y; w4[2] = q.z; w4[3] = q.w;
+            } else {
+                for (uint32_t t = 0; t < 16u && j0 + t < NV; ++t) w4[t >> 2] |= (uint32_t)a.codes[j0 + t] << (8u * (t & 3u));
+            }
+            /* records per vote, one byte each: event in 1..5 (e < 6: not INVALID / REJECTED),
+             * plus its RoundSkip bit */
+            uint32_t rc[4], tot = 0u;
+#pragma unroll
+            for (uint32_t d = 0; d < 4u; ++d) {
+                const uint32_t e = w4[d] & 0x07070707u;
+                const uint32_t valid = ~((e + 0x02020202u) >> 3) & 0x01010101u;
+                const uint32_t nz = (e | (e >> 1) | (e >> 2)) & 0x01010101u;
+                rc[d] = (nz & valid) + ((w4[d] >> 3) & valid);
+                tot += (rc[d] * 0x01010101u) >> 24;
+            }
+            const uint32_t incl = wave_scan_incl(tot), excl = incl - tot;
+            const uint32_t ctot = __builtin_amdgcn_readlane(incl, 63);
+            const uint64_t cend = c + 1024u;
+            /* records of the chunk's votes before position p (c <= p <= cend) */
+            auto before = [&](uint64_t p) -> uint32_t {
+                if (p >= cend) return ctot;
+                const uint32_t lp = (uint32_t)(p - c), ln = lp >> 4, bt = lp & 15u;
+                uint32_t mine = 0u; /* (every lane) its bytes below bt */
+#pragma unroll
+                for (uint32_t d = 0; d < 4u; ++d) {
+                    const uint32_t lo = 4u * d;
+                    const uint32_t keep = bt >= lo + 4u ? 0xFFFFFFFFu : (bt <= lo ? 0u : (1u << (8u * (bt - lo))) - 1u);
+                    mine += ((rc[d] & keep) * 0x01010101u) >> 24;
+                }
+                return __builtin_amdgcn_readlane(excl, ln) + __builtin_amdgcn_readlane(mine, ln);
+            };
+            /* the instances overlapping the chunk (uniform loop) */
+            uint64_t rest = __builtin_amdgcn_ballot_w64(lane < B.m && ol < cend && on > c);
+            while (rest) {
+                const uint32_t k = (uint32_t)__builtin_ctzll(rest);
+                rest &= rest - 1ull;
+                const uint64_t ks = ((uint64_t)__builtin_amdgcn_readlane(B.ohi, k) << 32) | (uint32_t)__builtin_amdgcn_readlane(B.olo, k);
+                const uint64_t ke = ((uint64_t)__builtin_amdgcn_readlane(B.ohi, k + 1u) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane(B.olo, k + 1u);
+                const uint32_t x = before(ke < cend ? ke : cend) - before(ks > c ? ks : c);
+                if (lane == k) cnt += x;
+            }
+        }
+        if (lane < B.m) a.offs[B.s0 + lane + 1u] = cnt;
+    }
+}
+
+__global__ __launch_bounds__(256) void event_emit_stream(EvArgs a) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t n = a.vb.n_instances, NB = (n + EB - 1u) / EB;
+    const uint64_t NV = a.vb.n_votes;
+    const uint32_t keys = a.keys;
+    /* per wave: the value slots [EB][keys], then the record staging area (512 records) */
+    uint32_t* const lab = reinterpret_cast<uint32_t*>(agnes_smem) + wave * (EB * keys + 512u * 6u);
+    uint32_t* const stage = lab + EB * keys;
+    for (uint32_t b = blockIdx.x * 4u + wave; b < NB; b += gridDim.x * 4u) {
+        const EvBatch B = ev_batch(a, b, lane);
+        for (uint32_t k = lane; k < EB * keys; k += 64u) lab[k] = 0u; /* VoteCount::new: Value{} */
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t ol = ((uint64_t)B.ohi << 32) | B.olo;
+        uint64_t cnt = a.offs[B.s0]; /* the batch's first record */
+        for (uint64_t c = B.O0 & ~3ull; c < B.Om; c += 256u) {
+            const uint64_t j0 = c + 4u * lane;
+            Pass cur;
+            load_pass(a, j0, NV, cur);
+            /* per vote: batch instance (the count of the batch's later instances starting at
+             * or before it: ballots over the offsets' lanes), key, records */
+            uint32_t kk[4];
+#pragma unroll
+            for (uint32_t s = 0; s < 4u; ++s) kk[s] = 0u;
+            {
+                /* instances 1..m-1 starting inside (c, c + 256): few; every vote counts them */
+                const uint64_t st = __builtin_amdgcn_ballot_w64(lane >= 1u && lane < B.m && ol > c && ol < c + 256u);
+                const uint64_t pre = __builtin_amdgcn_ballot_w64(lane >= 1u && lane < B.m && ol <= c);
+                const uint32_t k0 = (uint32_t)__builtin_popcountll(pre);
+#pragma unroll
+                for (uint32_t s = 0; s < 4u; ++s) kk[s] = k0;
+                uint64_t rest = st;
+                while (rest) {
+                    const uint32_t k = (uint32_t)__builtin_ctzll(rest);
+                    rest &= rest - 1ull;
+                    const uint64_t ks = ((uint64_t)__builtin_amdgcn_readlane(B.ohi, k) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readlane(B.olo, k);
+#pragma unroll
+                    for (uint32_t s = 0; s < 4u; ++s) kk[s] += (j0 + s >= ks) ? 1u : 0u;
+                }
+            }
+            uint32_t key[4], n_rec = 0, recs = 0;
+#pragma unroll
+            for (uint32_t s = 0; s < 4u; ++s) {
+                const uint64_t j = j0 + s;
+                const uint32_t cb = (cur.c4 >> (8u * s)) & 0xFFu, ev = cb & AGNES_CODE_EVENT_MASK;
+                const uint32_t rb = (cur.r4 >> (8u * s)) & 0xFFu, tb = (cur.t4 >> (8u * s)) & 0xFFu;
+                const uint32_t k = rb * 2u + tb;
+                const bool in = j >= B.O0 && j < B.Om && ev != AGNES_CODE_INVALID && ev != AGNES_CODE_REJECTED &&
+                                tb <= 1u && k < keys;
+                key[s] = in ? kk[s] * keys + k : 0xFFFFFFFFu;
+                const uint32_t skip = in ? (cb >> 3) & 1u : 0u, has = (in && ev != AGNES_CODE_NONE) ? 1u : 0u;
+                recs |= (skip | (has << 1)) << (2u * s);
+                n_rec += skip + has;
+            }
+            const uint32_t incl = wave_scan_incl(n_rec);
+            const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+            /* the value slot after each vote, per (instance, round, type) present
+             * (round_votes.rs:50-54: the last non-nil value its bucket took) */
+            uint32_t slot[4] = {0u, 0u, 0u, 0u};
+            uint32_t pend = (key[0] != 0xFFFFFFFFu ? 1u : 0u) | (key[1] != 0xFFFFFFFFu ? 2u : 0u) |
+                            (key[2] != 0xFFFFFFFFu ? 4u : 0u) | (key[3] != 0xFFFFFFFFu ? 8u : 0u);
+            for (;;) {
+                const uint64_t lm = __builtin_amdgcn_ballot_w64(pend != 0u);
+                if (!lm) break;
+                const uint32_t kl = (uint32_t)__builtin_ctzll(lm);
+                const uint32_t ks = (uint32_t)__builtin_ctz(__builtin_amdgcn_readlane(pend, kl));
+                const uint32_t kv = ks == 0u ? key[0] : (ks == 1u ? key[1] : (ks == 2u ? key[2] : key[3]));
+                const uint32_t K = __builtin_amdgcn_readlane(kv, kl);
+                uint32_t inb = 0, last = 0, hasv = 0;
+#pragma unroll
+                for (uint32_t s = 0; s < 4u; ++s) {
+                    const bool mm = key[s] == K;
+                    inb |= mm ? 1u << s : 0u;
+                    const bool nv = mm && cur.v[s] != AGNES_NIL;
+                    last = nv ? cur.v[s] : last;
+                    hasv |= nv ? 1u : 0u;
+                }
+                pend &= ~inb;
+                const uint64_t M = __builtin_amdgcn_ballot_w64(hasv != 0u);
+                const uint64_t bef = M & ((1ull << lane) - 1ull);
+                const uint32_t src = bef ? 63u - (uint32_t)__builtin_clzll(bef) : 0u;
+                const uint32_t from_lane = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)last);
+                uint32_t run = bef ? from_lane : lab[K];
+#pragma unroll
+                for (uint32_t s = 0; s < 4u; ++s) {
+                    if (key[s] == K) {
+                        if (cur.v[s] != AGNES_NIL) run = cur.v[s];
+                        slot[s] = run;
+                    }
+                }
+                if (M) {
+                    const uint32_t hl = 63u - (uint32_t)__builtin_clzll(M);
+                    const uint32_t nl = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(hl << 2), (int)last);
+                    __builtin_amdgcn_wave_barrier();
+                    if (lane == 0u) lab[K] = nl;
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+            /* the records into the staging area in stream order, then out as coalesced 8-B
+             * stores (records are 24 B: 3 words of 8 B) */
+            uint32_t o = incl - n_rec;
+#pragma unroll
+            for (uint32_t s = 0; s < 4u; ++s) {
+                const uint32_t two = (recs >> (2u * s)) & 3u;
+                if (two) {
+                    const uint32_t cb = (cur.c4 >> (8u * s)) & 0xFFu, ev = cb & AGNES_CODE_EVENT_MASK;
+                    const uint32_t rb = (cur.r4 >> (8u * s)) & 0xFFu, msg = cb >> AGNES_CODE_MSG_SHIFT;
+                    const uint64_t j = j0 + s;
+                    const uint32_t inst = B.s0 + (key[s] / keys);
+                    if (two & 1u) {
+                        uint2* const q = reinterpret_cast<uint2*>(stage + 6u * o++);
+                        q[0] = make_uint2((uint32_t)j, (uint32_t)(j >> 32));
+                        q[1] = make_uint2(inst, AGNES_NIL);
+                        q[2] = make_uint2(rb | (AGNES_EV_ROUND_SKIP << 8) | (msg << 16), 0u);
+                    }
+                    if (two & 2u) {
+                        const bool val = ev == AGNES_CODE_POLKA_VALUE || ev == AGNES_CODE_PRECOMMIT_VALUE;
+                        uint2* const q = reinterpret_cast<uint2*>(stage + 6u * o++);
+                        q[0] = make_uint2((uint32_t)j, (uint32_t)(j >> 32));
+                        q[1] = make_uint2(inst, val ? slot[s] : AGNES_NIL);
+                        q[2] = make_uint2(rb | (kind_of(ev) << 8) | (msg << 16), 0u);
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            uint2* const dst = reinterpret_cast<uint2*>(a.out + cnt);
+            for (uint32_t w8 = lane; w8 < 3u * total; w8 += 64u) dst[w8] = reinterpret_cast<const uint2*>(stage)[w8];
+            __builtin_amdgcn_wave_barrier();
+            cnt += total;
+        }
+    }
+}
+
 } // namespace events
 } // namespace agnes
 
@@ -337,13 +564,16 @@ hipError_t agnes_launch_events(const agnes_vote_batch* vb, const uint8_t* codes,
     const uint32_t n = vb->n_instances;
     EvArgs a{*vb, codes, offs, out, 2u * max_rounds};
     const dim3 grid((n + 63u) / 64u), blk(64);
-    if (!out) { /* pass 1: counts (codes only, 64-B windows when aligned), then the scan */
+    /* the batch-stream kernels: a wave per EB instances at a time, waves over the batches */
+    const uint32_t NB = (n + EB - 1u) / EB;
+    const uint32_t sblocks = (NB + 3u) / 4u < 8192u ? (NB + 3u) / 4u : 8192u;
+    if (!out) { /* pass 1: counts (codes only), then the scan */
         hipError_t e = hipMemsetAsync(offs, 0, sizeof(uint64_t), st);
         if (e != hipSuccess || n == 0) return e;
         {
             AgnesKt kt("event_count", st);
             if ((reinterpret_cast<uintptr_t>(codes) & 15u) == 0u)
-                hipLaunchKernelGGL((event_walk<false, 64u, true>), grid, blk, 0, st, a);
+                hipLaunchKernelGGL(event_count_stream, dim3(sblocks), dim3(256), 0, st, a);
             else
                 hipLaunchKernelGGL((event_walk<false, 4u, false>), grid, blk, 0, st, a);
         }
@@ -355,7 +585,10 @@ hipError_t agnes_launch_events(const agnes_vote_batch* vb, const uint8_t* codes,
     const bool a16 = ((reinterpret_cast<uintptr_t>(codes) | reinterpret_cast<uintptr_t>(vb->round) |
                        reinterpret_cast<uintptr_t>(vb->type) | reinterpret_cast<uintptr_t>(vb->value)) & 15u) == 0u;
     AgnesKt kt("event_emit", st);
-    if (a16) /* one wave per instance, coalesced */
+    if (a16 && a.keys <= 64u) { /* batches of EB instances as one stream per wave */
+        const size_t lds_s = (size_t)4u * (EB * a.keys + 512u * 6u) * sizeof(uint32_t);
+        hipLaunchKernelGGL(event_emit_stream, dim3(sblocks), dim3(256), lds_s, st, a);
+    } else if (a16) /* one wave per instance, coalesced */
     {
         /* one wave per instance (W = every wave: no second instance per wave); the
          * next pass of a long instance is loaded while the current one is processed */

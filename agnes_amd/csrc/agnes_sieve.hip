@@ -380,11 +380,17 @@ __global__ __launch_bounds__(256) void sieve(agnes_tally_args a, uint32_t lds_pe
                         csr = ld_carry ? cs[r] : 0u;
                         ts = q1 - csr - (Is - PS);
                     }
+                    /* a quiet round: even its sums after the chunk stay at or below the
+                     * thresholds (every vote of it Init, no RoundSkip) -- the usual case for the
+                     * few early next-round votes.  Uniform; sums < 2^31 in this domain. */
+                    const uint32_t ktot = (ld_carry ? ca[K] : 0u) + rdl(Ipa, 63u), ktc = (ld_carry ? ca[K + 1u] : 0u) + rdl(Ica, 63u);
+                    const bool quiet = ktot <= q2 && ktc <= q2 && (!SKIP || csr + rdl(Is, 63u) <= q1);
                     /* per vote (the lane prefixes again, fewer live registers): is_quorum on
                      * its own type's sums, precedence as a level; RoundSkip (3 * distinct >
                      * total <=> distinct > q1) */
                     uint64_t QA = 0, QN = 0;
                     uint32_t QS = 0;
+                    if (!quiet)
 #pragma unroll
                     for (uint32_t s = 0; s < LV; ++s) {
                         const uint32_t wm = ((am >> s) & 1u) ? w[s] : 0u;
