@@ -36,12 +36,12 @@ MODE_REFERENCE, MODE_DEDUP = 0, 1
 FLAG_ROUND_SKIP, FLAG_STATE_MACHINE, FLAG_DISTINCT_VALUES = 0x1, 0x2, 0x4
 FLAG_ONE_INSTANCE = 0x8  # agnes_tally_carried: segments are slices of one instance (id cfg.reserved)
 # route override (agnes.h AGNES_ROUTE_*): diagnostics / route-equivalence tests
-ROUTE_SHIFT, ROUTE_AUTO, ROUTE_INSTANCE, ROUTE_SPLIT, ROUTE_WIDE, ROUTE_FAST = 8, 0, 1, 2, 3, 4
+ROUTE_SHIFT, ROUTE_AUTO, ROUTE_INSTANCE, ROUTE_SPLIT, ROUTE_WIDE = 8, 0, 1, 2, 3
 EPOCH_BITS_SHIFT = 16
 
 
 def FLAG_ROUTE(r: int) -> int:
-    return (r & 7) << ROUTE_SHIFT
+    return (r & 3) << ROUTE_SHIFT
 
 
 def FLAG_EPOCH_BITS(b: int) -> int:

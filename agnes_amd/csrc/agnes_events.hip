@@ -12,11 +12,19 @@
  * tally added to that executor (every code but INVALID / REJECTED), Value{} (0)
  * before any.
  *
- * Two walks, one instance per lane (as the edge summary): a count pass over the
- * codes (1 B per vote), the exclusive scan of the counts (agnes_edges.hip), and an
- * emit pass that follows each executor's value slot in LDS ([key][lane], a wave's
- * 64 lookups on 64 banks) over codes, round, type and value (7 B per vote) and
- * writes 24-B records at the scanned offsets.  HBM bound.
+ * Two passes and a scan.  The count pass walks the codes (1 B per vote), one
+ * instance per lane in 64-B windows; the exclusive scan of the counts is
+ * agnes_edges.hip's.  The emit pass (event_emit_stream) walks a batch of EB
+ * consecutive instances as one vote stream per wave, 256 votes per pass over code,
+ * round, type and value (7 B per vote), the next pass loaded while the current one
+ * is processed; it writes the 24-B records through an LDS staging area as
+ * coalesced 8-B stores.  The value slot after a vote: its own value when non-nil,
+ * else the last non-nil value of its (instance, round, type) in the pass, else the
+ * carried slot in LDS ([EB][keys] per wave).  When the pass's (instance, round)
+ * runs do not go back (every config the bench runs), one max-scan per vote type
+ * finds that last value for all keys at once; otherwise one ballot pass per key
+ * present.  Measured (C2, 200M votes, 67.8M records): 0.85 ms, against 1.01 ms for
+ * the one-wave-per-instance walk (event_emit_wave, kept for keys > 64).
  */
 #include <hip/hip_runtime.h>
 
@@ -326,123 +334,105 @@ __global__ __launch_bounds__(256) void event_emit_wave(EvArgs a) {
     }
 }
 
-/* ---- the batch-stream forms (aligned columns): a wave walks a batch of up to EB
+/* ---- the batch-stream emit (aligned columns): a wave walks a batch of up to EB
  * consecutive instances as ONE vote stream, so a short instance (C2: 200 votes) no
- * longer leaves most of a pass idle, and the records leave through LDS as coalesced
- * 8-B stores ------------------------------------------------------------------- */
+ * longer leaves most of a pass idle; the next pass (this batch's, or the first of
+ * the wave's next batch, whose offsets were loaded one batch ahead) is loaded while
+ * the current one is processed ---------------------------------------------------- */
 constexpr uint32_t EB = 32u; /* instances per batch (offsets in lanes 0..EB) */
+#ifndef EV_STAGE
+#define EV_STAGE 256u /* records a pass stages in LDS (6 KB per wave) */
+#endif
+#ifndef EV_PREFETCH
+#define EV_PREFETCH 1
+#endif
 
-/* the batch's offsets in lanes 0..m (clamped to n_votes), as two halves */
+/* a batch's offsets in lanes 0..m (clamped to n_votes): the loads, then the
+ * wave-uniform bounds once they are needed */
+struct EvRaw {
+    uint32_t olo, ohi;
+};
 struct EvBatch {
     uint32_t s0, m, olo, ohi;
     uint64_t O0, Om;
 };
-__device__ __forceinline__ EvBatch ev_batch(const EvArgs& a, uint32_t b, uint32_t lane) {
-    EvBatch B;
-    const uint32_t n = a.vb.n_instances;
+__device__ __forceinline__ EvRaw ev_load(const EvArgs& a, uint32_t b, uint32_t lane) {
+    const uint32_t n = a.vb.n_instances, s0 = b * EB, m = n - s0 < EB ? n - s0 : EB;
     const uint64_t NV = a.vb.n_votes;
-    B.s0 = b * EB;
-    B.m = n - B.s0 < EB ? n - B.s0 : EB;
     uint64_t o = 0;
-    if (lane <= B.m) {
-        o = a.vb.offsets[B.s0 + lane];
+    if (lane <= m) {
+        o = a.vb.offsets[s0 + lane];
         o = o < NV ? o : NV;
     }
-    B.olo = (uint32_t)o;
-    B.ohi = (uint32_t)(o >> 32);
+    return EvRaw{(uint32_t)o, (uint32_t)(o >> 32)};
+}
+__device__ __forceinline__ EvBatch ev_batch(const EvArgs& a, uint32_t b, EvRaw r) {
+    EvBatch B;
+    const uint32_t n = a.vb.n_instances;
+    B.s0 = b * EB;
+    B.m = n - B.s0 < EB ? n - B.s0 : EB;
+    B.olo = r.olo;
+    B.ohi = r.ohi;
     B.O0 = ((uint64_t)__builtin_amdgcn_readlane(B.ohi, 0) << 32) | (uint32_t)__builtin_amdgcn_readlane(B.olo, 0);
     B.Om = ((uint64_t)__builtin_amdgcn_readlane(B.ohi, B.m) << 32) | (uint32_t)__builtin_amdgcn_readlane(B.olo, B.m);
     return B;
 }
 
-/* the count pass: per instance its records (a tallied vote gives its event and its
- * RoundSkip: code bits 0..2 in 1..5, bit 3), from the codes alone (1 B per vote) */
-__global__ __launch_bounds__(256) void event_count_stream(EvArgs a) {
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t n = a.vb.n_instances, NB = (n + EB - 1u) / EB;
-    const uint64_t NV = a.vb.n_votes;
-    for (uint32_t b = blockIdx.x * 4u + wave; b < NB; b += gridDim.x * 4u) {
-        const EvBatch B = ev_batch(a, b, lane);
-        const uint64_t ol = ((uint64_t)B.ohi << 32) | B.olo;
-        const uint64_t on = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * (lane + 1u)), (int)B.ohi) << 32) |
-                            (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * (lane + 1u)), (int)B.olo);
-        uint64_t cnt = 0; /* lane k < m: records of instance s0 + k */
-        /* 1024-vote chunks: lane l holds votes 16l .. 16l+15 (one 16-B load of codes) */
-        for (uint64_t c = B.O0 & ~15ull; c < B.Om; c += 1024u) {
-            const uint64_t j0 = c + 16u * lane;
-            uint32_t w4[4] = {0u, 0u, 0u, 0u};
-            if (j0 + 16u <= NV) {
-                const uint4 q = *reinterpret_cast<const uint4*>(a.codes + j0);
-                w4[0] = q.x; w4[1] = q.y; w4[2] = q.z; w4[3] = q.w;
-            } else {
-                for (uint32_t t = 0; t < 16u && j0 + t < NV; ++t) w4[t >> 2] |= (uint32_t)a.codes[j0 + t] << (8u * (t & 3u));
-            }
-            /* records per vote, one byte each: event in 1..5 (e < 6: not INVALID / REJECTED),
-             * plus its RoundSkip bit */
-            uint32_t rc[4], tot = 0u;
-#pragma unroll
-            for (uint32_t d = 0; d < 4u; ++d) {
-                const uint32_t e = w4[d] & 0x07070707u;
-                const uint32_t valid = ~((e + 0x02020202u) >> 3) & 0x01010101u;
-                const uint32_t nz = (e | (e >> 1) | (e >> 2)) & 0x01010101u;
-                rc[d] = (nz & valid) + ((w4[d] >> 3) & valid);
-                tot += (rc[d] * 0x01010101u) >> 24;
-            }
-            const uint32_t incl = wave_scan_incl(tot), excl = incl - tot;
-            const uint32_t ctot = __builtin_amdgcn_readlane(incl, 63);
-            const uint64_t cend = c + 1024u;
-            /* records of the chunk's votes before position p (c <= p <= cend) */
-            auto before = [&](uint64_t p) -> uint32_t {
-                if (p >= cend) return ctot;
-                const uint32_t lp = (uint32_t)(p - c), ln = lp >> 4, bt = lp & 15u;
-                uint32_t mine = 0u; /* (every lane) its bytes below bt */
-#pragma unroll
-                for (uint32_t d = 0; d < 4u; ++d) {
-                    const uint32_t lo = 4u * d;
-                    const uint32_t keep = bt >= lo + 4u ? 0xFFFFFFFFu : (bt <= lo ? 0u : (1u << (8u * (bt - lo))) - 1u);
-                    mine += ((rc[d] & keep) * 0x01010101u) >> 24;
-                }
-                return __builtin_amdgcn_readlane(excl, ln) + __builtin_amdgcn_readlane(mine, ln);
-            };
-            /* the instances overlapping the chunk (uniform loop) */
-            uint64_t rest = __builtin_amdgcn_ballot_w64(lane < B.m && ol < cend && on > c);
-            while (rest) {
-                const uint32_t k = (uint32_t)__builtin_ctzll(rest);
-                rest &= rest - 1ull;
-                const uint64_t ks = ((uint64_t)__builtin_amdgcn_readlane(B.ohi, k) << 32) | (uint32_t)__builtin_amdgcn_readlane(B.olo, k);
-                const uint64_t ke = ((uint64_t)__builtin_amdgcn_readlane(B.ohi, k + 1u) << 32) |
-                                    (uint32_t)__builtin_amdgcn_readlane(B.olo, k + 1u);
-                const uint32_t x = before(ke < cend ? ke : cend) - before(ks > c ? ks : c);
-                if (lane == k) cnt += x;
-            }
-        }
-        if (lane < B.m) a.offs[B.s0 + lane + 1u] = cnt;
-    }
+/* inclusive max-scan over the wave (row_shr 1,2,4,8, row_bcast 15, 31) */
+__device__ __forceinline__ uint32_t wave_max_incl(uint32_t x) {
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false));
+    return x;
+}
+/* the value of lane - 1 (0 in lane 0) */
+__device__ __forceinline__ uint32_t from_prev(uint32_t x, uint32_t lane) {
+    const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - 1u) << 2), (int)x);
+    return lane ? y : 0u;
 }
 
-__global__ __launch_bounds__(256) void event_emit_stream(EvArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void event_emit_stream(EvArgs a) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t n = a.vb.n_instances, NB = (n + EB - 1u) / EB;
+    const uint32_t n = a.vb.n_instances, NB = (n + EB - 1u) / EB, BS = gridDim.x * 4u;
     const uint64_t NV = a.vb.n_votes;
-    const uint32_t keys = a.keys;
-    /* per wave: the value slots [EB][keys], then the record staging area (512 records) */
-    uint32_t* const lab = reinterpret_cast<uint32_t*>(agnes_smem) + wave * (EB * keys + 512u * 6u);
+    const uint32_t keys = a.keys, R2 = keys >> 1;
+    /* per wave: the value slots [EB][keys], then the record staging area */
+    uint32_t* const lab = reinterpret_cast<uint32_t*>(agnes_smem) + wave * (EB * keys + 6u * EV_STAGE);
     uint32_t* const stage = lab + EB * keys;
-    for (uint32_t b = blockIdx.x * 4u + wave; b < NB; b += gridDim.x * 4u) {
-        const EvBatch B = ev_batch(a, b, lane);
-        for (uint32_t k = lane; k < EB * keys; k += 64u) lab[k] = 0u; /* VoteCount::new: Value{} */
-        __builtin_amdgcn_wave_barrier();
-        const uint64_t ol = ((uint64_t)B.ohi << 32) | B.olo;
-        uint64_t cnt = a.offs[B.s0]; /* the batch's first record */
-        for (uint64_t c = B.O0 & ~3ull; c < B.Om; c += 256u) {
-            const uint64_t j0 = c + 4u * lane;
-            Pass cur;
-            load_pass(a, j0, NV, cur);
+    uint32_t b = blockIdx.x * 4u + wave;
+    if (b >= NB) return; /* wave-uniform */
+    EvBatch B = ev_batch(a, b, ev_load(a, b, lane));
+    uint32_t nb = b + BS;
+    EvRaw NR = nb < NB ? ev_load(a, nb, lane) : EvRaw{0u, 0u};
+    uint64_t ncnt = nb < NB ? a.offs[nb * EB] : 0u;
+    uint64_t cnt = a.offs[B.s0]; /* the batch's first record */
+    uint64_t c = B.O0 & ~3ull;
+    Pass cur;
+    load_pass(a, c + 4u * lane, NV, cur);
+    for (uint32_t k = lane; k < EB * keys; k += 64u) lab[k] = 0u; /* VoteCount::new: Value{} */
+    __builtin_amdgcn_wave_barrier();
+    for (;;) {
+        uint64_t nc = c + 256u;
+        const bool sw = nc >= B.Om, last = sw && nb >= NB;
+        EvBatch NBt = B;
+        if (sw && !last) {
+            NBt = ev_batch(a, nb, NR);
+            nc = NBt.O0 & ~3ull;
+        }
+        Pass nxt;
+        if (!last) load_pass(a, nc + 4u * lane, NV, nxt);
+        if (c < B.Om) {
+            const uint64_t ol = ((uint64_t)B.ohi << 32) | B.olo;
+            /* the pass's positions of the batch's votes, [lo, hi) (wave-uniform) */
+            const uint32_t lo = B.O0 > c ? (uint32_t)(B.O0 - c) : 0u;
+            const uint32_t hi = B.Om - c < 256u ? (uint32_t)(B.Om - c) : 256u;
+            const uint32_t p0 = 4u * lane;
             /* per vote: batch instance (the count of the batch's later instances starting at
-             * or before it: ballots over the offsets' lanes), key, records */
+             * or before it: ballots over the offsets' lanes) */
             uint32_t kk[4];
-#pragma unroll
-            for (uint32_t s = 0; s < 4u; ++s) kk[s] = 0u;
             {
                 /* instances 1..m-1 starting inside (c, c + 256): few; every vote counts them */
                 const uint64_t st = __builtin_amdgcn_ballot_w64(lane >= 1u && lane < B.m && ol > c && ol < c + 256u);
@@ -454,102 +444,201 @@ __global__ __launch_bounds__(256) void event_emit_stream(EvArgs a) {
                 while (rest) {
                     const uint32_t k = (uint32_t)__builtin_ctzll(rest);
                     rest &= rest - 1ull;
-                    const uint64_t ks = ((uint64_t)__builtin_amdgcn_readlane(B.ohi, k) << 32) |
-                                        (uint32_t)__builtin_amdgcn_readlane(B.olo, k);
+                    const uint32_t ks = __builtin_amdgcn_readlane(B.olo, k) - (uint32_t)c; /* in (0, 256) */
 #pragma unroll
-                    for (uint32_t s = 0; s < 4u; ++s) kk[s] += (j0 + s >= ks) ? 1u : 0u;
+                    for (uint32_t s = 0; s < 4u; ++s) kk[s] += (p0 + s >= ks) ? 1u : 0u;
                 }
             }
-            uint32_t key[4], n_rec = 0, recs = 0;
+            /* the 4 votes' masks, bytewise: tallied (a batch vote, code not INVALID / REJECTED,
+             * type <= 1, round < max_rounds), with an event, with the RoundSkip bit */
+            uint32_t inm, hasm, skm;
+            {
+                const int l0 = min(max((int)lo - (int)p0, 0), 4), h0 = min(max((int)hi - (int)p0, 0), 4);
+                const uint32_t inr = ((1u << h0) - 1u) & ~((1u << l0) - 1u);
+                const uint32_t e4 = cur.c4 & 0x07070707u;
+                const uint32_t okev = ~((e4 + 0x02020202u) >> 3) & 0x01010101u;
+                const uint32_t tx = cur.t4 & 0xFEFEFEFEu;
+                const uint32_t okt = ~((((tx & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | tx) >> 7) & 0x01010101u;
+                const uint32_t okr = (~(((cur.r4 | 0x80808080u) - R2 * 0x01010101u) | cur.r4) >> 7) & 0x01010101u;
+                auto nib = [](uint32_t x) { return ((x * 0x01020408u) >> 24) & 0xFu; };
+                inm = nib(okev & okt & okr) & inr;
+                hasm = inm & nib((e4 | (e4 >> 1) | (e4 >> 2)) & 0x01010101u);
+                skm = inm & nib((cur.c4 >> 3) & 0x01010101u);
+            }
+            const uint32_t n_rec = (uint32_t)__builtin_popcount(hasm) + (uint32_t)__builtin_popcount(skm);
+            uint32_t key[4], rid[4];
+            /* the run check: (instance, round) non-decreasing over the pass's tallied votes */
+            uint32_t rmax = 0u, bad = 0u, rfirst = 0xFFFFFFFFu;
+            uint32_t lv[2] = {0u, 0u}, lr[2] = {0u, 0u}, fr[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
 #pragma unroll
             for (uint32_t s = 0; s < 4u; ++s) {
-                const uint64_t j = j0 + s;
-                const uint32_t cb = (cur.c4 >> (8u * s)) & 0xFFu, ev = cb & AGNES_CODE_EVENT_MASK;
-                const uint32_t rb = (cur.r4 >> (8u * s)) & 0xFFu, tb = (cur.t4 >> (8u * s)) & 0xFFu;
-                const uint32_t k = rb * 2u + tb;
-                const bool in = j >= B.O0 && j < B.Om && ev != AGNES_CODE_INVALID && ev != AGNES_CODE_REJECTED &&
-                                tb <= 1u && k < keys;
-                key[s] = in ? kk[s] * keys + k : 0xFFFFFFFFu;
-                const uint32_t skip = in ? (cb >> 3) & 1u : 0u, has = (in && ev != AGNES_CODE_NONE) ? 1u : 0u;
-                recs |= (skip | (has << 1)) << (2u * s);
-                n_rec += skip + has;
+                const uint32_t rb = (cur.r4 >> (8u * s)) & 0xFFu, tb = (cur.t4 >> (8u * s)) & 1u;
+                const bool in = (inm >> s) & 1u;
+                key[s] = in ? kk[s] * keys + rb * 2u + tb : 0xFFFFFFFFu;
+                /* run id + 1 (0: not tallied) */
+                rid[s] = in ? kk[s] * R2 + rb + 1u : 0u;
+                bad |= (in && rid[s] < rmax) ? 1u : 0u;
+                rmax = max(rmax, rid[s]);
+                rfirst = (in && rfirst == 0xFFFFFFFFu) ? rid[s] : rfirst;
+                const bool nn = in && cur.v[s] != AGNES_NIL;
+                /* per type: the lane's last non-nil vote (value, run) and its first's run */
+                lv[0] = (nn && !tb) ? cur.v[s] : lv[0];
+                lv[1] = (nn && tb) ? cur.v[s] : lv[1];
+                lr[0] = (nn && !tb) ? rid[s] : lr[0];
+                lr[1] = (nn && tb) ? rid[s] : lr[1];
+                fr[0] = (nn && !tb && fr[0] == 0xFFFFFFFFu) ? rid[s] : fr[0];
+                fr[1] = (nn && tb && fr[1] == 0xFFFFFFFFu) ? rid[s] : fr[1];
             }
             const uint32_t incl = wave_scan_incl(n_rec);
-            const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-            /* the value slot after each vote, per (instance, round, type) present
-             * (round_votes.rs:50-54: the last non-nil value its bucket took) */
             uint32_t slot[4] = {0u, 0u, 0u, 0u};
-            uint32_t pend = (key[0] != 0xFFFFFFFFu ? 1u : 0u) | (key[1] != 0xFFFFFFFFu ? 2u : 0u) |
-                            (key[2] != 0xFFFFFFFFu ? 4u : 0u) | (key[3] != 0xFFFFFFFFu ? 8u : 0u);
-            for (;;) {
-                const uint64_t lm = __builtin_amdgcn_ballot_w64(pend != 0u);
-                if (!lm) break;
-                const uint32_t kl = (uint32_t)__builtin_ctzll(lm);
-                const uint32_t ks = (uint32_t)__builtin_ctz(__builtin_amdgcn_readlane(pend, kl));
-                const uint32_t kv = ks == 0u ? key[0] : (ks == 1u ? key[1] : (ks == 2u ? key[2] : key[3]));
-                const uint32_t K = __builtin_amdgcn_readlane(kv, kl);
-                uint32_t inb = 0, last = 0, hasv = 0;
+            /* runs: one scan per type instead of a pass per key */
+            const uint32_t pmax = from_prev(wave_max_incl(rmax), lane);
+            bad |= (rfirst != 0xFFFFFFFFu && rfirst < pmax) ? 1u : 0u;
+            if (!__builtin_amdgcn_ballot_w64(bad != 0u)) {
+                /* per type: the last earlier lane holding a non-nil vote, (run << 6 | lane) */
+                uint32_t cr[2], cv[2], tail_nx[2];
 #pragma unroll
-                for (uint32_t s = 0; s < 4u; ++s) {
-                    const bool mm = key[s] == K;
-                    inb |= mm ? 1u << s : 0u;
-                    const bool nv = mm && cur.v[s] != AGNES_NIL;
-                    last = nv ? cur.v[s] : last;
-                    hasv |= nv ? 1u : 0u;
+                for (uint32_t t = 0; t < 2u; ++t) {
+                    const uint32_t P = lr[t] ? (lr[t] << 6) | lane : 0u;
+                    const uint32_t E = from_prev(wave_max_incl(P), lane);
+                    cr[t] = E >> 6;
+                    cv[t] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((E & 63u) << 2), (int)lv[t]);
+                    /* the next lane holding a non-nil vote of type t: its first run (a tail test) */
+                    const uint64_t M = __builtin_amdgcn_ballot_w64(lr[t] != 0u) & ~((2ull << lane) - 1ull);
+                    const uint32_t nl = M ? (uint32_t)__builtin_ctzll(M) : lane;
+                    const uint32_t f = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(nl << 2), (int)fr[t]);
+                    tail_nx[t] = M ? f : 0u;
                 }
-                pend &= ~inb;
-                const uint64_t M = __builtin_amdgcn_ballot_w64(hasv != 0u);
-                const uint64_t bef = M & ((1ull << lane) - 1ull);
-                const uint32_t src = bef ? 63u - (uint32_t)__builtin_clzll(bef) : 0u;
-                const uint32_t from_lane = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)last);
-                uint32_t run = bef ? from_lane : lab[K];
+                /* per vote, in order: its own value, the run's last in this pass, or the carry */
+                uint32_t wr = 0u; /* votes that are the last non-nil of their (run, type) in the pass */
 #pragma unroll
                 for (uint32_t s = 0; s < 4u; ++s) {
-                    if (key[s] == K) {
-                        if (cur.v[s] != AGNES_NIL) run = cur.v[s];
-                        slot[s] = run;
+                    if (rid[s]) {
+                        const uint32_t tb = (cur.t4 >> (8u * s)) & 1u;
+                        const uint32_t r_t = tb ? cr[1] : cr[0], v_t = tb ? cv[1] : cv[0];
+                        if (cur.v[s] != AGNES_NIL) {
+                            slot[s] = cur.v[s];
+                            if (tb) { cr[1] = rid[s]; cv[1] = cur.v[s]; } else { cr[0] = rid[s]; cv[0] = cur.v[s]; }
+                            wr |= 1u << s;
+                        } else {
+                            slot[s] = r_t == rid[s] ? v_t : lab[key[s]];
+                        }
                     }
                 }
-                if (M) {
-                    const uint32_t hl = 63u - (uint32_t)__builtin_clzll(M);
-                    const uint32_t nl = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(hl << 2), (int)last);
-                    __builtin_amdgcn_wave_barrier();
-                    if (lane == 0u) lab[K] = nl;
+                /* a non-nil vote is its (run, type)'s last in the pass unless a later one of the
+                 * lane, or the next lane's first of that type, has the same run */
+#pragma unroll
+                for (uint32_t s = 0; s < 4u; ++s) {
+                    if ((wr >> s) & 1u) {
+                        const uint32_t tb = (cur.t4 >> (8u * s)) & 1u;
+                        uint32_t nxr = tb ? tail_nx[1] : tail_nx[0];
+#pragma unroll
+                        for (uint32_t u = 3u; u > s; --u) {
+                            const uint32_t tu = (cur.t4 >> (8u * u)) & 1u;
+                            nxr = (((wr >> u) & 1u) && tu == tb) ? rid[u] : nxr;
+                        }
+                        if (nxr == rid[s]) wr &= ~(1u << s);
+                    }
                 }
                 __builtin_amdgcn_wave_barrier();
-            }
-            /* the records into the staging area in stream order, then out as coalesced 8-B
-             * stores (records are 24 B: 3 words of 8 B) */
-            uint32_t o = incl - n_rec;
 #pragma unroll
-            for (uint32_t s = 0; s < 4u; ++s) {
-                const uint32_t two = (recs >> (2u * s)) & 3u;
-                if (two) {
-                    const uint32_t cb = (cur.c4 >> (8u * s)) & 0xFFu, ev = cb & AGNES_CODE_EVENT_MASK;
-                    const uint32_t rb = (cur.r4 >> (8u * s)) & 0xFFu, msg = cb >> AGNES_CODE_MSG_SHIFT;
-                    const uint64_t j = j0 + s;
-                    const uint32_t inst = B.s0 + (key[s] / keys);
-                    if (two & 1u) {
-                        uint2* const q = reinterpret_cast<uint2*>(stage + 6u * o++);
-                        q[0] = make_uint2((uint32_t)j, (uint32_t)(j >> 32));
-                        q[1] = make_uint2(inst, AGNES_NIL);
-                        q[2] = make_uint2(rb | (AGNES_EV_ROUND_SKIP << 8) | (msg << 16), 0u);
+                for (uint32_t s = 0; s < 4u; ++s)
+                    if ((wr >> s) & 1u) lab[key[s]] = cur.v[s];
+                __builtin_amdgcn_wave_barrier();
+            } else {
+                /* rounds revisited inside the pass: one pass per (instance, round, type) present
+                 * (round_votes.rs:50-54: the last non-nil value its bucket took) */
+                uint32_t pend = (key[0] != 0xFFFFFFFFu ? 1u : 0u) | (key[1] != 0xFFFFFFFFu ? 2u : 0u) |
+                                (key[2] != 0xFFFFFFFFu ? 4u : 0u) | (key[3] != 0xFFFFFFFFu ? 8u : 0u);
+                for (;;) {
+                    const uint64_t lm = __builtin_amdgcn_ballot_w64(pend != 0u);
+                    if (!lm) break;
+                    const uint32_t kl = (uint32_t)__builtin_ctzll(lm);
+                    const uint32_t ks = (uint32_t)__builtin_ctz(__builtin_amdgcn_readlane(pend, kl));
+                    const uint32_t kv = ks == 0u ? key[0] : (ks == 1u ? key[1] : (ks == 2u ? key[2] : key[3]));
+                    const uint32_t K = __builtin_amdgcn_readlane(kv, kl);
+                    uint32_t inb = 0, lastv = 0, hasv = 0;
+#pragma unroll
+                    for (uint32_t s = 0; s < 4u; ++s) {
+                        const bool mm = key[s] == K;
+                        inb |= mm ? 1u << s : 0u;
+                        const bool nv = mm && cur.v[s] != AGNES_NIL;
+                        lastv = nv ? cur.v[s] : lastv;
+                        hasv |= nv ? 1u : 0u;
                     }
-                    if (two & 2u) {
-                        const bool val = ev == AGNES_CODE_POLKA_VALUE || ev == AGNES_CODE_PRECOMMIT_VALUE;
-                        uint2* const q = reinterpret_cast<uint2*>(stage + 6u * o++);
-                        q[0] = make_uint2((uint32_t)j, (uint32_t)(j >> 32));
-                        q[1] = make_uint2(inst, val ? slot[s] : AGNES_NIL);
-                        q[2] = make_uint2(rb | (kind_of(ev) << 8) | (msg << 16), 0u);
+                    pend &= ~inb;
+                    const uint64_t M = __builtin_amdgcn_ballot_w64(hasv != 0u);
+                    const uint64_t bef = M & ((1ull << lane) - 1ull);
+                    const uint32_t src = bef ? 63u - (uint32_t)__builtin_clzll(bef) : 0u;
+                    const uint32_t from_lane = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)lastv);
+                    uint32_t run = bef ? from_lane : lab[K];
+#pragma unroll
+                    for (uint32_t s = 0; s < 4u; ++s) {
+                        if (key[s] == K) {
+                            if (cur.v[s] != AGNES_NIL) run = cur.v[s];
+                            slot[s] = run;
+                        }
                     }
+                    if (M) {
+                        const uint32_t hl = 63u - (uint32_t)__builtin_clzll(M);
+                        const uint32_t nl = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(hl << 2), (int)lastv);
+                        __builtin_amdgcn_wave_barrier();
+                        if (lane == 0u) lab[K] = nl;
+                    }
+                    __builtin_amdgcn_wave_barrier();
                 }
             }
-            __builtin_amdgcn_wave_barrier();
-            uint2* const dst = reinterpret_cast<uint2*>(a.out + cnt);
-            for (uint32_t w8 = lane; w8 < 3u * total; w8 += 64u) dst[w8] = reinterpret_cast<const uint2*>(stage)[w8];
-            __builtin_amdgcn_wave_barrier();
+            /* the records in stream order: through the staging area and out as coalesced 8-B
+             * stores (a record is 3 of them), or straight out when the pass has more than
+             * the area holds */
+            const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+            const bool staged = total <= EV_STAGE;
+            auto emit = [&](agnes_vote_event* dst) {
+                uint32_t o = incl - n_rec;
+#pragma unroll
+                for (uint32_t s = 0; s < 4u; ++s) {
+                    const uint32_t two = ((skm >> s) & 1u) | (((hasm >> s) & 1u) << 1);
+                    if (two) {
+                        const uint32_t cb = (cur.c4 >> (8u * s)) & 0xFFu, ev = cb & AGNES_CODE_EVENT_MASK;
+                        const uint32_t rb = (cur.r4 >> (8u * s)) & 0xFFu, msg = cb >> AGNES_CODE_MSG_SHIFT;
+                        const uint64_t j = c + p0 + s;
+                        const uint32_t inst = B.s0 + kk[s];
+                        if (two & 1u) put(dst + o++, j, inst, AGNES_NIL, rb, AGNES_EV_ROUND_SKIP, msg);
+                        if (two & 2u) {
+                            const bool val = ev == AGNES_CODE_POLKA_VALUE || ev == AGNES_CODE_PRECOMMIT_VALUE;
+                            put(dst + o++, j, inst, val ? slot[s] : AGNES_NIL, rb, kind_of(ev), msg);
+                        }
+                    }
+                }
+            };
+            if (staged) /* (two instantiations: LDS stores here, global ones below) */
+                emit(reinterpret_cast<agnes_vote_event*>(stage));
+            else
+                emit(a.out + cnt);
+            if (staged) {
+                __builtin_amdgcn_wave_barrier();
+                uint2* const out8 = reinterpret_cast<uint2*>(a.out + cnt);
+                for (uint32_t w8 = lane; w8 < 3u * total; w8 += 64u) out8[w8] = reinterpret_cast<const uint2*>(stage)[w8];
+                __builtin_amdgcn_wave_barrier();
+            }
             cnt += total;
         }
+        if (last) break;
+        if (sw) { /* the wave's next batch */
+            b = nb;
+            B = NBt;
+            cnt = ncnt;
+            nb = b + BS;
+            if (nb < NB) {
+                NR = ev_load(a, nb, lane);
+                ncnt = a.offs[nb * EB];
+            }
+            __builtin_amdgcn_wave_barrier();
+            for (uint32_t k = lane; k < EB * keys; k += 64u) lab[k] = 0u;
+            __builtin_amdgcn_wave_barrier();
+        }
+        c = nc;
+        cur = nxt;
     }
 }
 
@@ -564,16 +653,13 @@ hipError_t agnes_launch_events(const agnes_vote_batch* vb, const uint8_t* codes,
     const uint32_t n = vb->n_instances;
     EvArgs a{*vb, codes, offs, out, 2u * max_rounds};
     const dim3 grid((n + 63u) / 64u), blk(64);
-    /* the batch-stream kernels: a wave per EB instances at a time, waves over the batches */
-    const uint32_t NB = (n + EB - 1u) / EB;
-    const uint32_t sblocks = (NB + 3u) / 4u < 8192u ? (NB + 3u) / 4u : 8192u;
     if (!out) { /* pass 1: counts (codes only), then the scan */
         hipError_t e = hipMemsetAsync(offs, 0, sizeof(uint64_t), st);
         if (e != hipSuccess || n == 0) return e;
         {
             AgnesKt kt("event_count", st);
-            if ((reinterpret_cast<uintptr_t>(codes) & 15u) == 0u)
-                hipLaunchKernelGGL(event_count_stream, dim3(sblocks), dim3(256), 0, st, a);
+            if ((reinterpret_cast<uintptr_t>(codes) & 15u) == 0u) /* 64-B windows when aligned */
+                hipLaunchKernelGGL((event_walk<false, 64u, true>), grid, blk, 0, st, a);
             else
                 hipLaunchKernelGGL((event_walk<false, 4u, false>), grid, blk, 0, st, a);
         }
@@ -585,18 +671,25 @@ hipError_t agnes_launch_events(const agnes_vote_batch* vb, const uint8_t* codes,
     const bool a16 = ((reinterpret_cast<uintptr_t>(codes) | reinterpret_cast<uintptr_t>(vb->round) |
                        reinterpret_cast<uintptr_t>(vb->type) | reinterpret_cast<uintptr_t>(vb->value)) & 15u) == 0u;
     AgnesKt kt("event_emit", st);
-    if (a16 && a.keys <= 64u) { /* batches of EB instances as one stream per wave */
-        const size_t lds_s = (size_t)4u * (EB * a.keys + 512u * 6u) * sizeof(uint32_t);
+    if (a16 && a.keys <= 64u) {
+        /* batches of EB instances as one stream per wave; a resident grid (the blocks a
+         * CU holds x 256 CUs), so each wave walks several batches and prefetches across them */
+        const uint32_t NB = (n + EB - 1u) / EB;
+        const size_t lds_s = (size_t)4u * (EB * a.keys + 6u * EV_STAGE) * sizeof(uint32_t);
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, event_emit_stream, 256, lds_s) != hipSuccess ||
+            per_cu < 1)
+            per_cu = 1;
+        const uint32_t cap = EV_PREFETCH ? 256u * (uint32_t)per_cu : 0xFFFFFFFFu;
+        const uint32_t sblocks = (NB + 3u) / 4u < cap ? (NB + 3u) / 4u : cap;
         hipLaunchKernelGGL(event_emit_stream, dim3(sblocks), dim3(256), lds_s, st, a);
-    } else if (a16) /* one wave per instance, coalesced */
-    {
-        /* one wave per instance (W = every wave: no second instance per wave); the
-         * next pass of a long instance is loaded while the current one is processed */
+    } else if (a16) {
+        /* one wave per instance, coalesced; the next pass of a long instance is loaded
+         * while the current one is processed */
         const size_t lds_w = (size_t)4u * a.keys * sizeof(uint32_t);
         const uint32_t blocks = (n + 3u) / 4u;
         hipLaunchKernelGGL(event_emit_wave, dim3(blocks), dim3(256), lds_w, st, a);
-    }
-    else
+    } else
         hipLaunchKernelGGL((event_walk<true, 4u, false>), grid, blk, lds, st, a);
     return hipGetLastError();
 }

@@ -82,9 +82,6 @@ hipError_t agnes_launch_tally_fast(const agnes_tally_args* a, uint32_t mode, int
  * and State machine in one pass; same deferral protocol */
 bool agnes_sweep_supported(const agnes_tally_args* a);
 hipError_t agnes_launch_sweep(const agnes_tally_args* a, int num_cus, hipStream_t stream);
-/* the DEDUP / RoundSkip codes-only tally (agnes_sieve.hip) */
-bool agnes_sieve_supported(const agnes_tally_args* a, uint32_t mode);
-hipError_t agnes_launch_sieve(const agnes_tally_args* a, uint32_t mode, int num_cus, hipStream_t stream);
 /* the 8-votes-per-lane flow kernel (agnes_flow.hip) for the sweep route's streams */
 bool agnes_flow_supported(const agnes_tally_args* a);
 hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t stream);

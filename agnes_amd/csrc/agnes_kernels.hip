@@ -1303,12 +1303,7 @@ static hipError_t launch_mode(const agnes_tally_args* a, uint32_t lpw, int num_c
             const bool split = SM && route != AGNES_ROUTE_INSTANCE && agnes_apply_codes_supported(a);
             agnes_tally_args b = *a;
             if (split) b.flags &= ~AGNES_FLAG_STATE_MACHINE;
-            /* codes only: the sieve (one pass per round over 512-vote chunks), unless
-             * forced onto tally_fast or its tables do not fit */
-            if (!(b.flags & AGNES_FLAG_STATE_MACHINE) && route != AGNES_ROUTE_FAST && agnes_sieve_supported(&b, MODE)) {
-                AgnesKt kt("sieve", st);
-                e = agnes_launch_sieve(&b, MODE, num_cus, st);
-            } else {
+            {
                 AgnesKt kt("tally_fast", st);
                 e = agnes_launch_tally_fast(&b, MODE, num_cus, st);
             }

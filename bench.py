@@ -38,7 +38,6 @@ BYTES_PER_VOTE = 15            # 14 B canonical SoA in + 1 B code out (BASELINE.
 KERNEL_BYTES_PER_VOTE = {
     "flow": 15,          # instance, value, validator u32 + round, type u8 in; code u8 out
     "tally_fast": 15,
-    "sieve": 15,
     "tally_wide": 15,
     "apply_codes": 2,    # code + round u8 in (+ the message bytes written back)
     "dedup_first": 10,   # C5 DEDUP: instance, validator u32 + round, type u8 in (+ 8 B atomic per key)
@@ -50,7 +49,6 @@ KERNEL_SYMBOLS = {
     "flow": "agnes::flow::flow<PC, SM, R1>",
     "sweep_walk": "agnes::sweep::sweep<PC, SM>",
     "tally_fast": "agnes::fast::tally_fast<...>",
-    "sieve": "agnes::sieve::sieve<MODE, SKIP, PC>",
     "tally_wide": "agnes::tally_kernel<true, ...>",
     "apply_codes": "agnes::apply::apply_codes<RoundSkip>",
 }

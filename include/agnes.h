@@ -191,24 +191,20 @@ typedef struct agnes_state {
                                            agnes_config.reserved (C5: one huge instance split over
                                            waves and GPUs) */
 
-/* Route override, bits 8..10 of agnes_config.flags (diagnostics and the
+/* Route override, bits 8..9 of agnes_config.flags (diagnostics and the
  * route-equivalence tests: every route gives identical codes and States).
  *   AUTO      the engine's choice: the fused flow kernel for REFERENCE without
- *             RoundSkip, the sieve (one pass per round over 512-vote chunks) + apply
- *             pass otherwise, the i64 kernel for instances outside the u32 domain
+ *             RoundSkip, the per-instance kernel + apply pass otherwise, the i64
+ *             kernel for instances outside the u32 domain
  *   INSTANCE  the per-instance u32 kernel with the State machine fused
- *   SPLIT     the sieve (tally_fast where the sieve does not fit), then the
- *             one-instance-per-lane apply pass
- *   WIDE      the i64 kernel for every instance
- *   FAST      the per-instance u32 kernel (one pass per (round, type) key over
- *             256-vote chunks), then the apply pass */
+ *   SPLIT     the per-instance u32 kernel, then the one-instance-per-lane apply pass
+ *   WIDE      the i64 kernel for every instance */
 #define AGNES_ROUTE_SHIFT 8
-#define AGNES_ROUTE_MASK 0x7u
+#define AGNES_ROUTE_MASK 0x3u
 #define AGNES_ROUTE_AUTO 0u
 #define AGNES_ROUTE_INSTANCE 1u
 #define AGNES_ROUTE_SPLIT 2u
 #define AGNES_ROUTE_WIDE 3u
-#define AGNES_ROUTE_FAST 4u
 #define AGNES_FLAG_ROUTE(r) ((uint32_t)(r) << AGNES_ROUTE_SHIFT)
 /* Bits 16..20 of agnes_config.flags: minimum bits the DEDUP / RoundSkip first-vote
  * tables spend on a vote's index inside its instance (0 = just enough for the

@@ -32,7 +32,6 @@ ROUTES = {
     "fused": abi.FLAG_ROUTE(abi.ROUTE_INSTANCE),
     "split": abi.FLAG_ROUTE(abi.ROUTE_SPLIT),
     "wide": abi.FLAG_ROUTE(abi.ROUTE_WIDE),
-    "fast": abi.FLAG_ROUTE(abi.ROUTE_FAST),
 }
 
 
