@@ -8,7 +8,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 NIL = 0xFFFFFFFF
 
 OK, E_INVALID, E_UNSUPPORTED, E_DEVICE, E_NOMEM, E_NODEVICE = 0, -1, -2, -3, -4, -5
@@ -35,6 +35,7 @@ CODE_EVENT_MASK, CODE_SKIP, CODE_MSG_SHIFT = 0x07, 0x08, 4
 MODE_REFERENCE, MODE_DEDUP = 0, 1
 FLAG_ROUND_SKIP, FLAG_STATE_MACHINE, FLAG_DISTINCT_VALUES = 0x1, 0x2, 0x4
 FLAG_ONE_INSTANCE = 0x8  # agnes_tally_carried: segments are slices of one instance (id cfg.reserved)
+FLAG_WEIGHTS_CACHED = 0x10  # agnes_tally_carried: batch.weight = agnes_tally_partials' weights (validated as without)
 # route override (agnes.h AGNES_ROUTE_*): diagnostics / route-equivalence tests
 ROUTE_SHIFT, ROUTE_AUTO, ROUTE_INSTANCE, ROUTE_SPLIT, ROUTE_WIDE = 8, 0, 1, 2, 3
 EPOCH_BITS_SHIFT = 16

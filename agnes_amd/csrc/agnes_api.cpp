@@ -112,7 +112,8 @@ agnes_set_info set_info(const int64_t* pw, uint32_t n_vals, int64_t total) {
 bool cfg_ok(const agnes_config* cfg) {
     return cfg && cfg->max_rounds >= 1 && cfg->max_rounds <= 256 && cfg->mode <= AGNES_MODE_DEDUP &&
            (cfg->flags & ~(AGNES_FLAG_ROUND_SKIP | AGNES_FLAG_STATE_MACHINE | AGNES_FLAG_DISTINCT_VALUES |
-                           AGNES_FLAG_ONE_INSTANCE | (AGNES_ROUTE_MASK << AGNES_ROUTE_SHIFT) |
+                           AGNES_FLAG_ONE_INSTANCE | AGNES_FLAG_WEIGHTS_CACHED |
+                           (AGNES_ROUTE_MASK << AGNES_ROUTE_SHIFT) |
                            AGNES_FLAG_EPOCH_BITS(0x1F))) == 0;
 }
 
@@ -362,14 +363,15 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
 
 int agnes_tally(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint8_t* codes,
                 agnes_state* states, void* stream) {
-    if (!c || !cfg || (cfg->flags & AGNES_FLAG_ONE_INSTANCE)) return AGNES_E_INVALID; /* needs counts */
+    if (!c || !cfg || (cfg->flags & (AGNES_FLAG_ONE_INSTANCE | AGNES_FLAG_WEIGHTS_CACHED)))
+        return AGNES_E_INVALID; /* agnes_tally_carried only */
     return tally_impl(c, cfg, b, codes, nullptr, states, nullptr, c->d_sets, c->n_sets, c->all_fast,
                       (hipStream_t)stream);
 }
 
 int agnes_tally_states(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint8_t* codes,
                        const agnes_state* states_in, agnes_state* states_out, void* stream) {
-    if (!c || !cfg || (cfg->flags & AGNES_FLAG_ONE_INSTANCE)) return AGNES_E_INVALID;
+    if (!c || !cfg || (cfg->flags & (AGNES_FLAG_ONE_INSTANCE | AGNES_FLAG_WEIGHTS_CACHED))) return AGNES_E_INVALID;
     return tally_impl(c, cfg, b, codes, states_in, states_out, nullptr, c->d_sets, c->n_sets, c->all_fast,
                       (hipStream_t)stream);
 }
@@ -384,6 +386,24 @@ int agnes_tally_carried(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_
         return AGNES_E_UNSUPPORTED;
     return tally_impl(c, cfg, b, codes, nullptr, nullptr, reinterpret_cast<agnes_carry_rec*>(counts), c->d_sets,
                       c->n_sets, c->all_fast, (hipStream_t)stream);
+}
+
+int agnes_tally_partials(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, agnes_vote_count* counts,
+                         int64_t* weights, void* stream) {
+    if (!c || !cfg_ok(cfg) || !b || !b->offsets || (b->n_instances && !counts)) return AGNES_E_INVALID;
+    if (b->n_votes && (!b->instance || !b->round || !b->type || !b->value || !b->validator))
+        return AGNES_E_INVALID;
+    if (cfg->mode != AGNES_MODE_REFERENCE || (cfg->flags & (AGNES_FLAG_ROUND_SKIP | AGNES_FLAG_STATE_MACHINE)))
+        return AGNES_E_UNSUPPORTED;
+    if (b->n_votes >= 0xFFFFFFFFull || cfg->max_rounds > 1024u) /* LDS: 48 B per round */
+        return AGNES_E_UNSUPPORTED;
+    if ((uintptr_t)weights & 7u) return AGNES_E_INVALID;
+    AGNES_TRY(hipSetDevice(c->device));
+    const hipStream_t st = (hipStream_t)stream;
+    AGNES_ORDER(c, st);
+    return status_of(agnes_launch_partials(b, c->d_power, c->d_power32, c->d_sets, c->n_sets, c->n_vals, cfg->max_rounds,
+                                           (cfg->flags & AGNES_FLAG_ONE_INSTANCE) ? 1u : 0u, cfg->reserved,
+                                           reinterpret_cast<agnes_carry_rec*>(counts), weights, st));
 }
 
 int agnes_last_error_count(agnes_ctx* c, uint64_t* out) {

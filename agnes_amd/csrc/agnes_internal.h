@@ -137,6 +137,10 @@ hipError_t agnes_launch_fold(agnes_vote_count* counts, uint32_t n_slices, uint32
                              const agnes_vote_count* carry, agnes_vote_count* totals, uint32_t flags,
                              hipStream_t stream);
 /* the event stream (agnes_events.hip): out == nullptr -> count pass + scan, else emit */
+hipError_t agnes_launch_partials(const agnes_vote_batch* vb, const int64_t* power, const uint32_t* power32,
+                                 const agnes_set_info* sets, uint32_t n_sets, uint32_t n_vals,
+                                 uint32_t max_rounds, uint32_t one_inst, uint32_t one_id, agnes_carry_rec* counts,
+                                 int64_t* weights, hipStream_t st);
 hipError_t agnes_launch_events(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds,
                                uint64_t* offs, agnes_vote_event* out, uint64_t* scratch, hipStream_t stream);
 hipError_t agnes_launch_edges(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds,

@@ -490,11 +490,13 @@ __device__ __forceinline__ void prep_chunk(const agnes_tally_args& a, const Inst
     const uint32_t nv = a.n_vals;
     const agnes_vote_batch& vb = a.vb;
     const bool has_w = WIDE && vb.weight != nullptr; /* caller weights run on the i64 kernels */
-    const bool need_val = !has_w || MODE == AGNES_MODE_DEDUP || SKIP;
+    /* AGNES_FLAG_WEIGHTS_CACHED: the weights agnes_tally_partials gathered, validated as without them */
+    const bool cached = has_w && (a.flags & AGNES_FLAG_WEIGHTS_CACHED);
+    const bool need_val = !has_w || cached || MODE == AGNES_MODE_DEDUP || SKIP;
     /* uniform part of the checks: the validator must index the set's row when the
      * vote needs it; the weight needs a valid set unless the caller supplied it */
     const bool set_ok = in_.set_ok;
-    const bool vote_ok_u = has_w || set_ok;
+    const bool vote_ok_u = (has_w && !cached) || set_ok;
     const bool table = !has_w && (uint64_t)a.n_sets * nv > 0u;
     /* the instance's votes in this chunk: positions [lo, hi) */
     const uint32_t lo = c < in_.beg ? (uint32_t)(in_.beg - c) : 0u;

@@ -206,7 +206,7 @@ def fold_counts(w: torch.Tensor, lab: torch.Tensor):
 
 
 def tally_one_instance(tally_carried, n_votes: int, cfg: abi.Config, n_segments: int, device,
-                       inst_id: int = 0, group=None, prior=None, offsets=None, fold=None):
+                       inst_id: int = 0, group=None, prior=None, offsets=None, fold=None, partials=None):
     """C5 driver.  This rank holds a contiguous slice (n_votes votes) of ONE
     instance's stream; ranks hold consecutive slices in rank order.  The slice is
     cut into n_segments segments (one wave each) and tallied twice:
@@ -223,6 +223,9 @@ def tally_one_instance(tally_carried, n_votes: int, cfg: abi.Config, n_segments:
     capture the whole step in a HIP graph).
     fold: Engine.fold_counts (agnes_fold_counts, HIP): the folds run as one kernel
     each on the device; None: torch ops (CPU tensors in the tests).
+    partials(cfg, offsets, counts) (with fold): pass A as one reduction
+    (agnes_tally_partials, which also keeps the votes' weights); pass B's cfg then
+    carries FLAG_WEIGHTS_CACHED and tally_carried must hand it those weights.
     Returns the instance's (w, label) after every rank's votes."""
     K = 2 * cfg.max_rounds
     if offsets is None:
@@ -233,7 +236,7 @@ def tally_one_instance(tally_carried, n_votes: int, cfg: abi.Config, n_segments:
         S = off.numel() - 1
     one = abi.Config(cfg.mode, cfg.flags | abi.FLAG_ONE_INSTANCE, cfg.max_rounds, inst_id)
     if fold is not None:
-        return _tally_one_instance_hip(tally_carried, fold, one, off, S, K, device, group, prior)
+        return _tally_one_instance_hip(tally_carried, fold, one, off, S, K, device, group, prior, partials)
     counts = torch.zeros((S, K, 3), dtype=torch.int64, device=device)
     counts[..., 2] = NIL
     tally_carried(one, off, counts)                                    # pass A
@@ -261,12 +264,17 @@ def tally_one_instance(tally_carried, n_votes: int, cfg: abi.Config, n_segments:
     return fin_w, torch.where(fin_lab == NIL, torch.zeros_like(fin_lab), fin_lab)
 
 
-def _tally_one_instance_hip(tally_carried, fold, one, off, S, K, device, group, prior):
+def _tally_one_instance_hip(tally_carried, fold, one, off, S, K, device, group, prior, partials=None):
     """tally_one_instance with the folds as agnes_fold_counts launches (no torch
     kernels between the two carried passes on one GPU)."""
     counts = torch.empty((S, K, 3), dtype=torch.int64, device=device)
-    fold(counts, flags=abi.FOLD_RESET)                                 # RoundVotes::new per slice
-    tally_carried(one, off, counts)                                    # pass A
+    one_b = one
+    if partials is not None:
+        partials(one, off, counts)                                     # pass A: one reduction
+        one_b = abi.Config(one.mode, one.flags | abi.FLAG_WEIGHTS_CACHED, one.max_rounds, one.reserved)
+    else:
+        fold(counts, flags=abi.FOLD_RESET)                             # RoundVotes::new per slice
+        tally_carried(one, off, counts)                                # pass A
     pr = None
     if prior is not None:
         pw, pl = prior
@@ -286,7 +294,7 @@ def _tally_one_instance_hip(tally_carried, fold, one, off, S, K, device, group, 
     else:
         fold(counts, carry=pr, totals=fin,
              flags=abi.FOLD_APPLY | abi.FOLD_ZERO_LABELS | abi.FOLD_CARRY_ZERO_NONE | abi.FOLD_TOTAL_ZERO_LABELS)
-    tally_carried(one, off, counts)                                    # pass B
+    tally_carried(one_b, off, counts)                                  # pass B
     return fin[:, :2], fin[:, 2]
 
 
@@ -326,7 +334,7 @@ def one_instance_states(sm_scan, sm_apply, sm_finish, marks: torch.Tensor, group
 
 def tally_one_instance_dedup(tally_carried, dedup_first, dedup_mask, dedup_reject, n_votes: int,
                              n_vals: int, cfg: abi.Config, n_segments: int, device, base: int = 0,
-                             group=None, offsets=None, fold=None):
+                             group=None, offsets=None, fold=None, partials=None):
     """C5 in DEDUP mode ("DEDUP mode adds an all-reduce(min) on
     first_index").  A vote's slice cannot see whether an earlier slice (or rank)
     already counted its (round, type, validator), so the first vote of every key is
@@ -355,7 +363,7 @@ def tally_one_instance_dedup(tally_carried, dedup_first, dedup_mask, dedup_rejec
     dedup_mask(base, first)
     ref = abi.Config(abi.MODE_REFERENCE, cfg.flags, cfg.max_rounds, cfg.reserved)
     out = tally_one_instance(tally_carried, n_votes, ref, n_segments, device, cfg.reserved, group,
-                             offsets=offsets, fold=fold)
+                             offsets=offsets, fold=fold, partials=partials)
     dedup_reject()
     return out
 

@@ -156,6 +156,20 @@ class Engine:
         check(self.lib.agnes_tally_carried(self.ctx, C.byref(cfg), C.byref(b), _ptr(codes), _ptr(counts),
                                            _stream_handle(stream)), "agnes_tally_carried")
 
+    def tally_partials(self, cfg: abi.Config, batch: DeviceBatch, counts: torch.Tensor,
+                       weights: Optional[torch.Tensor] = None, stream=None):
+        """agnes_tally_partials (C5 pass A as one reduction): counts := int64 [n_instances,
+        2 * max_rounds, 3] (each segment's VoteCounts from RoundVotes::new, label NIL when
+        none); weights (int64 [n_votes] or None) := each vote's weight, 0 when not valid."""
+        if (counts.dtype != torch.int64 or not counts.is_contiguous()
+                or counts.numel() < batch.n_instances * 2 * cfg.max_rounds * 3):
+            raise ValueError("counts must be a contiguous int64 [n_instances, 2R, 3] tensor")
+        if weights is not None and (weights.dtype != torch.int64 or weights.numel() < batch.n_votes):
+            raise ValueError("weights must be an int64 tensor of n_votes")
+        b = batch.c()
+        check(self.lib.agnes_tally_partials(self.ctx, C.byref(cfg), C.byref(b), _ptr(counts), _ptr(weights),
+                                            _stream_handle(stream)), "agnes_tally_partials")
+
     def fold_counts(self, counts: torch.Tensor, carry: Optional[torch.Tensor] = None,
                     totals: Optional[torch.Tensor] = None, flags: int = 0, stream=None):
         """agnes_fold_counts on counts = contiguous int64 [S, K, 3] (agnes_vote_count

@@ -64,6 +64,7 @@ def load():
         "agnes_tally": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P], C.c_int),
         "agnes_tally_states": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P], C.c_int),
         "agnes_tally_carried": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P], C.c_int),
+        "agnes_tally_partials": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P], C.c_int),
         "agnes_last_error_count": ([P, C.POINTER(C.c_uint64)], C.c_int),
         "agnes_lds_bytes_per_wave": ([C.POINTER(abi.Config), C.c_uint32], C.c_int64),
         "agnes_apply_events": ([P, P, C.c_uint32, P, P, P, C.c_uint32, P], C.c_int),

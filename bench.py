@@ -42,7 +42,10 @@ KERNEL_BYTES_PER_VOTE = {
     "apply_codes": 2,    # code + round u8 in (+ the message bytes written back)
     "dedup_first": 10,   # C5 DEDUP: instance, validator u32 + round, type u8 in (+ 8 B atomic per key)
     "dedup_mask": 11,    # the same in, the masked type u8 out
+    "partials": 30,      # C5 pass A: the 14 B in + the gathered i64 weight + the weight column out
 }
+# C5 pass B reads the weight column pass A wrote (AGNES_FLAG_WEIGHTS_CACHED) on top of the 15 B
+C5_PASS_B_BYTES_PER_VOTE = 23
 KERNEL_SYMBOLS = {
     # template parameters: PC (power table in LDS), SM (State machine), R1 (one round);
     # c2 runs flow<true, true, true>, c3 flow<false, true, false> (rocprofv3 names them)
@@ -51,6 +54,7 @@ KERNEL_SYMBOLS = {
     "tally_fast": "agnes::fast::tally_fast<...>",
     "tally_wide": "agnes::tally_kernel<true, ...>",
     "apply_codes": "agnes::apply::apply_codes<RoundSkip>",
+    "partials": "agnes::partials::partials_kernel",
 }
 
 WORKLOADS = {
@@ -448,8 +452,16 @@ def bench_one_instance(args, w, eng, rank, world):
     segs = max(1, min(args.segments or w["segments"], max(1, (hi - lo) // 4)))
     off = torch.from_numpy(adist.segment_offsets(hi - lo, segs).view(np.int64)).to(eng.device)
 
+    # pass A as one reduction (agnes_tally_partials), which keeps the votes' weights
+    # for pass B (AGNES_FLAG_WEIGHTS_CACHED): the power table is gathered once
+    wcol = torch.empty(max(hi - lo, 1), dtype=torch.int64, device=eng.device)
+
     def tc(one, o, counts):  # on the current stream: a graph capture's while capturing
-        eng.tally_carried(one, dataclasses.replace(batch, offsets=o), codes, counts)
+        cached = one.flags & abi.FLAG_WEIGHTS_CACHED
+        eng.tally_carried(one, dataclasses.replace(batch, offsets=o, weight=wcol if cached else None), codes, counts)
+
+    def pa(one, o, counts):
+        eng.tally_partials(one, dataclasses.replace(batch, offsets=o), counts, wcol)
 
     def step():
         if dedup:
@@ -457,9 +469,9 @@ def bench_one_instance(args, w, eng, rank, world):
                 tc, lambda base, f: eng.dedup_first(cfg, src, base, f),
                 lambda base, f: eng.dedup_mask(cfg, src, base, f, tmask),
                 lambda: eng.dedup_reject(tmask, codes, hi - lo), hi - lo, p.n_vals, cfg, segs,
-                eng.device, base=lo, offsets=off, fold=eng.fold_counts)
+                eng.device, base=lo, offsets=off, fold=eng.fold_counts, partials=pa)
         return adist.tally_one_instance(tc, hi - lo, cfg, segs, eng.device, 0, None, offsets=off,
-                                        fold=eng.fold_counts)
+                                        fold=eng.fold_counts, partials=pa)
 
     for _ in range(args.warmup):
         step()
@@ -504,15 +516,17 @@ def bench_one_instance(args, w, eng, rank, world):
         kernels = {}
         for name, (launches, total) in ktimes.items():
             avg = total / max(launches, 1)
-            ab = KERNEL_BYTES_PER_VOTE.get(name, 0) * (hi - lo)
+            bpv = C5_PASS_B_BYTES_PER_VOTE if name == "tally_wide" else KERNEL_BYTES_PER_VOTE.get(name, 0)
+            ab = bpv * (hi - lo)
             kernels[name] = {"launches": launches, "avg_ms": avg, "algorithmic_bytes": ab,
                              "GBps": ab / (avg * 1e-3) / 1e9 if ab and avg > 0 else None}
         # the roofline's kernel: the dominant one among those that stream the votes
         # (the slice fold and the exchange work on per-slice records)
-        streaming = [k for k in kernels if KERNEL_BYTES_PER_VOTE.get(k)]
+        streaming = [k for k in kernels if kernels[k]["algorithmic_bytes"]]
         dom = max(streaming, key=lambda k: kernels[k]["avg_ms"] * kernels[k]["launches"])
         dom_ms = kernels[dom]["avg_ms"]
-        achieved = KERNEL_BYTES_PER_VOTE[dom] * (hi - lo) / (dom_ms * 1e-3) / 1e9
+        dom_bpv = kernels[dom]["algorithmic_bytes"] // max(hi - lo, 1)
+        achieved = kernels[dom]["algorithmic_bytes"] / (dom_ms * 1e-3) / 1e9
         out = {
             "metric": "votes_tallied_per_sec", "value": n * args.steps / elapsed, "unit": "votes/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -529,9 +543,10 @@ def bench_one_instance(args, w, eng, rank, world):
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None, "traffic_source": None,
                          "kernel": KERNEL_SYMBOLS.get(dom, dom), "kernel_avg_ms": dom_ms,
-                         "bytes_per_vote": KERNEL_BYTES_PER_VOTE[dom],
-                         "algorithmic_bytes": KERNEL_BYTES_PER_VOTE[dom] * (hi - lo),
-                         "note": "two passes per step (partials, exact rescan); latency-bound at 2e6 votes"},
+                         "bytes_per_vote": dom_bpv,
+                         "algorithmic_bytes": kernels[dom]["algorithmic_bytes"],
+                         "note": "pass A: one reduction (agnes_tally_partials, keeps the weights); "
+                                 "pass B: the carried tally over the cached weights; latency-bound at 2e6 votes"},
             "kernels": kernels,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AGNES_ABI_VERSION 5u
+#define AGNES_ABI_VERSION 6u
 
 /* ---------------------------------------------------------------------------
  * Status codes (reference never fails, state_machine.rs:212; these report
@@ -190,6 +190,10 @@ typedef struct agnes_state {
                                            slices of ONE instance whose votes carry instance id
                                            agnes_config.reserved (C5: one huge instance split over
                                            waves and GPUs) */
+#define AGNES_FLAG_WEIGHTS_CACHED 0x10u /* agnes_tally_carried only: batch->weight holds the weights
+                                           agnes_tally_partials wrote for this batch; the votes are
+                                           validated (set, validator index) as without it and the
+                                           power table is not gathered again (C5 pass B) */
 
 /* Route override, bits 8..9 of agnes_config.flags (diagnostics and the
  * route-equivalence tests: every route gives identical codes and States).
@@ -336,6 +340,19 @@ typedef struct agnes_vote_count {
  * REFERENCE mode without RoundSkip or State machine; runs the i64 kernel. */
 int agnes_tally_carried(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
                         uint8_t* codes, agnes_vote_count* counts, void* stream);
+
+/* Pass A of the split-instance protocol as one reduction (C5, agnes_amd/dist.py
+ * tally_one_instance): counts (DEVICE, [n_instances][2 * max_rounds]) := each
+ * segment's VoteCounts from RoundVotes::new (round_votes.rs:48-56: the weights of
+ * its valid votes summed per side, value = its last non-nil value, AGNES_NIL when
+ * none): what AGNES_FOLD_RESET + agnes_tally_carried leave in counts, without the
+ * thresholds and the codes.  weights (DEVICE, i64 [n_votes], or NULL): each vote's
+ * weight, 0 for a vote that is not valid; pass B then runs agnes_tally_carried with
+ * batch->weight = weights and AGNES_FLAG_WEIGHTS_CACHED.  The configurations, the
+ * validity rules and AGNES_FLAG_ONE_INSTANCE are agnes_tally_carried's; the batch's
+ * columns need no alignment; n_votes < 2^32 - 1.  Asynchronous on `stream`. */
+int agnes_tally_partials(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
+                         agnes_vote_count* counts, int64_t* weights, void* stream);
 
 /* The fold of one instance's slices (C5, agnes_amd/dist.py tally_one_instance):
  * counts (DEVICE, [n_slices][keys]) hold each slice's partial VoteCounts (value

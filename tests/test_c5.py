@@ -289,7 +289,7 @@ def test_gpu_split_instance(eng, segments, n_vals, R, nil, hip_fold):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("S,K", [(1, 2), (7, 4), (1000, 2), (5000, 8)])
+@pytest.mark.parametrize("S,K", [(1, 2), (7, 4), (1000, 2), (5000, 8), (8192, 2), (9000, 3)])
 def test_gpu_fold_counts_equals_torch_fold(eng, S, K):
     """agnes_fold_counts (reset / apply / totals, carry, label conventions) against
     dist.fold_counts on random partials (wrapping weights, sparse labels)"""
@@ -301,6 +301,7 @@ def test_gpu_fold_counts_equals_torch_fold(eng, S, K):
     counts = torch.from_numpy(np.concatenate([w, lab[..., None]], axis=-1)).to(eng.device).contiguous()
     cr = torch.from_numpy(carry).to(eng.device).contiguous()
     tot = torch.empty((K, 3), dtype=torch.int64, device=eng.device)
+    orig = counts.clone()
     eng.fold_counts(counts, carry=cr, totals=tot,
                     flags=abi.FOLD_APPLY | abi.FOLD_ZERO_LABELS | abi.FOLD_CARRY_ZERO_NONE | abi.FOLD_TOTAL_ZERO_LABELS)
     # torch: prior (label 0 = none) as the first "slice"
@@ -315,6 +316,11 @@ def test_gpu_fold_counts_equals_torch_fold(eng, S, K):
     assert np.array_equal(got[..., 2], ex_lab[1:].numpy())
     tg = tot.cpu().numpy()
     assert np.array_equal(tg[:, :2], t_w.numpy()) and np.array_equal(tg[:, 2], t_lab.numpy())
+    # totals only (no APPLY): the slices stay as they are
+    before = orig.clone()
+    tot2 = torch.empty((K, 3), dtype=torch.int64, device=eng.device)
+    eng.fold_counts(orig, carry=cr, totals=tot2, flags=abi.FOLD_CARRY_ZERO_NONE | abi.FOLD_TOTAL_ZERO_LABELS)
+    assert torch.equal(orig, before) and torch.equal(tot2, tot)
     eng.fold_counts(counts, flags=abi.FOLD_RESET)
     r = counts.cpu().numpy()
     assert (r[..., :2] == 0).all() and (r[..., 2] == ad.NIL).all()
