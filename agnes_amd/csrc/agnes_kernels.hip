@@ -815,6 +815,8 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
     const uint64_t NV = vb.n_votes;
     const uint32_t Wn = gridDim.x * AGNES_WAVES_PER_BLOCK;
     const uint32_t gw = blockIdx.x * AGNES_WAVES_PER_BLOCK + wave;
+    /* the deferred list empty (every instance fit the u32 kernels): leave before staging */
+    if (LIST && *(volatile const uint32_t*)a.list_count == 0u) return;
 
     /* block-shared set cache: q2[ns] q1[ns] mp[ns] (maxpow | fast<<31) tot[ns] (u64) */
     const uint32_t ns = a.n_sets;

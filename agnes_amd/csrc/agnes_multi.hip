@@ -305,10 +305,10 @@ struct OneBufs {
     uint64_t *segoff = nullptr, *first = nullptr, *off1 = nullptr;
     agnes_vote_count *counts = nullptr, *mine = nullptr, *ranks = nullptr, *fin = nullptr;
     agnes_state* state = nullptr;
-    int64_t* marks = nullptr;
+    int64_t *marks = nullptr, *weights = nullptr;
     void release() {
         void* ps[] = {inst, value, val, round, type, tmask, codes, segoff, first, off1,
-                      counts, mine, ranks, fin, state, marks};
+                      counts, mine, ranks, fin, state, marks, weights};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         *this = OneBufs{};
@@ -359,6 +359,7 @@ int run_one(agnes_multi* m, uint32_t d, const agnes_config* cfg, const agnes_vot
     OTRY(hipMalloc(&b.round, v));
     OTRY(hipMalloc(&b.type, v));
     OTRY(hipMalloc(&b.codes, v));
+    OTRY(hipMalloc(&b.weights, 8 * v));
     OTRY(hipMalloc(&b.segoff, 8 * ((uint64_t)S + 1u)));
     OTRY(hipMalloc(&b.off1, 16));
     OTRY(hipMalloc(&b.counts, sizeof(agnes_vote_count) * (uint64_t)S * K));
@@ -421,9 +422,9 @@ int run_one(agnes_multi* m, uint32_t d, const agnes_config* cfg, const agnes_vot
         OCALL(agnes_dedup_mask(dv.ctx, &dcfg, &sl, lo, b.first, b.tmask, dv.st));
         seg.type = b.tmask;
     }
-    /* pass A: every segment from RoundVotes::new -> its partial; this slice's total */
-    OCALL(agnes_fold_counts(dv.ctx, b.counts, S, K, nullptr, nullptr, AGNES_FOLD_RESET, dv.st));
-    OCALL(agnes_tally_carried(dv.ctx, &one, &seg, b.codes, b.counts, dv.st));
+    /* pass A: every segment from RoundVotes::new -> its partial (one reduction, which
+     * keeps the votes' weights for pass B); this slice's total */
+    OCALL(agnes_tally_partials(dv.ctx, &one, &seg, b.counts, b.weights, dv.st));
     OCALL(agnes_fold_counts(dv.ctx, b.counts, S, K, nullptr, b.mine, 0u, dv.st));
     OTRY(hipStreamSynchronize(dv.st));
     /* the exchange: every slice's total to every device */
@@ -434,7 +435,12 @@ int run_one(agnes_multi* m, uint32_t d, const agnes_config* cfg, const agnes_vot
                             AGNES_FOLD_APPLY | AGNES_FOLD_CARRY_ZERO_NONE | AGNES_FOLD_TOTAL_ZERO_LABELS, dv.st));
     OCALL(agnes_fold_counts(dv.ctx, b.counts, S, K, b.ranks + (uint64_t)d * K, nullptr,
                             AGNES_FOLD_APPLY | AGNES_FOLD_ZERO_LABELS, dv.st));
-    OCALL(agnes_tally_carried(dv.ctx, &one, &seg, b.codes, b.counts, dv.st));
+    /* pass B: the exact rescan from the carry-ins, over the cached weights */
+    agnes_config oneb = one;
+    oneb.flags |= AGNES_FLAG_WEIGHTS_CACHED;
+    agnes_vote_batch segb = seg;
+    segb.weight = b.weights;
+    OCALL(agnes_tally_carried(dv.ctx, &oneb, &segb, b.codes, b.counts, dv.st));
     if (dedup) OCALL(agnes_dedup_reject(dv.ctx, b.tmask, nv, b.codes, dv.st));
     if (sm) { /* P1 / C: MIN over slices; valid, decision round: MAX; the State */
         const int64_t init[4] = {INT64_MAX, INT64_MAX, 0, 0};

@@ -133,6 +133,8 @@ __global__ __launch_bounds__(256) void sweep(agnes_tally_args a, uint32_t lds_pe
     const uint32_t R = a.max_rounds, nv = a.n_vals, ns = a.n_sets, n = a.vb.n_instances;
     const uint64_t NV = a.vb.n_votes;
     const uint32_t p0 = 4u * lane, o16 = 16u * lane;
+    /* nothing walked (every batch streamed): leave before staging anything */
+    if (*(volatile const uint32_t*)(a.list_count + AGNES_WALK_COUNT) == 0u) return;
 
     /* block-shared u32 power table (launcher-staged only when it costs no occupancy) */
     if (PC) {
