@@ -7,9 +7,8 @@
  * instance's stream is cut into slices, a vote's slice cannot tell whether an
  * earlier slice saw its key, so the split path finds the first vote of every key
  * up front:
- *   1. agnes_dedup_first — every valid vote j of the slice lowers first[key] to
- *      base + j (its index in the whole stream): a plain seeding pass, then
- *      atomicMin only for the votes still below their entry;
+ *   1. agnes_dedup_first — every valid vote j of the slice atomically lowers
+ *      first[key] to base + j (its index in the whole stream);
  *   2. the caller all-reduces `first` with MIN over the ranks (agnes_amd/dist.py);
  *   3. agnes_dedup_mask — a copy of the type column in which every valid vote that
  *      is not its key's first carries AGNES_TYPE_MASKED: the carried tally (REFERENCE
@@ -50,27 +49,11 @@ __device__ __forceinline__ bool valid_key(const DedupArgs& a, uint64_t j, uint64
     return ok;
 }
 
-/* first[key] = min(first[key], base + j) over the valid votes, mostly without
- * atomics (a device-scope atomicMin on a random line costs ~4x a plain gather):
- *   seed  a vote whose index is below the current entry stores it, plainly; racing
- *         votes of one key leave one of their indices, every one below the old entry;
- *   fix   a vote whose index is still below the entry lowers it with atomicMin — only
- *         duplicates that lost the race in the wrong order (a few % of the votes).
- * After both, every entry is the minimum of its old value and its votes' indices. */
-__global__ __launch_bounds__(256) void first_seed(DedupArgs a, unsigned long long* first) {
+__global__ __launch_bounds__(256) void first_kernel(DedupArgs a, unsigned long long* first) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < a.n_votes; j += stride) {
         uint64_t key;
-        if (valid_key(a, j, key) && a.base + j < first[key]) first[key] = a.base + j;
-    }
-}
-
-__global__ __launch_bounds__(256) void first_fix(DedupArgs a, unsigned long long* first) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < a.n_votes; j += stride) {
-        uint64_t key;
-        if (valid_key(a, j, key) && a.base + j < __builtin_nontemporal_load(first + key))
-            atomicMin(first + key, (unsigned long long)(a.base + j));
+        if (valid_key(a, j, key)) atomicMin(first + key, (unsigned long long)(a.base + j));
     }
 }
 
@@ -117,8 +100,7 @@ hipError_t agnes_launch_dedup(const agnes_vote_batch* vb, uint32_t inst_id, uint
     unsigned long long* f = reinterpret_cast<unsigned long long*>(first);
     if (!type_out) {
         AgnesKt kt("dedup_first", st);
-        hipLaunchKernelGGL(first_seed, dedup_grid(vb->n_votes), dim3(256), 0, st, a, f);
-        hipLaunchKernelGGL(first_fix, dedup_grid(vb->n_votes), dim3(256), 0, st, a, f);
+        hipLaunchKernelGGL(first_kernel, dedup_grid(vb->n_votes), dim3(256), 0, st, a, f);
     } else {
         AgnesKt kt("dedup_mask", st);
         hipLaunchKernelGGL(mask_kernel, dedup_grid(vb->n_votes), dim3(256), 0, st, a, f, type_out);
