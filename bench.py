@@ -217,6 +217,15 @@ def edge_summary(eng, cfg, batch, codes, reps: int = 5):
     return res
 
 
+def with_traffic(res: dict, traffic: dict) -> dict:
+    """Per-launch HBM bytes (the committed PMC passes) next to each timed kernel."""
+    for name, rec in res.items():
+        if isinstance(rec, dict) and "avg_ms" in rec:
+            t = traffic.get(name)
+            rec["traffic"] = t.get("traffic_bytes") if t else None
+    return res
+
+
 def event_stream(eng, cfg, batch, codes, reps: int = 3):
     """The stream-compacted event output (agnes_event_offsets + agnes_events: every
     Some(Event) with its payload) of the last step's codes, timed OUTSIDE the
@@ -352,6 +361,8 @@ def main():
         ms_per_step = elapsed * 1e3 / args.steps
         value = total_votes_step * args.steps / elapsed
         traffic = measured_traffic(args.config)
+        with_traffic(events, traffic)
+        with_traffic(edges, traffic)
         # per-kernel: launches, average ms, algorithmic bytes per launch
         kernels = {}
         for name, (launches, total) in ktimes.items():
@@ -527,6 +538,9 @@ def bench_one_instance(args, w, eng, rank, world):
         dom_ms = kernels[dom]["avg_ms"]
         dom_bpv = kernels[dom]["algorithmic_bytes"] // max(hi - lo, 1)
         achieved = kernels[dom]["algorithmic_bytes"] / (dom_ms * 1e-3) / 1e9
+        traffic = measured_traffic(args.config) if world == 1 else {}
+        with_traffic(kernels, traffic)
+        td = traffic.get(dom)
         out = {
             "metric": "votes_tallied_per_sec", "value": n * args.steps / elapsed, "unit": "votes/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -541,7 +555,8 @@ def bench_one_instance(args, w, eng, rank, world):
                                       + "one all_gather per step)",
                        "hip_graph": graph},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "traffic_source": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": td.get("traffic_bytes") if td else None,
+                         "traffic_source": td.get("sources") if td else None,
                          "kernel": KERNEL_SYMBOLS.get(dom, dom), "kernel_avg_ms": dom_ms,
                          "bytes_per_vote": dom_bpv,
                          "algorithmic_bytes": kernels[dom]["algorithmic_bytes"],

@@ -19,18 +19,20 @@ import sys
 # engine kernel name (agnes_kernel_times) -> regex on the demangled symbol
 KERNELS = {
     "flow": r"agnes::flow::flow<",
-    "sweep_walk": r"agnes::sweep::sweep<\w+, \w+, true>",
-    "sweep": r"agnes::sweep::sweep<\w+, \w+, false>",
+    "sweep_walk": r"agnes::sweep::sweep<",
     "tally_fast": r"agnes::fast::tally_fast<",
     "apply_codes": r"agnes::apply::apply_codes<",
     "tally_list": r"agnes::tally_kernel<true, \w+, \w+, \w+, true,",
     "tally_wide": r"agnes::tally_kernel<true, \w+, \w+, \w+, false,",
-    "fold": r"agnes::fold::fold_kernel",
+    "partials": r"agnes::partials::partials_kernel",
+    "fold": r"agnes::fold::fold_",
     "dedup_first": r"agnes::dedup::first_kernel",
     "dedup_mask": r"agnes::dedup::mask_kernel",
     "dedup_reject": r"agnes::dedup::reject_kernel",
-    "edge_walk": r"agnes::edges::edge_walk",
-    "event_walk": r"agnes::events::event_walk",
+    "edge_count": r"agnes::edges::edge_walk<false,",
+    "edge_emit": r"agnes::edges::edge_walk<true,",
+    "event_count": r"agnes::events::event_walk<false,",
+    "event_emit": r"agnes::events::(event_emit_stream|event_emit_wave|event_walk<true,)",
 }
 
 
