@@ -55,6 +55,8 @@ KERNEL_SYMBOLS = {
     "tally_wide": "agnes::tally_kernel<true, ...>",
     "apply_codes": "agnes::apply::apply_codes<RoundSkip>",
     "partials": "agnes::partials::partials_kernel",
+    "dedup_first": "agnes::dedup::first_kernel",
+    "dedup_mask": "agnes::dedup::mask_kernel",
 }
 
 WORKLOADS = {
