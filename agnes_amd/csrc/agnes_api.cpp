@@ -286,7 +286,7 @@ int64_t agnes_lds_bytes_per_wave(const agnes_config* cfg, uint32_t n_vals) {
 static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b,
                       uint8_t* codes, const agnes_state* states_in, agnes_state* states,
                       agnes_carry_rec* carry, const agnes_set_info* sets, uint32_t n_sets, bool sets_fast,
-                      hipStream_t st) {
+                      hipStream_t st, uint64_t* ev_counts = nullptr, bool* counted = nullptr) {
     if (!c || !cfg_ok(cfg) || !b || !b->offsets) return AGNES_E_INVALID;
     if (b->n_votes && (!codes || !b->instance || !b->round || !b->type || !b->value ||
                        !b->validator))
@@ -357,6 +357,14 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
         a.epoch_shift = lb;
     } else {
         a.epoch_shift = 31;
+    }
+    /* agnes_tally_events: the flow route counts each instance's event records as it goes */
+    if (ev_counts) {
+        const uint32_t route = (cfg->flags >> AGNES_ROUTE_SHIFT) & AGNES_ROUTE_MASK;
+        const bool flow = !wide_all && route == AGNES_ROUTE_AUTO && cfg->mode == AGNES_MODE_REFERENCE &&
+                          !(cfg->flags & AGNES_FLAG_ROUND_SKIP) && agnes_flow_counts_events(cfg->flags, cfg->max_rounds);
+        if (flow) a.ev_counts = ev_counts;
+        if (counted) *counted = flow;
     }
     return status_of(agnes_launch_tally(&a, cfg->mode, c->num_cus, wide_all, st));
 }
@@ -615,6 +623,46 @@ int agnes_event_offsets(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_
     }
     return status_of(agnes_launch_events(b, codes, cfg->max_rounds, offsets, nullptr, c->d_scan,
                                          (hipStream_t)stream));
+}
+
+uint64_t agnes_events_capacity(const agnes_config* cfg, const agnes_vote_batch* b) {
+    if (!cfg || !b) return 0;
+    return b->n_votes * ((cfg->flags & AGNES_FLAG_ROUND_SKIP) ? 2u : 1u);
+}
+
+int agnes_tally_events(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint8_t* codes,
+                       const agnes_state* states_in, agnes_state* states_out, uint64_t* offsets,
+                       agnes_vote_event* out, void* stream) {
+    if (!c || !cfg || !b || (cfg->flags & (AGNES_FLAG_ONE_INSTANCE | AGNES_FLAG_WEIGHTS_CACHED))) return AGNES_E_INVALID;
+    if (!offsets || !out || ((uintptr_t)out & 7u)) return AGNES_E_INVALID;
+    if (b->n_votes && (!b->value || ((uintptr_t)b->value & 3u))) return AGNES_E_INVALID;
+    if (cfg_ok(cfg) && cfg->max_rounds > 64u) return AGNES_E_UNSUPPORTED; /* the emit's value slots in LDS */
+    const hipStream_t st = (hipStream_t)stream;
+    bool counted = false;
+    const int rc = tally_impl(c, cfg, b, codes, states_in, states_out, nullptr, c->d_sets, c->n_sets, c->all_fast, st,
+                              offsets + 1, &counted);
+    if (rc != AGNES_OK) return rc;
+    const uint64_t words = agnes_edges_scratch_words(b->n_instances);
+    if (words > c->scan_cap) {
+        AGNES_TRY(hipStreamSynchronize(st));
+        if (c->d_scan) AGNES_TRY(hipFree(c->d_scan));
+        c->d_scan = nullptr;
+        c->scan_cap = 0;
+        AGNES_TRY(hipMalloc(&c->d_scan, words * sizeof(uint64_t)));
+        c->scan_cap = words;
+    }
+    if (counted) {
+        /* the flow kernel counted its batches' records; the walk list's instances here */
+        AGNES_TRY(hipMemsetAsync(offsets, 0, sizeof(uint64_t), st));
+        AGNES_TRY(agnes_launch_event_count_list(b, codes, c->d_list + (size_t)c->list_cap,
+                                                reinterpret_cast<const uint32_t*>(c->d_err + 1) + AGNES_WALK_COUNT,
+                                                offsets, c->num_cus, st));
+        AgnesKt kt("event_scan", st);
+        AGNES_TRY(agnes_launch_offsets_scan(offsets, b->n_instances, c->d_scan, st));
+    } else {
+        AGNES_TRY(agnes_launch_events(b, codes, cfg->max_rounds, offsets, nullptr, c->d_scan, st));
+    }
+    return status_of(agnes_launch_events(b, codes, cfg->max_rounds, offsets, out, nullptr, st));
 }
 
 int agnes_events(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, const uint8_t* codes,

@@ -101,14 +101,51 @@ __device__ __forceinline__ void put(agnes_vote_event* o, uint64_t j, uint32_t i,
     q[2] = make_uint2(round | (kind << 8) | (msg << 16), 0u);
 }
 
+/* the number of records of instance i: one per vote whose code is Some(Event), plus
+ * one per RoundSkip bit, over the votes the tally added (W-byte windows of codes) */
+template <uint32_t W>
+__device__ __forceinline__ uint64_t count_records(const EvArgs& a, uint32_t i) {
+    const uint64_t NV = a.vb.n_votes;
+    uint64_t lo = a.vb.offsets[i], hi = a.vb.offsets[i + 1u];
+    lo = lo < NV ? lo : NV;
+    hi = hi < NV ? hi : NV;
+    uint64_t cnt = 0;
+    for (uint64_t w = lo & ~(uint64_t)(W - 1u); w < hi; w += W) {
+        uint32_t c[W / 4u];
+        load_bytes<W>(a.codes, w, NV, c);
+#pragma unroll
+        for (uint32_t b = 0; b < W; ++b) {
+            const uint64_t j = w + b;
+            const uint32_t cb = (c[b >> 2] >> (8u * (b & 3u))) & 0xFFu, ev = cb & AGNES_CODE_EVENT_MASK;
+            if (j < lo || j >= hi || ev == AGNES_CODE_INVALID || ev == AGNES_CODE_REJECTED) continue;
+            cnt += ((cb >> 3) & 1u) + (ev != AGNES_CODE_NONE ? 1u : 0u);
+        }
+    }
+    return cnt;
+}
+
+/* the counts of the instances a tally's flow kernel handed to its walk list (the
+ * flow kernel counted every other one itself): a grid-stride loop over the list */
+template <uint32_t W>
+__global__ __launch_bounds__(64) void event_count_list(EvArgs a, const uint32_t* walk, const uint32_t* walk_n) {
+    const uint32_t L = *(volatile const uint32_t*)walk_n;
+    for (uint32_t k = blockIdx.x * 64u + threadIdx.x; k < L; k += gridDim.x * 64u) {
+        const uint32_t i = walk[k];
+        a.offs[i + 1u] = count_records<W>(a, i);
+    }
+}
+
 template <bool EMIT, uint32_t W, bool A16>
 __global__ __launch_bounds__(64) void event_walk(EvArgs a) {
     uint32_t* const lab = reinterpret_cast<uint32_t*>(agnes_smem);
     const uint32_t lane = threadIdx.x;
     const uint32_t i = blockIdx.x * 64u + lane;
     if (i >= a.vb.n_instances) return;
-    if (EMIT)
-        for (uint32_t k = 0; k < a.keys; ++k) lab[k * 64u + lane] = 0u; /* VoteCount::new: Value{} */
+    if (!EMIT) {
+        a.offs[i + 1u] = count_records<W>(a, i);
+        return;
+    }
+    for (uint32_t k = 0; k < a.keys; ++k) lab[k * 64u + lane] = 0u; /* VoteCount::new: Value{} */
     const uint64_t NV = a.vb.n_votes;
     uint64_t lo = a.vb.offsets[i], hi = a.vb.offsets[i + 1u];
     lo = lo < NV ? lo : NV;
@@ -132,10 +169,6 @@ __global__ __launch_bounds__(64) void event_walk(EvArgs a) {
             /* outside the instance, or a vote the tally did not add */
             if (j < lo || j >= hi || ev == AGNES_CODE_INVALID || ev == AGNES_CODE_REJECTED) continue;
             const uint32_t skip = (cb >> 3) & 1u, has = ev != AGNES_CODE_NONE ? 1u : 0u;
-            if (!EMIT) {
-                cnt += skip + has;
-                continue;
-            }
             const uint32_t rb = (r[b >> 2] >> sh8) & 0xFFu, tb = (t[b >> 2] >> sh8) & 0xFFu;
             const uint32_t key = rb * 2u + tb;
             if (tb > 1u || key >= a.keys) continue; /* (never for a code the tally wrote) */
@@ -149,7 +182,6 @@ __global__ __launch_bounds__(64) void event_walk(EvArgs a) {
             }
         }
     }
-    if (!EMIT) a.offs[i + 1u] = cnt;
 }
 
 /* The emit pass, one WAVE per instance (columns aligned: codes / round / type 4 B,
@@ -646,6 +678,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void e
 } // namespace agnes
 
 /* ------------------------------------------------------------------ */
+
+hipError_t agnes_launch_event_count_list(const agnes_vote_batch* vb, const uint8_t* codes, const uint32_t* walk,
+                                         const uint32_t* walk_n, uint64_t* offs, int num_cus, hipStream_t st) {
+    using namespace agnes::events;
+    const uint32_t n = vb->n_instances;
+    if (n == 0) return hipSuccess;
+    EvArgs a{*vb, codes, offs, nullptr, 0u};
+    /* the list is usually empty: a small grid that strides over it */
+    uint32_t blocks = (n + 63u) / 64u;
+    const uint32_t cap = 4u * (uint32_t)(num_cus > 0 ? num_cus : 256);
+    if (blocks > cap) blocks = cap;
+    AgnesKt kt("event_count_list", st);
+    if ((reinterpret_cast<uintptr_t>(codes) & 15u) == 0u)
+        hipLaunchKernelGGL((event_count_list<64u>), dim3(blocks), dim3(64), 0, st, a, walk, walk_n);
+    else
+        hipLaunchKernelGGL((event_count_list<4u>), dim3(blocks), dim3(64), 0, st, a, walk, walk_n);
+    return hipGetLastError();
+}
 
 hipError_t agnes_launch_events(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds,
                                uint64_t* offs, agnes_vote_event* out, uint64_t* scratch, hipStream_t st) {

@@ -84,8 +84,8 @@ constexpr uint32_t EV_HI = AGNES_CODE_NONE | (AGNES_CODE_PRECOMMIT_ANY << 8) | (
 __host__ __device__ inline uint32_t carry_bytes(uint32_t R) { return (uint32_t)align16(32ull * R); }
 /* per-wave LDS: DMA slot | carried executors (2 copies x (vw[2R], vn[2R]) u32) |
  * instance records | (State machine) valid candidates, two batches' staged States */
-__host__ __device__ inline uint32_t lds_bytes(bool sm, uint32_t R) {
-    return F_BYTES + carry_bytes(R) + FB * RECW * 4u + (sm ? FB * 8u + 2u * FB * 64u : 0u);
+__host__ __device__ inline uint32_t lds_bytes(bool sm, uint32_t R, bool evc = false) {
+    return F_BYTES + carry_bytes(R) + FB * RECW * 4u + (sm ? FB * 8u + 2u * FB * 64u : 0u) + (evc ? FB * 4u : 0u);
 }
 
 __device__ __forceinline__ uint32_t zero_marks(uint32_t x) { /* 0x80 in the bytes of x that are zero */
@@ -152,8 +152,16 @@ struct Hdr {
     uint32_t stream;    /* stage 2: the offsets pass; stage 3: walked by this kernel */
 };
 
-template <bool PC, bool SM, bool R1>
+/* EVC: also the number of event records of each instance of a flow batch (votes whose
+ * code is Some(Event), 1..5: this route never sets the RoundSkip bit) into
+ * a.ev_counts[instance] -- the count pass of the event stream (agnes_events.hip) */
+template <bool PC, bool SM, bool R1, bool EVC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void flow(agnes_tally_args a, uint32_t lds_per_wave) {
+#ifdef AGNES_EXP_EARLYDMA
+    constexpr bool EARLY_DMA = PC;
+#else
+    constexpr bool EARLY_DMA = false;
+#endif
     const uint32_t lane = lane_id();
     const uint32_t wave = rfl(threadIdx.x >> 6);
     const uint32_t R = R1 ? 1u : a.max_rounds, nv = a.n_vals, ns = a.n_sets, n = a.vb.n_instances;
@@ -175,6 +183,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
     uint32_t* const itab = reinterpret_cast<uint32_t*>(base + F_BYTES + carry_bytes(R));
     unsigned long long* const vtab = reinterpret_cast<unsigned long long*>(base + F_BYTES + carry_bytes(R) + FB * RECW * 4u);
     unsigned char* const sb = base + F_BYTES + carry_bytes(R) + FB * RECW * 4u + FB * 8u;
+    uint32_t* const etab = reinterpret_cast<uint32_t*>(base + F_BYTES + carry_bytes(R) + FB * RECW * 4u +
+                                                       (SM ? FB * 8u + 2u * FB * 64u : 0u)); /* (EVC) records */
     const agnes_state* const st_in = a.states_in ? a.states_in : a.states;
     uint32_t cpar = 0;
     uint64_t pf_at = ~0ull;
@@ -391,6 +401,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                     rk[R_DF] = 0u;
                     rk[R_DR] = 0u;
                     if (SM) vtab[lane] = 0ull;
+                    if (EVC) etab[lane] = 0u;
                 }
                 if (SM && smf) { /* the State machine's view of each instance (state_machine.rs:184) */
                     if (lane < m) {
@@ -456,6 +467,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                 const uint4 recA = *reinterpret_cast<const uint4*>(itab + RECW * kA); /* q2, pbase, nv, State.round (0x100: none) */
                 const uint4 recB = multi ? *reinterpret_cast<const uint4*>(itab + RECW * kB) : recA;
 
+                /* the next chunk by LDS-DMA (this stream's, or the next batch's first) */
+                auto next_dma = [&]() {
+                    uint64_t nc = ~0ull;
+                    uint32_t nl = 0, nlo = 0;
+                    if (rc + CH < Lend) {
+                        nc = c + CH;
+                        nl = Lend - rc - CH;
+                    } else if (N.s0 < N.e0 && N.stage == 3u && N.stream) {
+                        const uint32_t mN = N.e0 - N.s0;
+                        const uint64_t n0 = u64of(rdl(N.olo, 0u), rdl(N.ohi, 0u));
+                        nc = n0 & ~127ull;
+                        nlo = (uint32_t)(n0 - nc);
+                        nl = rdl(N.olo, mN) - (uint32_t)n0 + nlo;
+                    }
+                    if (nc != ~0ull && nl != nlo) {
+                        dma_chunk(nc, nlo, nl);
+                        pf_at = nc;
+                    } else {
+                        pf_at = ~0ull;
+                    }
+                };
                 /* ---- K1: votes of the chunk + validation + weight gather ---- */
                 uint32_t value[LV], val[LV], r8[2], t8[2];
                 uint32_t nb0 = 0, nb1 = 0; /* 0x10 in the bytes of nil votes */
@@ -481,6 +513,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                         r8[0] = rr.x; r8[1] = rr.y;
                         t8[0] = tt.x; t8[1] = tt.y;
                     }
+                    /* (power table in LDS: no HBM gather to order behind) the slot is in
+                     * registers, so the next chunk's DMA goes out now, a whole K1 earlier */
+                    if (EARLY_DMA) next_dma();
 #pragma unroll
                     for (uint32_t s = 0; s < 4u; ++s) {
                         nb0 |= value[s] == AGNES_NIL ? 0x10u << (8u * s) : 0u;
@@ -544,26 +579,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                  * behind the DMA would wait for the DMA too (in-order vmcnt) */
                 if (!PC) asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]),
                                       "v"(w[6]), "v"(w[7]));
-                { /* the next chunk by LDS-DMA (this stream's, or the next batch's first) */
-                    uint64_t nc = ~0ull;
-                    uint32_t nl = 0, nlo = 0;
-                    if (rc + CH < Lend) {
-                        nc = c + CH;
-                        nl = Lend - rc - CH;
-                    } else if (N.s0 < N.e0 && N.stage == 3u && N.stream) {
-                        const uint32_t mN = N.e0 - N.s0;
-                        const uint64_t n0 = u64of(rdl(N.olo, 0u), rdl(N.ohi, 0u));
-                        nc = n0 & ~127ull;
-                        nlo = (uint32_t)(n0 - nc);
-                        nl = rdl(N.olo, mN) - (uint32_t)n0 + nlo;
-                    }
-                    if (nc != ~0ull && nl != nlo) {
-                        dma_chunk(nc, nlo, nl);
-                        pf_at = nc;
-                    } else {
-                        pf_at = ~0ull;
-                    }
-                }
+                if (!EARLY_DMA) next_dma();
                 flush(); /* the previous chunk's codes */
 
                 /* ---- K2 + K3 ---- */
@@ -912,6 +928,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                     }
                 }
 
+                if (EVC) { /* records per unit: the votes whose event is Some (codes 1..5) */
+                    auto recs = [](uint32_t cw4) -> uint32_t {
+                        const uint32_t e = cw4 & 0x07070707u;
+                        const uint32_t nz = (e + 0x7F7F7F7Fu) & 0x80808080u; /* event != None        */
+                        const uint32_t iv = (e + 0x7A7A7A7Au) & 0x80808080u; /* INVALID / REJECTED   */
+                        return (uint32_t)__builtin_popcount(nz & ~iv);
+                    };
+                    const uint32_t nA = actA ? recs(c0) : 0u, nB = actB ? recs(c1) : 0u;
+                    atomicAdd(etab + kA, kA == kB ? nA + nB : nA);
+                    atomicAdd(etab + kB, kA == kB ? 0u : nB);
+                }
+
                 /* codes (deferred) */
                 dc0 = c0;
                 dc1 = c1;
@@ -920,7 +948,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                 __builtin_amdgcn_wave_barrier();
             }
         }
-        /* batch end: the States out (a walk-list batch's are the walk kernel's) */
+        /* batch end: the record counts and the States out (a walk-list batch's are the
+         * walk kernel's) */
+        if (EVC && m && H.stream) {
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t Le = rdl(H.olo, m) - rdl(H.olo, 0u) + (rdl(H.olo, 0u) & 127u);
+            if (lane < m) a.ev_counts[H.s0 + lane] = Le ? (uint64_t)etab[lane] : 0ull;
+        }
         if (SM && m && H.stream) {
             if (smf) { /* no vote: the States as they came */
                 dma_wait();
@@ -953,14 +987,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
 /* ------------------------------------------------------------------ */
 /* launcher                                                            */
 
-template <bool SM, bool R1>
+template <bool SM, bool R1, bool EVC>
 static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStream_t st) {
     const uint32_t n = a->vb.n_instances;
     if (n == 0) return hipSuccess;
     using agnes::flow::flow;
-    const void* fns[2] = {reinterpret_cast<const void*>(&flow<false, SM, R1>),
-                          reinterpret_cast<const void*>(&flow<true, SM, R1>)};
-    const uint32_t lpw = agnes::flow::lds_bytes(SM, a->max_rounds);
+    const void* fns[2] = {reinterpret_cast<const void*>(&flow<false, SM, R1, EVC>),
+                          reinterpret_cast<const void*>(&flow<true, SM, R1, EVC>)};
+    const uint32_t lpw = agnes::flow::lds_bytes(SM, a->max_rounds, EVC);
     const uint64_t wave_lds = (uint64_t)lpw * AGNES_WAVES_PER_BLOCK;
     const uint64_t pcb = agnes::align16(4ull * a->n_sets * a->n_vals);
     /* blocks per CU from the occupancy query; the LDS power table only where it
@@ -1004,8 +1038,8 @@ static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStrea
     const uint64_t cap = ncu * (uint64_t)o->per_cu;
     if (blocks > cap) blocks = cap;
     if (blocks == 0) blocks = 1;
-    if (o->pc) hipLaunchKernelGGL((flow<true, SM, R1>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
-    else hipLaunchKernelGGL((flow<false, SM, R1>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
+    if (o->pc) hipLaunchKernelGGL((flow<true, SM, R1, EVC>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
+    else hipLaunchKernelGGL((flow<false, SM, R1, EVC>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
     return hipGetLastError();
 }
 
@@ -1013,11 +1047,23 @@ bool agnes_flow_supported(const agnes_tally_args* a) {
     /* rounds 0..14 in the byte checks; the per-wave LDS fits the waves a CU holds (16
      * without the State machine, 12 with it: its VGPRs allow 3 waves per SIMD) */
     const bool sm = (a->flags & AGNES_FLAG_STATE_MACHINE) != 0 && a->states != nullptr;
-    return a->max_rounds <= 15u && agnes::flow::lds_bytes(sm, a->max_rounds) * (sm ? 12u : 16u) <= 160u * 1024u;
+    return a->max_rounds <= 15u &&
+           agnes::flow::lds_bytes(sm, a->max_rounds, a->ev_counts != nullptr) * (sm ? 12u : 16u) <= 160u * 1024u;
+}
+
+bool agnes_flow_counts_events(uint32_t flags, uint32_t max_rounds) {
+    const bool sm = (flags & AGNES_FLAG_STATE_MACHINE) != 0;
+    return max_rounds <= 15u && agnes::flow::lds_bytes(sm, max_rounds, true) * (sm ? 12u : 16u) <= 160u * 1024u;
 }
 
 hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t st) {
     const bool sm = (a->flags & AGNES_FLAG_STATE_MACHINE) != 0 && a->states != nullptr;
-    if (a->max_rounds == 1u) return sm ? launch_flow_k<true, true>(a, num_cus, st) : launch_flow_k<false, true>(a, num_cus, st);
-    return sm ? launch_flow_k<true, false>(a, num_cus, st) : launch_flow_k<false, false>(a, num_cus, st);
+    if (a->ev_counts) {
+        if (a->max_rounds == 1u)
+            return sm ? launch_flow_k<true, true, true>(a, num_cus, st) : launch_flow_k<false, true, true>(a, num_cus, st);
+        return sm ? launch_flow_k<true, false, true>(a, num_cus, st) : launch_flow_k<false, false, true>(a, num_cus, st);
+    }
+    if (a->max_rounds == 1u)
+        return sm ? launch_flow_k<true, true, false>(a, num_cus, st) : launch_flow_k<false, true, false>(a, num_cus, st);
+    return sm ? launch_flow_k<true, false, false>(a, num_cus, st) : launch_flow_k<false, false, false>(a, num_cus, st);
 }

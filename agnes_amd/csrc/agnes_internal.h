@@ -54,6 +54,9 @@ typedef struct agnes_tally_args {
     uint32_t power_cache; /* bytes of block LDS holding the u32 power table (0: gather from HBM) */
     uint32_t one_inst;    /* AGNES_FLAG_ONE_INSTANCE: every segment is a slice of instance one_id */
     uint32_t one_id;
+    uint64_t* ev_counts;  /* optional [n_instances]: the flow kernel writes each instance's event
+                             record count (agnes_tally_events); instances it hands to the walk
+                             list are left to agnes_launch_event_count_list */
 } agnes_tally_args;
 
 /* agnes_kernel_timing: HIP events around each launch while enabled (agnes_api.cpp) */
@@ -85,6 +88,8 @@ hipError_t agnes_launch_sweep(const agnes_tally_args* a, int num_cus, hipStream_
 /* the 8-votes-per-lane flow kernel (agnes_flow.hip) for the sweep route's streams */
 bool agnes_flow_supported(const agnes_tally_args* a);
 hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t stream);
+/* the flow kernel can count event records (agnes_tally_events) in this configuration */
+bool agnes_flow_counts_events(uint32_t flags, uint32_t max_rounds);
 /* the batched State::apply pass over the codes a tally kernel left (agnes_apply.hip):
  * one instance per lane, skipping the instances deferred to the LIST kernel */
 bool agnes_apply_codes_supported(const agnes_tally_args* a);
@@ -143,6 +148,10 @@ hipError_t agnes_launch_partials(const agnes_vote_batch* vb, const int64_t* powe
                                  int64_t* weights, hipStream_t st);
 hipError_t agnes_launch_events(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds,
                                uint64_t* offs, agnes_vote_event* out, uint64_t* scratch, hipStream_t stream);
+/* the event-record counts of the instances on a tally's walk list (walk[0 .. *walk_n)),
+ * into offs[1 + instance]: the ones the flow kernel did not count */
+hipError_t agnes_launch_event_count_list(const agnes_vote_batch* vb, const uint8_t* codes, const uint32_t* walk,
+                                         const uint32_t* walk_n, uint64_t* offs, int num_cus, hipStream_t stream);
 hipError_t agnes_launch_edges(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds,
                               uint64_t* offs, agnes_edge* out, uint64_t* scratch, hipStream_t stream);
 

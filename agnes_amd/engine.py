@@ -143,6 +143,35 @@ class Engine:
         check(self.lib.agnes_tally_states(self.ctx, C.byref(cfg), C.byref(b), _ptr(codes), _ptr(states_in),
                                           _ptr(states_out), _stream_handle(stream)), "agnes_tally_states")
 
+    def tally_events(self, cfg: abi.Config, batch: DeviceBatch, codes: torch.Tensor,
+                     states_in: Optional[torch.Tensor] = None, states_out: Optional[torch.Tensor] = None,
+                     offsets: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, stream=None):
+        """agnes_tally_events: the tally (as tally_states) and its event stream in one call.
+        offsets int64 [n_instances + 1] (offsets[-1] = the record count), out uint8
+        [events_capacity(cfg, batch), 24]; both allocated when None.  Returns (offsets,
+        out) without reading the count back (no sync)."""
+        if codes.dtype != torch.uint8 or codes.numel() < batch.n_votes:
+            raise ValueError("codes must be a uint8 tensor of n_votes")
+        for t in (states_in, states_out):
+            if t is not None and t.numel() < 64 * batch.n_instances:
+                raise ValueError("states must hold n_instances 64-byte records")
+        cap = self.events_capacity(cfg, batch)
+        if offsets is None:
+            offsets = torch.empty(batch.n_instances + 1, dtype=torch.int64, device=self.device)
+        if out is None:
+            out = torch.empty((max(cap, 1), 24), dtype=torch.uint8, device=self.device)
+        if offsets.numel() < batch.n_instances + 1 or out.numel() < 24 * cap:
+            raise ValueError("offsets must hold n_instances + 1, out events_capacity records")
+        b = batch.c()
+        check(self.lib.agnes_tally_events(self.ctx, C.byref(cfg), C.byref(b), _ptr(codes), _ptr(states_in),
+                                          _ptr(states_out), _ptr(offsets), _ptr(out), _stream_handle(stream)),
+              "agnes_tally_events")
+        return offsets, out
+
+    def events_capacity(self, cfg: abi.Config, batch: DeviceBatch) -> int:
+        b = batch.c()
+        return int(self.lib.agnes_events_capacity(C.byref(cfg), C.byref(b)))
+
     def tally_carried(self, cfg: abi.Config, batch: DeviceBatch, codes: torch.Tensor,
                       counts: torch.Tensor, stream=None):
         """agnes_tally_carried: counts = int64 tensor [n_instances, 2 * max_rounds, 3]

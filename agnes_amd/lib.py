@@ -91,6 +91,8 @@ def load():
         "agnes_fold_counts": ([P, P, C.c_uint32, C.c_uint32, P, P, C.c_uint32, P], C.c_int),
         "agnes_event_offsets": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P], C.c_int),
         "agnes_events": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P], C.c_int),
+        "agnes_tally_events": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P, P, P], C.c_int),
+        "agnes_events_capacity": ([C.POINTER(abi.Config), C.POINTER(abi.VoteBatch)], C.c_uint64),
         "agnes_dedup_first": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), C.c_uint64, P, P], C.c_int),
         "agnes_dedup_mask": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), C.c_uint64, P, P, P],
                              C.c_int),

@@ -252,6 +252,48 @@ def event_stream(eng, cfg, batch, codes, reps: int = 3):
     return res
 
 
+def tally_events_timed(eng, cfg, batch, codes, st0, states, steps, ref_offs, ref_recs):
+    """agnes_tally_events: the step and its event stream in ONE call (SURVEY.md §8(b),
+    the records counted inside the tally kernel), captured in a HIP graph and timed
+    like the step, outside the timed region of `value`; its records must equal the
+    two-call stream's (ref_offs / ref_recs) byte for byte."""
+    cap = eng.events_capacity(cfg, batch)
+    offs = torch.empty(batch.n_instances + 1, dtype=torch.int64, device=eng.device)
+    out = torch.empty((max(cap, 1), 24), dtype=torch.uint8, device=eng.device)
+
+    def call():
+        eng.tally_events(cfg, batch, codes, st0, states, offs, out)
+
+    call()
+    torch.cuda.synchronize()
+    eng.kernel_timing(True)
+    for _ in range(3):
+        call()
+    torch.cuda.synchronize()
+    kt = eng.kernel_times()
+    eng.kernel_timing(False)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        call()
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        call()
+    g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.replay()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / steps
+    n = int(offs[-1].item())
+    equal = bool(torch.equal(offs, ref_offs) and torch.equal(out[:n], ref_recs))
+    del g, out
+    return {"ms_per_call": ms, "records": n, "equal_to_two_call_stream": equal,
+            "kernels": {name: {"launches": k, "avg_ms": t / max(k, 1)} for name, (k, t) in kt.items()}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -352,6 +394,9 @@ def main():
     events = event_stream(eng, cfg, batch, codes)
     edges = edge_summary(eng, cfg, batch, codes)
     ev_offs, ev_recs = events.pop("_offsets"), events.pop("_records")
+    te = tally_events_timed(eng, cfg, batch, codes, st0, states, args.steps, ev_offs, ev_recs)
+    te["records_ms"] = te["ms_per_call"] - elapsed * 1e3 / args.steps  # over the tally step alone
+    events["tally_events"] = te
     ed_offs = edges.pop("_offsets")
     if world > 1:  # every rank's edge records to every rank (RCCL), outside the timed region
         edges["all_gather"] = adist.gather_edges_timed(edges.pop("_records"))

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AGNES_ABI_VERSION 6u
+#define AGNES_ABI_VERSION 7u
 
 /* ---------------------------------------------------------------------------
  * Status codes (reference never fails, state_machine.rs:212; these report
@@ -667,6 +667,20 @@ int agnes_event_offsets(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vot
  * reads codes, round, type and value.  max_rounds <= 64. */
 int agnes_events(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
                  const uint8_t* codes, const uint64_t* offsets, agnes_vote_event* out, void* stream);
+
+/* The tally and its event stream in ONE call (agnes_tally with
+ * d_out / d_n_out): agnes_tally_states, then the records of every Some(Event) as
+ * agnes_event_offsets + agnes_events would give them.  offsets (DEVICE,
+ * n_instances + 1) receives the exclusive record offsets, offsets[n_instances] the
+ * number of records (d_n_out); out (DEVICE, 8-B aligned) must hold
+ * agnes_events_capacity(cfg, batch) records (the most a batch can produce: one per
+ * vote, two with RoundSkip).  On the fused route (REFERENCE without RoundSkip,
+ * max_rounds <= 15) the tally kernel counts each instance's records itself, so no
+ * count pass re-reads the codes.  batch->value 4-B aligned; max_rounds <= 64. */
+int agnes_tally_events(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch, uint8_t* codes,
+                       const agnes_state* states_in, agnes_state* states_out, uint64_t* offsets,
+                       agnes_vote_event* out, void* stream);
+uint64_t agnes_events_capacity(const agnes_config* cfg, const agnes_vote_batch* batch);
 
 /* ---------------------------------------------------------------------------
  * Synthetic workload generator (counter-based splitmix64; identical on host

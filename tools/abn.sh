@@ -6,7 +6,7 @@ if [ -n "${PAR:-}" ]; then
   timeout -k 10 600 python -u -m pytest tests -m "gpu and not slow" -x -q --timeout 200 --timeout-method thread -k "$PAR" > gpurun_out/abn_tests.log 2>&1 || { tail -30 gpurun_out/abn_tests.log; exit 1; }
   tail -2 gpurun_out/abn_tests.log
 fi
-summ() { python3 -c "import json,sys; d=json.loads(open('$1').read().strip().splitlines()[-1]); print('$2', round(d['ms_per_step'],4), round(d['roofline'].get('path_frac') or 0,3), {k:round(v['avg_ms'],4) for k,v in d['kernels'].items()}, {k:round(v['avg_ms'],4) for k,v in d.get('event_stream',{}).items() if isinstance(v,dict)})"; }
+summ() { python3 -c "import json,sys; d=json.loads(open('$1').read().strip().splitlines()[-1]); print('$2', round(d['ms_per_step'],4), round(d['roofline'].get('path_frac') or 0,3), {k:round(v['avg_ms'],4) for k,v in d['kernels'].items()}, {k:round(v.get('avg_ms', v.get('ms_per_call', 0)),4) for k,v in d.get('event_stream',{}).items() if isinstance(v,dict)})"; }
 for r in $(seq ${REPS:-2}); do
   for c in ${CFGS:-c2}; do
     for spec in ${LIBS:-new=-}; do
