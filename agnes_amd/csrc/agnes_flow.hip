@@ -130,6 +130,28 @@ __device__ __forceinline__ void sdma4(const void* base, uint32_t voff, uint32_t 
                  : "v"(voff), "s"(base), "s"(lds)
                  : "memory");
 }
+/* a whole chunk: the five columns, each column's two 256-vote halves under ONE m0 (the
+ * instruction offset moves the global and the LDS address alike), m0 saved once */
+__device__ __forceinline__ void sdma_chunk(const void* bi, const void* bv, const void* bd, const void* br,
+                                           const void* bt, uint32_t o16, uint32_t o4, uint32_t slotl) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\t"
+                 "s_mov_b32 m0, %8\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, %3 nt\n\tglobal_load_lds_dwordx4 %1, %3 offset:1024 nt\n\t"
+                 "s_mov_b32 m0, %9\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, %4 nt\n\tglobal_load_lds_dwordx4 %1, %4 offset:1024 nt\n\t"
+                 "s_mov_b32 m0, %10\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, %5 nt\n\tglobal_load_lds_dwordx4 %1, %5 offset:1024 nt\n\t"
+                 "s_mov_b32 m0, %11\n\ts_nop 0\n\t"
+                 "global_load_lds_dword %2, %6 nt\n\tglobal_load_lds_dword %2, %6 offset:256 nt\n\t"
+                 "s_mov_b32 m0, %12\n\ts_nop 0\n\t"
+                 "global_load_lds_dword %2, %7 nt\n\tglobal_load_lds_dword %2, %7 offset:256 nt\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(o16), "v"(o4), "s"(bi), "s"(bv), "s"(bd), "s"(br), "s"(bt), "s"(slotl + F_INST),
+                   "s"(slotl + F_VALUE), "s"(slotl + F_VAL), "s"(slotl + F_ROUND), "s"(slotl + F_TYPE)
+                 : "memory");
+}
 __device__ __forceinline__ void sstore4(void* base, uint32_t voff, uint32_t d) {
     asm volatile("global_store_dword %0, %1, %2" ::"v"(voff), "v"(d), "s"(base) : "memory");
 }
@@ -161,6 +183,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
     constexpr bool EARLY_DMA = PC;
 #else
     constexpr bool EARLY_DMA = false;
+#endif
+#ifdef AGNES_EXP_STEAL
+    constexpr bool STEAL = true;
+#else
+    constexpr bool STEAL = false;
 #endif
     const uint32_t lane = lane_id();
     const uint32_t wave = rfl(threadIdx.x >> 6);
@@ -194,8 +221,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
 
     /* ---- work queue: batches of FB, then SMALLB ones for the tail ---- */
     const uint32_t qn = gridDim.x < QN ? gridDim.x : QN;
-    const uint32_t qk = blockIdx.x % qn;
-    uint32_t* const ctr = a.list_count + 1u + qk;
+    uint32_t qk = blockIdx.x % qn; /* this wave's queue (STEAL: the one it now takes batches from) */
+    uint32_t* ctr = a.list_count + 1u + qk;
     const uint64_t NB = (uint64_t)(n / FB) * 15u / 16u;
     auto range_of = [&](uint32_t t, uint32_t& s0, uint32_t& e0) {
         const uint64_t b = (uint64_t)t * qn + qk;
@@ -277,16 +304,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
     auto dma_chunk = [&](uint64_t c, uint32_t lo, uint32_t lim) { /* the chunk's votes lo..lim into the slot */
         __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): the slot's LDS reads are done */
         if (lo == 0u && lim >= CH) {
-            sdma16(a.vb.instance + c, o16, slotl + F_INST);
-            sdma16(a.vb.instance + c + 256u, o16, slotl + F_INST + 1024u);
-            sdma16(a.vb.value + c, o16, slotl + F_VALUE);
-            sdma16(a.vb.value + c + 256u, o16, slotl + F_VALUE + 1024u);
-            sdma16(a.vb.validator + c, o16, slotl + F_VAL);
-            sdma16(a.vb.validator + c + 256u, o16, slotl + F_VAL + 1024u);
-            sdma4(a.vb.round + c, o4, slotl + F_ROUND);
-            sdma4(a.vb.round + c + 256u, o4, slotl + F_ROUND + 256u);
-            sdma4(a.vb.type + c, o4, slotl + F_TYPE);
-            sdma4(a.vb.type + c + 256u, o4, slotl + F_TYPE + 256u);
+            sdma_chunk(a.vb.instance + c, a.vb.value + c, a.vb.validator + c, a.vb.round + c, a.vb.type + c, o16, o4,
+                       slotl);
         } else { /* a stream's first or last chunk: only its lanes load (4-vote groups; the
                   * rest of the slot is never read as active) */
             if (4u * lane >= lo && 4u * lane < lim) {
@@ -973,6 +992,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
         H = N;
         spar ^= 1u;
         range_of(rdl(tq, 0u), N.s0, N.e0); /* the batch after, grabbed one batch ago */
+        if (STEAL && N.s0 >= N.e0) {
+            /* this queue is done: take the rest of another one's (queues whose counter
+             * shows batches left, read 4 per lane; a stale count only costs a try) */
+            const uint64_t BT = NB + ((uint64_t)n - NB * FB + SMALLB - 1u) / SMALLB; /* batches in all */
+            for (uint32_t tries = 0; tries < 8u && N.s0 >= N.e0; ++tries) {
+                uint32_t left = 0; /* bit i: queue lane + 64 i has batches left */
+#pragma unroll
+                for (uint32_t i = 0; i < 4u; ++i) {
+                    const uint32_t q = lane + 64u * i;
+                    if (q < qn) {
+                        const uint32_t c = __hip_atomic_load(a.list_count + 1u + q, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT);
+                        left |= ((uint64_t)c * qn + q < BT ? 1u : 0u) << i;
+                    }
+                }
+                /* the first such queue after this one, in queue order */
+                uint32_t pick = 0xFFFFFFFFu;
+#pragma unroll
+                for (uint32_t i = 0; i < 4u; ++i) {
+                    const uint64_t bl = ballot((left >> i) & 1u);
+                    if (bl) {
+                        const uint32_t q = 64u * i + (uint32_t)__builtin_ctzll(bl);
+                        const uint32_t d = (q + qn - qk) % qn;
+                        pick = min(pick, (d << 8) | q);
+                    }
+                }
+                if (pick == 0xFFFFFFFFu) break;
+                qk = pick & 0xFFu;
+                ctr = a.list_count + 1u + qk;
+                uint32_t t = 0;
+                if (lane == 0) t = atomicAdd(ctr, 1u);
+                range_of(rdl(t, 0u), N.s0, N.e0);
+            }
+        }
         if (lane == 0) tq = atomicAdd(ctr, 1u);
         hdr1(N);
     }
