@@ -179,16 +179,7 @@ struct Hdr {
  * a.ev_counts[instance] -- the count pass of the event stream (agnes_events.hip) */
 template <bool PC, bool SM, bool R1, bool EVC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void flow(agnes_tally_args a, uint32_t lds_per_wave) {
-#ifdef AGNES_EXP_EARLYDMA
-    constexpr bool EARLY_DMA = PC;
-#else
-    constexpr bool EARLY_DMA = false;
-#endif
-#ifdef AGNES_EXP_STEAL
-    constexpr bool STEAL = true;
-#else
-    constexpr bool STEAL = false;
-#endif
+
     const uint32_t lane = lane_id();
     const uint32_t wave = rfl(threadIdx.x >> 6);
     const uint32_t R = R1 ? 1u : a.max_rounds, nv = a.n_vals, ns = a.n_sets, n = a.vb.n_instances;
@@ -221,8 +212,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
 
     /* ---- work queue: batches of FB, then SMALLB ones for the tail ---- */
     const uint32_t qn = gridDim.x < QN ? gridDim.x : QN;
-    uint32_t qk = blockIdx.x % qn; /* this wave's queue (STEAL: the one it now takes batches from) */
-    uint32_t* ctr = a.list_count + 1u + qk;
+    const uint32_t qk = blockIdx.x % qn;
+    uint32_t* const ctr = a.list_count + 1u + qk;
     const uint64_t NB = (uint64_t)(n / FB) * 15u / 16u;
     auto range_of = [&](uint32_t t, uint32_t& s0, uint32_t& e0) {
         const uint64_t b = (uint64_t)t * qn + qk;
@@ -532,9 +523,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                         r8[0] = rr.x; r8[1] = rr.y;
                         t8[0] = tt.x; t8[1] = tt.y;
                     }
-                    /* (power table in LDS: no HBM gather to order behind) the slot is in
-                     * registers, so the next chunk's DMA goes out now, a whole K1 earlier */
-                    if (EARLY_DMA) next_dma();
 #pragma unroll
                     for (uint32_t s = 0; s < 4u; ++s) {
                         nb0 |= value[s] == AGNES_NIL ? 0x10u << (8u * s) : 0u;
@@ -598,7 +586,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                  * behind the DMA would wait for the DMA too (in-order vmcnt) */
                 if (!PC) asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]),
                                       "v"(w[6]), "v"(w[7]));
-                if (!EARLY_DMA) next_dma();
+                next_dma();
                 flush(); /* the previous chunk's codes */
 
                 /* ---- K2 + K3 ---- */
@@ -992,40 +980,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
         H = N;
         spar ^= 1u;
         range_of(rdl(tq, 0u), N.s0, N.e0); /* the batch after, grabbed one batch ago */
-        if (STEAL && N.s0 >= N.e0) {
-            /* this queue is done: take the rest of another one's (queues whose counter
-             * shows batches left, read 4 per lane; a stale count only costs a try) */
-            const uint64_t BT = NB + ((uint64_t)n - NB * FB + SMALLB - 1u) / SMALLB; /* batches in all */
-            for (uint32_t tries = 0; tries < 8u && N.s0 >= N.e0; ++tries) {
-                uint32_t left = 0; /* bit i: queue lane + 64 i has batches left */
-#pragma unroll
-                for (uint32_t i = 0; i < 4u; ++i) {
-                    const uint32_t q = lane + 64u * i;
-                    if (q < qn) {
-                        const uint32_t c = __hip_atomic_load(a.list_count + 1u + q, __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_AGENT);
-                        left |= ((uint64_t)c * qn + q < BT ? 1u : 0u) << i;
-                    }
-                }
-                /* the first such queue after this one, in queue order */
-                uint32_t pick = 0xFFFFFFFFu;
-#pragma unroll
-                for (uint32_t i = 0; i < 4u; ++i) {
-                    const uint64_t bl = ballot((left >> i) & 1u);
-                    if (bl) {
-                        const uint32_t q = 64u * i + (uint32_t)__builtin_ctzll(bl);
-                        const uint32_t d = (q + qn - qk) % qn;
-                        pick = min(pick, (d << 8) | q);
-                    }
-                }
-                if (pick == 0xFFFFFFFFu) break;
-                qk = pick & 0xFFu;
-                ctr = a.list_count + 1u + qk;
-                uint32_t t = 0;
-                if (lane == 0) t = atomicAdd(ctr, 1u);
-                range_of(rdl(t, 0u), N.s0, N.e0);
-            }
-        }
         if (lane == 0) tq = atomicAdd(ctr, 1u);
         hdr1(N);
     }
