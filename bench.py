@@ -373,23 +373,24 @@ def main():
     g.replay()
     torch.cuda.synchronize()
 
-    pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-             for _ in range(args.steps)]
+    # one HIP event pair around the K replays (events between the replays would sit in
+    # the stream between the steps and be timed with them)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        pairs[k][0].record(stream)
+    ev0.record(stream)
+    for _ in range(args.steps):
         g.replay()
-        pairs[k][1].record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     elapsed = adist.max_over_ranks(elapsed)
     total_votes_step = adist.sum_over_ranks(batch.n_votes)
     if world > 1:
         dist.barrier()
-    step_gpu_ms = float(np.mean([a.elapsed_time(b) for a, b in pairs]))
+    step_gpu_ms = ev0.elapsed_time(ev1) / args.steps
 
     events = event_stream(eng, cfg, batch, codes)
     edges = edge_summary(eng, cfg, batch, codes)
