@@ -32,6 +32,7 @@ KERNELS = {
     "edge_count": r"agnes::edges::edge_walk<false,",
     "edge_emit": r"agnes::edges::edge_walk<true,",
     "event_count": r"agnes::events::event_walk<false,",
+    "event_count_list": r"agnes::events::event_count_list<",
     "event_emit": r"agnes::events::(event_emit_stream|event_emit_wave|event_walk<true,)",
 }
 
