@@ -301,6 +301,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--route", choices=["auto", "instance", "split", "wide"], default="auto",
+                    help="force a tally route (AGNES_ROUTE_*; diagnostics: every route gives identical results)")
     ap.add_argument("--segments", type=int, default=0,
                     help="c5/c5d: segments per GPU (one wave each; default: the workload's)")
     args = ap.parse_args()
@@ -335,7 +337,8 @@ def main():
     batch = eng.gen_batch(p)
     set_of = adist.set_of_instances(shard, n_sets)   # global instance id mod n_sets
     batch.instance_set = torch.from_numpy(set_of.view(np.int32)).to(eng.device)
-    cfg = abi.config(w["mode"], w["flags"], w["max_rounds"])
+    route = {"auto": 0, "instance": 1, "split": 2, "wide": 3}[args.route]
+    cfg = abi.config(w["mode"], w["flags"] | (route << 8), w["max_rounds"])
     st0_host = start_states(p.n_instances)
     st0 = states_to_device(st0_host, eng.device)
     states = torch.empty_like(st0)
