@@ -182,3 +182,28 @@ def test_tally_events_full_c2(eng):
     power = ol.gen_power(0xA6E5, 1, 100, abi.POWER_UNIFORM, 1, 1000)
     _check(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 1), hb, power,
            abi.new_states(1_000_000, 1, abi.STEP_PREVOTE), in_place=False)
+
+
+@pytest.mark.slow
+def test_tally_events_full_c3_shard(eng):
+    """a C3 shard: 125k instances x 150 validators x 1..4 rounds, 1024 power sets (the
+    flow kernel's runs mode counts the records of several rounds per chunk)"""
+    p = abi.gen_params(seed=0xA6E5, n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300)
+    hb = ol.gen_batch(p)
+    hb.instance_set = ad.set_of_instances(ad.Shard(p, 0, p.n_instances), 1024)
+    power = ol.gen_power(0xA6E5, 1024, 150, abi.POWER_UNIFORM, 1, 1000)
+    _check(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 4), hb, power,
+           abi.new_states(125_000, 1, abi.STEP_PREVOTE))
+
+
+@pytest.mark.slow
+def test_tally_events_full_c4_shard(eng):
+    """a C4 shard: DEDUP + RoundSkip + DISTINCT_VALUES, Zipf power (the count pass route)"""
+    p = abi.gen_params(seed=0xA6E5, n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300,
+                       dup_permille=100, equiv_permille=100, higher_permille=50)
+    hb = ol.gen_batch(p)
+    hb.instance_set = ad.set_of_instances(ad.Shard(p, 0, p.n_instances), 1024)
+    power = ol.gen_power(0xA6E5, 1024, 150, abi.POWER_ZIPF, 1, 1_000_000)
+    cfg = abi.config(abi.MODE_DEDUP, abi.FLAG_STATE_MACHINE | abi.FLAG_ROUND_SKIP | abi.FLAG_DISTINCT_VALUES, 5)
+    ev = _check(eng, cfg, hb, power, abi.new_states(125_000, 1, abi.STEP_PREVOTE))
+    assert (ev["kind"] == abi.EV_ROUND_SKIP).any()
