@@ -46,6 +46,11 @@ KERNEL_BYTES_PER_VOTE = {
 }
 # C5 pass B reads the weight column pass A wrote (AGNES_FLAG_WEIGHTS_CACHED) on top of the 15 B
 C5_PASS_B_BYTES_PER_VOTE = 23
+# SURVEY.md §8(d), amortized extras: with the State machine on, each instance's State is
+# read and written once per step (64-B agnes_state in, 64 B out) by the kernel that
+# applies the events (flow on the fused route, apply_codes on the split one)
+STATE_BYTES_PER_INSTANCE = 128
+KERNEL_STATE_IO = {"flow", "apply_codes"}
 KERNEL_SYMBOLS = {
     # template parameters: PC (power table in LDS), SM (State machine), R1 (one round);
     # c2 runs flow<true, true, true>, c3 flow<false, true, false> (rocprofv3 names them)
@@ -411,6 +416,8 @@ def main():
     if rank == 0:
         ms_per_step = elapsed * 1e3 / args.steps
         value = total_votes_step * args.steps / elapsed
+        # the States this GPU's step reads and writes (State machine on)
+        st_bytes = STATE_BYTES_PER_INSTANCE * p.n_instances if w["flags"] & abi.FLAG_STATE_MACHINE else 0
         traffic = measured_traffic(args.config)
         with_traffic(events, traffic)
         with_traffic(edges, traffic)
@@ -418,16 +425,17 @@ def main():
         kernels = {}
         for name, (launches, total) in ktimes.items():
             avg = total / max(launches, 1)
-            ab = KERNEL_BYTES_PER_VOTE.get(name, 0) * batch.n_votes
+            ab = KERNEL_BYTES_PER_VOTE.get(name, 0) * batch.n_votes + (st_bytes if name in KERNEL_STATE_IO else 0)
             t = traffic.get(name)
             kernels[name] = {"launches": launches, "avg_ms": avg, "algorithmic_bytes": ab,
                              "GBps": ab / (avg * 1e-3) / 1e9 if ab and avg > 0 else None,
                              "traffic": t.get("traffic_bytes") if t else None}
         dom = max(kernels, key=lambda k: kernels[k]["avg_ms"] * kernels[k]["launches"])
         dom_ms = kernels[dom]["avg_ms"]
-        ab_dom = KERNEL_BYTES_PER_VOTE[dom] * batch.n_votes
+        ab_dom = KERNEL_BYTES_PER_VOTE[dom] * batch.n_votes + (st_bytes if dom in KERNEL_STATE_IO else 0)
         achieved = ab_dom / (dom_ms * 1e-3) / 1e9
-        path_achieved = BYTES_PER_VOTE * batch.n_votes / (ms_per_step * 1e-3) / 1e9
+        path_bytes = BYTES_PER_VOTE * batch.n_votes + st_bytes
+        path_achieved = path_bytes / (ms_per_step * 1e-3) / 1e9
         td = traffic.get(dom)
         out = {
             "metric": "votes_tallied_per_sec",
@@ -456,9 +464,11 @@ def main():
                          "kernel": KERNEL_SYMBOLS.get(dom, dom),
                          "kernel_avg_ms": dom_ms,
                          "bytes_per_vote": KERNEL_BYTES_PER_VOTE[dom],
+                         "state_bytes": st_bytes if dom in KERNEL_STATE_IO else 0,
                          "algorithmic_bytes": ab_dom,
                          # the whole step (every launch agnes_tally_states enqueues, wall
                          # clock of the timed region) at 15 B/vote against the same peak
+                         "path_bytes": path_bytes,
                          "path_achieved": path_achieved,
                          "path_frac": path_achieved / HBM_PEAK_GBS},
             "kernels": kernels,
