@@ -426,7 +426,56 @@ __device__ __forceinline__ uint32_t from_prev(uint32_t x, uint32_t lane) {
     return lane ? y : 0u;
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void event_emit_stream(EvArgs a) {
+/* V votes per lane (a pass is 64 V votes): byte columns as V/4 dwords, values as V u32 */
+template <uint32_t V>
+struct PassV {
+    uint32_t c4[V / 4u], r4[V / 4u], t4[V / 4u], v[V];
+};
+template <uint32_t V>
+__device__ __forceinline__ void load_pass_v(const EvArgs& a, uint64_t j0, uint64_t NV, PassV<V>& p) {
+#pragma unroll
+    for (uint32_t q = 0; q < V / 4u; ++q) p.c4[q] = p.r4[q] = p.t4[q] = 0u;
+#pragma unroll
+    for (uint32_t s = 0; s < V; ++s) p.v[s] = AGNES_NIL;
+    if (j0 + V <= NV) {
+        if constexpr (V == 8u) { /* j0 is a multiple of 8: 8-B byte-column loads, 32-B value loads */
+            const uint2 c = *reinterpret_cast<const uint2*>(a.codes + j0);
+            const uint2 r = *reinterpret_cast<const uint2*>(a.vb.round + j0);
+            const uint2 t = *reinterpret_cast<const uint2*>(a.vb.type + j0);
+            p.c4[0] = c.x; p.c4[1] = c.y;
+            p.r4[0] = r.x; p.r4[1] = r.y;
+            p.t4[0] = t.x; p.t4[1] = t.y;
+        } else {
+#pragma unroll
+            for (uint32_t q = 0; q < V / 4u; ++q) {
+                p.c4[q] = *reinterpret_cast<const uint32_t*>(a.codes + j0 + 4u * q);
+                p.r4[q] = *reinterpret_cast<const uint32_t*>(a.vb.round + j0 + 4u * q);
+                p.t4[q] = *reinterpret_cast<const uint32_t*>(a.vb.type + j0 + 4u * q);
+            }
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < V / 4u; ++q) {
+            const uint4 x = *reinterpret_cast<const uint4*>(a.vb.value + j0 + 4u * q);
+            p.v[4u * q] = x.x;
+            p.v[4u * q + 1u] = x.y;
+            p.v[4u * q + 2u] = x.z;
+            p.v[4u * q + 3u] = x.w;
+        }
+    } else {
+#pragma unroll
+        for (uint32_t s = 0; s < V; ++s)
+            if (j0 + s < NV) {
+                p.c4[s >> 2] |= (uint32_t)a.codes[j0 + s] << (8u * (s & 3u));
+                p.r4[s >> 2] |= (uint32_t)a.vb.round[j0 + s] << (8u * (s & 3u));
+                p.t4[s >> 2] |= (uint32_t)a.vb.type[j0 + s] << (8u * (s & 3u));
+                p.v[s] = a.vb.value[j0 + s];
+            }
+    }
+}
+
+template <uint32_t V, uint32_t WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void event_emit_stream(EvArgs a) {
+    constexpr uint32_t P = 64u * V; /* votes per pass */
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t n = a.vb.n_instances, NB = (n + EB - 1u) / EB, BS = gridDim.x * 4u;
     const uint64_t NV = a.vb.n_votes;
@@ -441,70 +490,78 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void e
     EvRaw NR = nb < NB ? ev_load(a, nb, lane) : EvRaw{0u, 0u};
     uint64_t ncnt = nb < NB ? a.offs[nb * EB] : 0u;
     uint64_t cnt = a.offs[B.s0]; /* the batch's first record */
-    uint64_t c = B.O0 & ~3ull;
-    Pass cur;
-    load_pass(a, c + 4u * lane, NV, cur);
+    uint64_t c = B.O0 & ~(uint64_t)(V - 1u);
+    PassV<V> cur;
+    load_pass_v<V>(a, c + V * lane, NV, cur);
     for (uint32_t k = lane; k < EB * keys; k += 64u) lab[k] = 0u; /* VoteCount::new: Value{} */
     __builtin_amdgcn_wave_barrier();
+    auto byte_at = [](const uint32_t (&w)[V / 4u], uint32_t s) -> uint32_t { return (w[s >> 2] >> (8u * (s & 3u))) & 0xFFu; };
     for (;;) {
-        uint64_t nc = c + 256u;
+        uint64_t nc = c + P;
         const bool sw = nc >= B.Om, last = sw && nb >= NB;
         EvBatch NBt = B;
         if (sw && !last) {
             NBt = ev_batch(a, nb, NR);
-            nc = NBt.O0 & ~3ull;
+            nc = NBt.O0 & ~(uint64_t)(V - 1u);
         }
-        Pass nxt;
-        if (!last) load_pass(a, nc + 4u * lane, NV, nxt);
+        PassV<V> nxt;
+        if (!last) load_pass_v<V>(a, nc + V * lane, NV, nxt);
         if (c < B.Om) {
             const uint64_t ol = ((uint64_t)B.ohi << 32) | B.olo;
             /* the pass's positions of the batch's votes, [lo, hi) (wave-uniform) */
             const uint32_t lo = B.O0 > c ? (uint32_t)(B.O0 - c) : 0u;
-            const uint32_t hi = B.Om - c < 256u ? (uint32_t)(B.Om - c) : 256u;
-            const uint32_t p0 = 4u * lane;
+            const uint32_t hi = B.Om - c < P ? (uint32_t)(B.Om - c) : P;
+            const uint32_t p0 = V * lane;
             /* per vote: batch instance (the count of the batch's later instances starting at
              * or before it: ballots over the offsets' lanes) */
-            uint32_t kk[4];
+            uint32_t kk[V];
             {
-                /* instances 1..m-1 starting inside (c, c + 256): few; every vote counts them */
-                const uint64_t st = __builtin_amdgcn_ballot_w64(lane >= 1u && lane < B.m && ol > c && ol < c + 256u);
+                /* instances 1..m-1 starting inside (c, c + P): few; every vote counts them */
+                const uint64_t st = __builtin_amdgcn_ballot_w64(lane >= 1u && lane < B.m && ol > c && ol < c + P);
                 const uint64_t pre = __builtin_amdgcn_ballot_w64(lane >= 1u && lane < B.m && ol <= c);
                 const uint32_t k0 = (uint32_t)__builtin_popcountll(pre);
 #pragma unroll
-                for (uint32_t s = 0; s < 4u; ++s) kk[s] = k0;
+                for (uint32_t s = 0; s < V; ++s) kk[s] = k0;
                 uint64_t rest = st;
                 while (rest) {
                     const uint32_t k = (uint32_t)__builtin_ctzll(rest);
                     rest &= rest - 1ull;
-                    const uint32_t ks = __builtin_amdgcn_readlane(B.olo, k) - (uint32_t)c; /* in (0, 256) */
+                    const uint32_t ks = __builtin_amdgcn_readlane(B.olo, k) - (uint32_t)c; /* in (0, P) */
 #pragma unroll
-                    for (uint32_t s = 0; s < 4u; ++s) kk[s] += (p0 + s >= ks) ? 1u : 0u;
+                    for (uint32_t s = 0; s < V; ++s) kk[s] += (p0 + s >= ks) ? 1u : 0u;
                 }
             }
-            /* the 4 votes' masks, bytewise: tallied (a batch vote, code not INVALID / REJECTED,
-             * type <= 1, round < max_rounds), with an event, with the RoundSkip bit */
-            uint32_t inm, hasm, skm;
+            /* the votes' masks, bit s = vote s: tallied (a batch vote, code not INVALID /
+             * REJECTED, type <= 1, round < max_rounds), with an event, with the RoundSkip bit */
+            uint32_t inm = 0, hasm = 0, skm = 0;
             {
-                const int l0 = min(max((int)lo - (int)p0, 0), 4), h0 = min(max((int)hi - (int)p0, 0), 4);
+                const int l0 = min(max((int)lo - (int)p0, 0), (int)V), h0 = min(max((int)hi - (int)p0, 0), (int)V);
                 const uint32_t inr = ((1u << h0) - 1u) & ~((1u << l0) - 1u);
-                const uint32_t e4 = cur.c4 & 0x07070707u;
-                const uint32_t okev = ~((e4 + 0x02020202u) >> 3) & 0x01010101u;
-                const uint32_t tx = cur.t4 & 0xFEFEFEFEu;
-                const uint32_t okt = ~((((tx & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | tx) >> 7) & 0x01010101u;
-                const uint32_t okr = (~(((cur.r4 | 0x80808080u) - R2 * 0x01010101u) | cur.r4) >> 7) & 0x01010101u;
                 auto nib = [](uint32_t x) { return ((x * 0x01020408u) >> 24) & 0xFu; };
-                inm = nib(okev & okt & okr) & inr;
-                hasm = inm & nib((e4 | (e4 >> 1) | (e4 >> 2)) & 0x01010101u);
-                skm = inm & nib((cur.c4 >> 3) & 0x01010101u);
+#pragma unroll
+                for (uint32_t q = 0; q < V / 4u; ++q) {
+                    const uint32_t e4 = cur.c4[q] & 0x07070707u;
+                    const uint32_t okev = ~((e4 + 0x02020202u) >> 3) & 0x01010101u;
+                    const uint32_t tx = cur.t4[q] & 0xFEFEFEFEu;
+                    const uint32_t okt = ~((((tx & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | tx) >> 7) & 0x01010101u;
+                    const uint32_t okr = (~(((cur.r4[q] | 0x80808080u) - R2 * 0x01010101u) | cur.r4[q]) >> 7) & 0x01010101u;
+                    const uint32_t in4 = nib(okev & okt & okr) << (4u * q);
+                    inm |= in4;
+                    hasm |= in4 & (nib((e4 | (e4 >> 1) | (e4 >> 2)) & 0x01010101u) << (4u * q));
+                    skm |= in4 & (nib((cur.c4[q] >> 3) & 0x01010101u) << (4u * q));
+                }
+                inm &= inr;
+                hasm &= inr;
+                skm &= inr;
             }
             const uint32_t n_rec = (uint32_t)__builtin_popcount(hasm) + (uint32_t)__builtin_popcount(skm);
-            uint32_t key[4], rid[4];
+            uint32_t key[V], rid[V];
             /* the run check: (instance, round) non-decreasing over the pass's tallied votes */
             uint32_t rmax = 0u, bad = 0u, rfirst = 0xFFFFFFFFu;
             uint32_t lv[2] = {0u, 0u}, lr[2] = {0u, 0u}, fr[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
 #pragma unroll
-            for (uint32_t s = 0; s < 4u; ++s) {
-                const uint32_t rb = (cur.r4 >> (8u * s)) & 0xFFu, tb = (cur.t4 >> (8u * s)) & 1u;
+            for (uint32_t s = 0; s < V; ++s) {
+                const uint32_t rb = byte_at(cur.r4, s), tb = byte_at(cur.t4, s) & 1u;
                 const bool in = (inm >> s) & 1u;
                 key[s] = in ? kk[s] * keys + rb * 2u + tb : 0xFFFFFFFFu;
                 /* run id + 1 (0: not tallied) */
@@ -522,7 +579,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void e
                 fr[1] = (nn && tb && fr[1] == 0xFFFFFFFFu) ? rid[s] : fr[1];
             }
             const uint32_t incl = wave_scan_incl(n_rec);
-            uint32_t slot[4] = {0u, 0u, 0u, 0u};
+            uint32_t slot[V];
+#pragma unroll
+            for (uint32_t s = 0; s < V; ++s) slot[s] = 0u;
             /* runs: one scan per type instead of a pass per key */
             const uint32_t pmax = from_prev(wave_max_incl(rmax), lane);
             bad |= (rfirst != 0xFFFFFFFFu && rfirst < pmax) ? 1u : 0u;
@@ -531,8 +590,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void e
                 uint32_t cr[2], cv[2], tail_nx[2];
 #pragma unroll
                 for (uint32_t t = 0; t < 2u; ++t) {
-                    const uint32_t P = lr[t] ? (lr[t] << 6) | lane : 0u;
-                    const uint32_t E = from_prev(wave_max_incl(P), lane);
+                    const uint32_t Pm = lr[t] ? (lr[t] << 6) | lane : 0u;
+                    const uint32_t E = from_prev(wave_max_incl(Pm), lane);
                     cr[t] = E >> 6;
                     cv[t] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((E & 63u) << 2), (int)lv[t]);
                     /* the next lane holding a non-nil vote of type t: its first run (a tail test) */
@@ -544,9 +603,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void e
                 /* per vote, in order: its own value, the run's last in this pass, or the carry */
                 uint32_t wr = 0u; /* votes that are the last non-nil of their (run, type) in the pass */
 #pragma unroll
-                for (uint32_t s = 0; s < 4u; ++s) {
+                for (uint32_t s = 0; s < V; ++s) {
                     if (rid[s]) {
-                        const uint32_t tb = (cur.t4 >> (8u * s)) & 1u;
+                        const uint32_t tb = byte_at(cur.t4, s) & 1u;
                         const uint32_t r_t = tb ? cr[1] : cr[0], v_t = tb ? cv[1] : cv[0];
                         if (cur.v[s] != AGNES_NIL) {
                             slot[s] = cur.v[s];
@@ -558,40 +617,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void e
                     }
                 }
                 /* a non-nil vote is its (run, type)'s last in the pass unless a later one of the
-                 * lane, or the next lane's first of that type, has the same run */
+                 * lane, or the next lane's first of that type, has the same run: scanning the
+                 * lane's votes backwards, the next non-nil vote of each type */
+                {
+                    uint32_t nx[2] = {tail_nx[0], tail_nx[1]};
 #pragma unroll
-                for (uint32_t s = 0; s < 4u; ++s) {
-                    if ((wr >> s) & 1u) {
-                        const uint32_t tb = (cur.t4 >> (8u * s)) & 1u;
-                        uint32_t nxr = tb ? tail_nx[1] : tail_nx[0];
-#pragma unroll
-                        for (uint32_t u = 3u; u > s; --u) {
-                            const uint32_t tu = (cur.t4 >> (8u * u)) & 1u;
-                            nxr = (((wr >> u) & 1u) && tu == tb) ? rid[u] : nxr;
+                    for (int s = (int)V - 1; s >= 0; --s) {
+                        if ((wr >> s) & 1u) {
+                            const uint32_t tb = byte_at(cur.t4, (uint32_t)s) & 1u;
+                            const uint32_t nxr = tb ? nx[1] : nx[0];
+                            if (nxr == rid[s]) wr &= ~(1u << s);
+                            if (tb) nx[1] = rid[s]; else nx[0] = rid[s];
                         }
-                        if (nxr == rid[s]) wr &= ~(1u << s);
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
 #pragma unroll
-                for (uint32_t s = 0; s < 4u; ++s)
+                for (uint32_t s = 0; s < V; ++s)
                     if ((wr >> s) & 1u) lab[key[s]] = cur.v[s];
                 __builtin_amdgcn_wave_barrier();
             } else {
                 /* rounds revisited inside the pass: one pass per (instance, round, type) present
                  * (round_votes.rs:50-54: the last non-nil value its bucket took) */
-                uint32_t pend = (key[0] != 0xFFFFFFFFu ? 1u : 0u) | (key[1] != 0xFFFFFFFFu ? 2u : 0u) |
-                                (key[2] != 0xFFFFFFFFu ? 4u : 0u) | (key[3] != 0xFFFFFFFFu ? 8u : 0u);
+                uint32_t pend = 0;
+#pragma unroll
+                for (uint32_t s = 0; s < V; ++s) pend |= (key[s] != 0xFFFFFFFFu ? 1u : 0u) << s;
                 for (;;) {
                     const uint64_t lm = __builtin_amdgcn_ballot_w64(pend != 0u);
                     if (!lm) break;
                     const uint32_t kl = (uint32_t)__builtin_ctzll(lm);
                     const uint32_t ks = (uint32_t)__builtin_ctz(__builtin_amdgcn_readlane(pend, kl));
-                    const uint32_t kv = ks == 0u ? key[0] : (ks == 1u ? key[1] : (ks == 2u ? key[2] : key[3]));
+                    uint32_t kv = key[0];
+#pragma unroll
+                    for (uint32_t s = 1; s < V; ++s) kv = ks == s ? key[s] : kv;
                     const uint32_t K = __builtin_amdgcn_readlane(kv, kl);
                     uint32_t inb = 0, lastv = 0, hasv = 0;
 #pragma unroll
-                    for (uint32_t s = 0; s < 4u; ++s) {
+                    for (uint32_t s = 0; s < V; ++s) {
                         const bool mm = key[s] == K;
                         inb |= mm ? 1u << s : 0u;
                         const bool nv = mm && cur.v[s] != AGNES_NIL;
@@ -605,7 +667,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void e
                     const uint32_t from_lane = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)lastv);
                     uint32_t run = bef ? from_lane : lab[K];
 #pragma unroll
-                    for (uint32_t s = 0; s < 4u; ++s) {
+                    for (uint32_t s = 0; s < V; ++s) {
                         if (key[s] == K) {
                             if (cur.v[s] != AGNES_NIL) run = cur.v[s];
                             slot[s] = run;
@@ -628,11 +690,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void e
             auto emit = [&](agnes_vote_event* dst) {
                 uint32_t o = incl - n_rec;
 #pragma unroll
-                for (uint32_t s = 0; s < 4u; ++s) {
+                for (uint32_t s = 0; s < V; ++s) {
                     const uint32_t two = ((skm >> s) & 1u) | (((hasm >> s) & 1u) << 1);
                     if (two) {
-                        const uint32_t cb = (cur.c4 >> (8u * s)) & 0xFFu, ev = cb & AGNES_CODE_EVENT_MASK;
-                        const uint32_t rb = (cur.r4 >> (8u * s)) & 0xFFu, msg = cb >> AGNES_CODE_MSG_SHIFT;
+                        const uint32_t cb = byte_at(cur.c4, s), ev = cb & AGNES_CODE_EVENT_MASK;
+                        const uint32_t rb = byte_at(cur.r4, s), msg = cb >> AGNES_CODE_MSG_SHIFT;
                         const uint64_t j = c + p0 + s;
                         const uint32_t inst = B.s0 + kk[s];
                         if (two & 1u) put(dst + o++, j, inst, AGNES_NIL, rb, AGNES_EV_ROUND_SKIP, msg);
@@ -726,13 +788,16 @@ hipError_t agnes_launch_events(const agnes_vote_batch* vb, const uint8_t* codes,
          * CU holds x 256 CUs), so each wave walks several batches and prefetches across them */
         const uint32_t NB = (n + EB - 1u) / EB;
         const size_t lds_s = (size_t)4u * (EB * a.keys + 6u * EV_STAGE) * sizeof(uint32_t);
+/* 4 votes per lane (256-vote passes).  8 (512-vote passes, 4 waves per SIMD)
+         * measured: C2 0.80 vs 0.78 ms, C3 2.94 vs 3.02, C4 1.90 vs ~1.4 (its next-round
+         * votes send more passes to the per-key path, and a wider pass holds more keys) */
+        const void* fn = reinterpret_cast<const void*>(&event_emit_stream<4u, 5u>);
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, event_emit_stream, 256, lds_s) != hipSuccess ||
-            per_cu < 1)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds_s) != hipSuccess || per_cu < 1)
             per_cu = 1;
         const uint32_t cap = EV_PREFETCH ? 256u * (uint32_t)per_cu : 0xFFFFFFFFu;
         const uint32_t sblocks = (NB + 3u) / 4u < cap ? (NB + 3u) / 4u : cap;
-        hipLaunchKernelGGL(event_emit_stream, dim3(sblocks), dim3(256), lds_s, st, a);
+        hipLaunchKernelGGL((event_emit_stream<4u, 5u>), dim3(sblocks), dim3(256), lds_s, st, a);
     } else if (a16) {
         /* one wave per instance, coalesced; the next pass of a long instance is loaded
          * while the current one is processed */
