@@ -289,6 +289,9 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
         for (uint64_t c = c0; c < I.end; c += CHUNK) {
             Chunk x;
             uint32_t val[VPL], t4;
+            /* raised priority while this chunk's loads, the gather and the next chunk's
+             * requests go out (same-box A/B: C4 tally_fast 0.797 -> 0.779 ms) */
+            __builtin_amdgcn_s_setprio(1);
             load_chunk(I, c, x, val, t4);
             const uint32_t p0 = 4u * lane;
             /* K1: w = power[set][validator] (consensus_executor.rs:62-63 -> validators.rs:7) */
@@ -328,6 +331,7 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
                     pf_at = ~0ull;
                 }
             }
+            __builtin_amdgcn_s_setprio(0);
 
             /* first-vote tables: atomic max of (epoch << lb | LMASK - local index), so
              * the earliest vote of the instance wins (DEDUP: per (round, type,

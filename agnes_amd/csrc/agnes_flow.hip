@@ -400,6 +400,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                 const uint32_t lo_r = rc == 0u ? lead : 0u; /* the chunk's active votes: lo_r .. hi_r */
                 if (pf_at != c) dma_chunk(c, lo_r, Lend - rc); /* not prefetched: a wave's first chunk */
                 dma_wait(); /* this chunk's DMA (and a new batch's States) have landed */
+                /* raised priority from here until the next chunk's DMA and the deferred code
+                 * store are out: a wave's memory traffic goes out ahead of the other waves'
+                 * K2-K4 work (same-box A/B: flow -1 % on C2 and C3) */
+                __builtin_amdgcn_s_setprio(1);
                 if (rc == 0u && lane < m) { /* instance records */
                     uint32_t* const rk = itab + RECW * lane;
                     rk[R_Q2] = q2k;
@@ -588,6 +592,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                                       "v"(w[6]), "v"(w[7]));
                 next_dma();
                 flush(); /* the previous chunk's codes */
+                __builtin_amdgcn_s_setprio(0);
 
                 /* ---- K2 + K3 ---- */
                 uint32_t* const A = crow + cpar * cw;
