@@ -1317,9 +1317,6 @@ static hipError_t launch_mode(const agnes_tally_args* a, uint32_t lpw, int num_c
             }
         }
     }
-#ifdef AGNES_EXP_NOTAIL
-    if (MODE == AGNES_MODE_REFERENCE && !SKIP) return e;
-#endif
     if (e == hipSuccess) {
         AgnesKt kt("tally_list", st);
         e = launch_k<true, MODE, SKIP, SM, true>(a, lpw, num_cus, st);

@@ -708,9 +708,6 @@ hipError_t agnes_launch_sweep(const agnes_tally_args* a, int num_cus, hipStream_
         e = agnes_launch_flow(a, num_cus, st);
     }
     if (e != hipSuccess) return e;
-#ifdef AGNES_EXP_NOTAIL
-    return e;
-#endif
     AgnesKt kt("sweep_walk", st);
     return sm ? launch_sweep_k<true>(a, num_cus, st) : launch_sweep_k<false>(a, num_cus, st);
 }
