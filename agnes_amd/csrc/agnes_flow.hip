@@ -88,6 +88,8 @@ __host__ __device__ inline uint32_t lds_bytes(bool sm, uint32_t R, bool evc = fa
     return F_BYTES + carry_bytes(R) + FB * RECW * 4u + (sm ? FB * 8u + 2u * FB * 64u : 0u) + (evc ? FB * 4u : 0u);
 }
 
+/* a State out (plain stores: non-temporal ones measured slower on C2) */
+__device__ __forceinline__ void st_out(uint4* p, uint4 v) { *p = v; }
 __device__ __forceinline__ uint32_t zero_marks(uint32_t x) { /* 0x80 in the bytes of x that are zero */
     const uint32_t t = (x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
     return ((t | x) & 0x80808080u) ^ 0x80808080u;
@@ -152,11 +154,13 @@ __device__ __forceinline__ void sdma_chunk(const void* bi, const void* bv, const
                    "s"(slotl + F_VALUE), "s"(slotl + F_VAL), "s"(slotl + F_ROUND), "s"(slotl + F_TYPE)
                  : "memory");
 }
+/* the codes are written once and not read again by the step: non-temporal stores
+ * (same-box A/B: C2 flow 0.643 -> 0.613 ms, C3 -1..3 %) */
 __device__ __forceinline__ void sstore4(void* base, uint32_t voff, uint32_t d) {
-    asm volatile("global_store_dword %0, %1, %2" ::"v"(voff), "v"(d), "s"(base) : "memory");
+    asm volatile("global_store_dword %0, %1, %2 nt" ::"v"(voff), "v"(d), "s"(base) : "memory");
 }
 __device__ __forceinline__ void sstore8(void* base, uint32_t voff, uint32_t d0, uint32_t d1) {
-    asm volatile("global_store_dwordx2 %0, %1, %2" ::"v"(voff), "v"(u64of(d0, d1)), "s"(base) : "memory");
+    asm volatile("global_store_dwordx2 %0, %1, %2 nt" ::"v"(voff), "v"(u64of(d0, d1)), "s"(base) : "memory");
 }
 
 /* a batch: instances [s0, e0).  Its header is built in three stages, each one
@@ -346,8 +350,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
             sp[13] = fl;
         }
         __builtin_amdgcn_wave_barrier();
-        for (uint32_t j = lane; j < 4u * mm; j += 64u)
-            reinterpret_cast<uint4*>(a.states + s0)[j] = *reinterpret_cast<const uint4*>(sbp + 16u * j);
+        for (uint32_t j = lane; j < 4u * mm; j += 64u) st_out(reinterpret_cast<uint4*>(a.states + s0) + j,
+                                                             *reinterpret_cast<const uint4*>(sbp + 16u * j));
     };
 
     Hdr H, N;
@@ -971,7 +975,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
             if (smf) { /* no vote: the States as they came */
                 dma_wait();
                 for (uint32_t j = lane; j < 4u * m; j += 64u)
-                    reinterpret_cast<uint4*>(a.states + H.s0)[j] = *reinterpret_cast<const uint4*>(sbh + 16u * j);
+                    st_out(reinterpret_cast<uint4*>(a.states + H.s0) + j, *reinterpret_cast<const uint4*>(sbh + 16u * j));
             } else {
                 finalize(m, H.s0, sbh);
             }
