@@ -127,9 +127,9 @@ __device__ __forceinline__ uint64_t count_records(const EvArgs& a, uint32_t i) {
 /* the counts of the instances a tally's flow kernel handed to its walk list (the
  * flow kernel counted every other one itself): a grid-stride loop over the list */
 template <uint32_t W>
-__global__ __launch_bounds__(64) void event_count_list(EvArgs a, const uint32_t* walk, const uint32_t* walk_n) {
+__global__ __launch_bounds__(256) void event_count_list(EvArgs a, const uint32_t* walk, const uint32_t* walk_n) {
     const uint32_t L = *(volatile const uint32_t*)walk_n;
-    for (uint32_t k = blockIdx.x * 64u + threadIdx.x; k < L; k += gridDim.x * 64u) {
+    for (uint32_t k = blockIdx.x * 256u + threadIdx.x; k < L; k += gridDim.x * 256u) {
         const uint32_t i = walk[k];
         a.offs[i + 1u] = count_records<W>(a, i);
     }
@@ -747,15 +747,16 @@ hipError_t agnes_launch_event_count_list(const agnes_vote_batch* vb, const uint8
     const uint32_t n = vb->n_instances;
     if (n == 0) return hipSuccess;
     EvArgs a{*vb, codes, offs, nullptr, 0u};
-    /* the list is usually empty: a small grid that strides over it */
-    uint32_t blocks = (n + 63u) / 64u;
-    const uint32_t cap = 4u * (uint32_t)(num_cus > 0 ? num_cus : 256);
+    /* the list is usually empty: a small grid (a block of 256 lanes per CU) that
+     * strides over it */
+    uint32_t blocks = (n + 255u) / 256u;
+    const uint32_t cap = (uint32_t)(num_cus > 0 ? num_cus : 256);
     if (blocks > cap) blocks = cap;
     AgnesKt kt("event_count_list", st);
     if ((reinterpret_cast<uintptr_t>(codes) & 15u) == 0u)
-        hipLaunchKernelGGL((event_count_list<64u>), dim3(blocks), dim3(64), 0, st, a, walk, walk_n);
+        hipLaunchKernelGGL((event_count_list<64u>), dim3(blocks), dim3(256), 0, st, a, walk, walk_n);
     else
-        hipLaunchKernelGGL((event_count_list<4u>), dim3(blocks), dim3(64), 0, st, a, walk, walk_n);
+        hipLaunchKernelGGL((event_count_list<4u>), dim3(blocks), dim3(256), 0, st, a, walk, walk_n);
     return hipGetLastError();
 }
 
