@@ -363,8 +363,12 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
         const uint32_t route = (cfg->flags >> AGNES_ROUTE_SHIFT) & AGNES_ROUTE_MASK;
         const bool flow = !wide_all && route == AGNES_ROUTE_AUTO && cfg->mode == AGNES_MODE_REFERENCE &&
                           !(cfg->flags & AGNES_FLAG_ROUND_SKIP) && agnes_flow_counts_events(cfg->flags, cfg->max_rounds);
-        if (flow) a.ev_counts = ev_counts;
-        if (counted) *counted = flow;
+        /* DEDUP / RoundSkip on the stream kernel: it counts too (the LIST kernel's
+         * instances go on the walk list, counted after their codes) */
+        const bool dfl = !wide_all && (cfg->mode == AGNES_MODE_DEDUP || (cfg->flags & AGNES_FLAG_ROUND_SKIP)) &&
+                         agnes_dflow_route(&a);
+        if (flow || dfl) a.ev_counts = ev_counts;
+        if (counted) *counted = flow || dfl;
     }
     return status_of(agnes_launch_tally(&a, cfg->mode, c->num_cus, wide_all, st));
 }
@@ -403,6 +407,9 @@ int agnes_tally_partials(agnes_ctx* c, const agnes_config* cfg, const agnes_vote
         return AGNES_E_INVALID;
     if (cfg->mode != AGNES_MODE_REFERENCE || (cfg->flags & (AGNES_FLAG_ROUND_SKIP | AGNES_FLAG_STATE_MACHINE)))
         return AGNES_E_UNSUPPORTED;
+    /* the partials gather the power table; caller weights (carried's has_w validity
+     * rules: no valid validator or set needed) are not what pass A computes */
+    if (b->weight) return AGNES_E_UNSUPPORTED;
     if (b->n_votes >= 0xFFFFFFFFull || cfg->max_rounds > 1024u) /* LDS: 48 B per round */
         return AGNES_E_UNSUPPORTED;
     if ((uintptr_t)weights & 7u) return AGNES_E_INVALID;

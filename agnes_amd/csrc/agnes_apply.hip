@@ -157,7 +157,7 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
         if (set < ns) {
             const agnes_set_info si = a.sets[set];
             const uint64_t len = hi - lo;
-            if (!si.fast || len >= (1ull << 32) || len * (uint64_t)si.maxpow >= (1ull << 31)) return;
+            if (fast::defer_to_list(si.fast, si.maxpow, len)) return;
         }
     }
 

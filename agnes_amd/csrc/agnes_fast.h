@@ -24,6 +24,14 @@ constexpr uint32_t NONE = 0xFFFFFFFFu;
                             * over-fetched tail of a chunk is re-read as the next instance's start) */
 #endif
 
+/* The u32 domain of the fast kernels, per instance: every power of its set in [0, 2^31),
+ * fewer than 2^30 votes and len * maxpow < 2^31, so no running sum reaches 2^31.  An
+ * instance outside it goes to the i64 LIST kernel; the u32 tally kernels and the apply
+ * pass (agnes_apply.hip), which skips the LIST kernel's instances, test it alike. */
+__host__ __device__ __forceinline__ bool defer_to_list(uint32_t fast, uint32_t maxpow, uint64_t len) {
+    return !fast || len >= (1ull << 30) || len * (uint64_t)maxpow >= (1ull << 31);
+}
+
 /* LDS-DMA prefetch buffer of one chunk: instance, value, validator (1 KiB each,
  * lane l's 16 B at 16 l), round, type (256 B each, lane l's 4 B at 4 l) */
 constexpr uint32_t PF_INST = 0, PF_VALUE = 1024, PF_VAL = 2048, PF_ROUND = 3072, PF_TYPE = 3328,

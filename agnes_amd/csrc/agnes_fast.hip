@@ -253,7 +253,7 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
         if (I.set_ok) {
             const agnes_set_info si = a.sets[set];
             /* sums provably < 2^31 (u32 arithmetic), else the i64 LIST kernel */
-            if (!si.fast || len >= (1ull << 32) || len * (uint64_t)si.maxpow >= (1ull << 31)) {
+            if (defer_to_list(si.fast, si.maxpow, len)) {
                 if (lane == 0) a.list[atomicAdd(a.list_count, 1u)] = I.i;
                 run = false;
             }

@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
@@ -96,6 +97,10 @@ struct agnes_multi {
     uint32_t n_vals = 0;
     uint32_t xmode = AGNES_MULTI_EXCHANGE_AUTO;
     std::vector<ncclComm_t> comms; /* one rank per device (RCCL exchanges), created on first use */
+    bool comms_dead = false;       /* a collective failed on some rank: aborted, rebuilt on the next call */
+    std::atomic<bool> rccl_checked{false};     /* the first RCCL all-gather was compared with the host exchange */
+    std::atomic<bool> rccl_bad{false};         /* ... and differed: the host exchange from then on */
+    std::vector<int> xerr;         /* per device: its status entering an RCCL exchange (host agreement) */
     agnes::multi::Barrier bar;
     std::vector<unsigned char*> stage; /* pinned host staging of the host exchange, per device */
     std::vector<uint64_t> stage_cap;
@@ -249,20 +254,76 @@ int stage_grow(agnes_multi* m, uint32_t d, uint64_t bytes) {
 /* in place on the device (count int64 / u64 elements); X_GATHER: count elements per
  * device from send into recv (D * count, device order).  Every thread reaches every
  * barrier, also after an error (it then reports the error). */
-int exchange(agnes_multi* m, uint32_t d, XOp op, const int64_t* send, int64_t* recv, uint64_t count) {
+/* RCCL: the device threads agree on every status before and after a collective is
+ * enqueued.  A thread that has already failed (a hipMalloc, a launch) never issues a
+ * collective on its unfilled buffers, and nor does any other thread -- their matching
+ * collectives would wait forever; a collective one rank could not enqueue aborts every
+ * communicator (the others' enqueued halves are cancelled), and the next call rebuilds
+ * them.  `mine` is the calling thread's status so far. */
+bool agree_ok(agnes_multi* m, uint32_t d, int mine) {
+    m->xerr[d] = mine;
+    m->bar.wait();
+    bool ok = true;
+    for (int e : m->xerr) ok = ok && e == AGNES_OK;
+    m->bar.wait(); /* every thread has read xerr before it is written again */
+    return ok;
+}
+
+/* The first RCCL all-gather of a handle is checked against the same gather through
+ * pinned host memory (the multi-device RCCL path has not run on hardware in this
+ * repository's tests, which share one device): every thread compares its received
+ * rows with every device's staged send buffer.  A mismatch anywhere makes every
+ * thread take the host rows and the handle use the host exchange from then on. */
+int check_gather(agnes_multi* m, uint32_t d, const int64_t* send, int64_t* recv, uint64_t count) {
+    Dev& dv = m->dev[d];
+    const uint32_t D = (uint32_t)m->dev.size();
+    const uint64_t bytes = 8u * count;
+    int rc = stage_grow(m, d, bytes);
+    std::vector<int64_t> got((size_t)D * count);
+    if (rc == AGNES_OK && hipMemcpyAsync(m->stage[d], send, bytes, hipMemcpyDeviceToHost, dv.st) != hipSuccess)
+        rc = AGNES_E_DEVICE;
+    if (rc == AGNES_OK && hipMemcpyAsync(got.data(), recv, D * bytes, hipMemcpyDeviceToHost, dv.st) != hipSuccess)
+        rc = AGNES_E_DEVICE;
+    if (rc == AGNES_OK && hipStreamSynchronize(dv.st) != hipSuccess) rc = AGNES_E_DEVICE;
+    if (!agree_ok(m, d, rc)) return rc != AGNES_OK ? rc : AGNES_E_DEVICE; /* every stage written */
+    bool same = true;
+    for (uint32_t k = 0; k < D; ++k)
+        same = same && std::memcmp(got.data() + (size_t)k * count, m->stage[k], bytes) == 0;
+    const bool all_same = agree_ok(m, d, same ? AGNES_OK : AGNES_E_DEVICE);
+    if (!all_same) {
+        for (uint32_t k = 0; k < D && rc == AGNES_OK; ++k)
+            if (hipMemcpyAsync(recv + k * count, m->stage[k], bytes, hipMemcpyHostToDevice, dv.st) != hipSuccess)
+                rc = AGNES_E_DEVICE;
+        if (rc == AGNES_OK && hipStreamSynchronize(dv.st) != hipSuccess) rc = AGNES_E_DEVICE;
+        if (d == 0u) m->rccl_bad = true;
+    }
+    m->bar.wait(); /* the stages are free again; every thread has seen rccl_bad */
+    if (d == 0u) m->rccl_checked = true;
+    return rc;
+}
+
+int exchange(agnes_multi* m, uint32_t d, XOp op, const int64_t* send, int64_t* recv, uint64_t count, int mine) {
     Dev& dv = m->dev[d];
     const uint32_t D = (uint32_t)m->dev.size();
     if (!m->comms.empty()) {
+        if (!agree_ok(m, d, mine)) return mine != AGNES_OK ? mine : AGNES_E_DEVICE;
         ncclResult_t r;
         if (op == X_GATHER)
             r = ncclAllGather(send, recv, count, ncclInt64, m->comms[d], dv.st);
         else
             r = ncclAllReduce(send, recv, count, op == X_MIN_U64 ? ncclUint64 : ncclInt64,
                               op == X_MAX_I64 ? ncclMax : ncclMin, m->comms[d], dv.st);
-        return r == ncclSuccess ? AGNES_OK : AGNES_E_DEVICE;
+        const int rc = r == ncclSuccess ? AGNES_OK : AGNES_E_DEVICE;
+        if (!agree_ok(m, d, rc)) {
+            (void)ncclCommAbort(m->comms[d]);
+            m->comms_dead = true;
+            return AGNES_E_DEVICE;
+        }
+        if (op == X_GATHER && !m->rccl_checked) return check_gather(m, d, send, recv, count);
+        return AGNES_OK;
     }
     const uint64_t bytes = 8u * count;
-    int rc = stage_grow(m, d, bytes);
+    int rc = mine != AGNES_OK ? mine : stage_grow(m, d, bytes);
     if (rc == AGNES_OK && hipMemcpyAsync(m->stage[d], send, bytes, hipMemcpyDeviceToHost, dv.st) != hipSuccess)
         rc = AGNES_E_DEVICE;
     if (rc == AGNES_OK && hipStreamSynchronize(dv.st) != hipSuccess) rc = AGNES_E_DEVICE;
@@ -418,7 +479,7 @@ int run_one(agnes_multi* m, uint32_t d, const agnes_config* cfg, const agnes_vot
         OCALL(agnes_dedup_first(dv.ctx, &dcfg, &sl, lo, b.first, dv.st));
         OTRY(hipStreamSynchronize(dv.st));
         OXCH(exchange(m, d, X_MIN_U64, reinterpret_cast<const int64_t*>(b.first), reinterpret_cast<int64_t*>(b.first),
-                      (uint64_t)K * m->n_vals));
+                      (uint64_t)K * m->n_vals, rc));
         OCALL(agnes_dedup_mask(dv.ctx, &dcfg, &sl, lo, b.first, b.tmask, dv.st));
         seg.type = b.tmask;
     }
@@ -429,7 +490,7 @@ int run_one(agnes_multi* m, uint32_t d, const agnes_config* cfg, const agnes_vot
     OTRY(hipStreamSynchronize(dv.st));
     /* the exchange: every slice's total to every device */
     OXCH(exchange(m, d, X_GATHER, reinterpret_cast<const int64_t*>(b.mine), reinterpret_cast<int64_t*>(b.ranks),
-                  3ull * K));
+                  3ull * K, rc));
     /* the slices before each device, then before each segment: pass B's carry-ins */
     OCALL(agnes_fold_counts(dv.ctx, b.ranks, D, K, nullptr, b.fin,
                             AGNES_FOLD_APPLY | AGNES_FOLD_CARRY_ZERO_NONE | AGNES_FOLD_TOTAL_ZERO_LABELS, dv.st));
@@ -447,10 +508,10 @@ int run_one(agnes_multi* m, uint32_t d, const agnes_config* cfg, const agnes_vot
         OTRY(hipMemcpyAsync(b.marks, init, sizeof(init), hipMemcpyHostToDevice, dv.st));
         OCALL(agnes_one_sm_scan(dv.ctx, &scfg, &sl, lo, b.codes, b.state, b.marks, dv.st));
         OTRY(hipStreamSynchronize(dv.st));
-        OXCH(exchange(m, d, X_MIN_I64, b.marks, b.marks, 2u));
+        OXCH(exchange(m, d, X_MIN_I64, b.marks, b.marks, 2u, rc));
         OCALL(agnes_one_sm_apply(dv.ctx, &scfg, &sl, lo, b.codes, b.state, b.marks, dv.st));
         OTRY(hipStreamSynchronize(dv.st));
-        OXCH(exchange(m, d, X_MAX_I64, b.marks + 2, b.marks + 2, 2u));
+        OXCH(exchange(m, d, X_MAX_I64, b.marks + 2, b.marks + 2, 2u, rc));
         OCALL(agnes_one_sm_finish(dv.ctx, b.marks, b.state, dv.st));
     }
     OTRY(hipStreamSynchronize(dv.st));
@@ -489,11 +550,18 @@ int ensure_exchange(agnes_multi* m) {
         m->stage_cap.assign(D, 0);
     }
     m->bar.n = D;
+    m->xerr.assign(D, AGNES_OK);
+    if (m->comms_dead) { /* a collective failed in an earlier call: its communicators were aborted */
+        for (ncclComm_t c : m->comms) (void)ncclCommDestroy(c);
+        m->comms.clear();
+        m->comms_dead = false;
+    }
     bool distinct = true;
     for (uint32_t i = 0; i < D; ++i)
         for (uint32_t j = i + 1; j < D; ++j)
             if (m->dev[i].device == m->dev[j].device) distinct = false;
-    const bool want = m->xmode == AGNES_MULTI_EXCHANGE_RCCL || (m->xmode == AGNES_MULTI_EXCHANGE_AUTO && distinct && D > 1);
+    const bool want = !m->rccl_bad && (m->xmode == AGNES_MULTI_EXCHANGE_RCCL ||
+                                       (m->xmode == AGNES_MULTI_EXCHANGE_AUTO && distinct && D > 1));
     if (!want) {
         for (ncclComm_t c : m->comms) (void)ncclCommDestroy(c);
         m->comms.clear();

@@ -39,10 +39,13 @@ KERNEL_BYTES_PER_VOTE = {
     "flow": 15,          # instance, value, validator u32 + round, type u8 in; code u8 out
     "tally_fast": 15,
     "tally_wide": 15,
+    "tally_list": 15,    # the i64 kernel over the instances the u32 kernels hand over (c2w: all)
+    "sweep_walk": 15,
     "apply_codes": 2,    # code + round u8 in (+ the message bytes written back)
     "dedup_first": 10,   # C5 DEDUP: instance, validator u32 + round, type u8 in (+ 8 B atomic per key)
     "dedup_mask": 11,    # the same in, the masked type u8 out
-    "partials": 30,      # C5 pass A: the 14 B in + the gathered i64 weight + the weight column out
+    "partials": 22,      # C5 pass A: the 14 B in + the i64 weight column out (the power table
+                         # gather hits the cache-resident table: not compulsory HBM traffic)
 }
 # C5 pass B reads the weight column pass A wrote (AGNES_FLAG_WEIGHTS_CACHED) on top of the 15 B
 C5_PASS_B_BYTES_PER_VOTE = 23
@@ -50,7 +53,7 @@ C5_PASS_B_BYTES_PER_VOTE = 23
 # read and written once per step (64-B agnes_state in, 64 B out) by the kernel that
 # applies the events (flow on the fused route, apply_codes on the split one)
 STATE_BYTES_PER_INSTANCE = 128
-KERNEL_STATE_IO = {"flow", "apply_codes"}
+KERNEL_STATE_IO = {"flow", "apply_codes", "tally_list", "sweep_walk"}
 KERNEL_SYMBOLS = {
     # template parameters: PC (power table in LDS), SM (State machine), R1 (one round);
     # c2 runs flow<true, true, true>, c3 flow<false, true, false> (rocprofv3 names them)
@@ -58,6 +61,7 @@ KERNEL_SYMBOLS = {
     "sweep_walk": "agnes::sweep::sweep<PC, SM>",
     "tally_fast": "agnes::fast::tally_fast<...>",
     "tally_wide": "agnes::tally_kernel<true, ...>",
+    "tally_list": "agnes::tally_kernel<true, MODE, SKIP, SM, LIST=true>",
     "apply_codes": "agnes::apply::apply_codes<RoundSkip>",
     "partials": "agnes::partials::partials_kernel",
     "dedup_first": "agnes::dedup::first_kernel",
@@ -78,6 +82,23 @@ WORKLOADS = {
                         nil_permille=300),
                power=(abi.POWER_UNIFORM, 1, 1000, 1024), mode=abi.MODE_REFERENCE,
                flags=abi.FLAG_STATE_MACHINE, max_rounds=4, scaling="strong"),
+    # one C3 rank's share on 8 GPUs (125k instances, global ids 0..125k): the strong-scaling
+    # shard size, measured on one GPU (queue tail and per-wave imbalance at 1/8 the work)
+    "c3shard": dict(desc="C3 8-GPU shard: 125k instances x 150 validators x 1..4 rounds, 30% nil, "
+                         "1024 power sets (one rank's share of C3 on 8 GPUs)",
+                    gen=dict(n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4,
+                             nil_permille=300),
+                    power=(abi.POWER_UNIFORM, 1, 1000, 1024), mode=abi.MODE_REFERENCE,
+                    flags=abi.FLAG_STATE_MACHINE, max_rounds=4, scaling="weak"),
+    # the C2 shape with i64 stakes: powers U[2^28, 2^34], set totals ~8.6e11 > 2^32 (the
+    # reference's i64 arithmetic, round_votes.rs:9,16-18,31-33), through the route the
+    # engine picks for a set outside the u32 domain
+    "c2w": dict(desc="C2x100 with i64 stakes: 1M instances x 100 validators x 1 round, powers "
+                     "U[2^28, 2^34] (set totals > 2^32), 80/20 value/nil, shuffled",
+                gen=dict(n_instances=10_000 * 100, n_vals=100, rounds_min=1, rounds_max=1,
+                         nil_permille=200),
+                power=(abi.POWER_UNIFORM, 1 << 28, 1 << 34, 1), mode=abi.MODE_REFERENCE,
+                flags=abi.FLAG_STATE_MACHINE, max_rounds=1, scaling="weak"),
     "c4": dict(desc="C4: C3 shape per rank (125k instances), Zipf power, 10% dup + 10% "
                     "equivocation + 5% next-round votes, DEDUP + RoundSkip",
                gen=dict(n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4,

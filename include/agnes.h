@@ -349,8 +349,10 @@ int agnes_tally_carried(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vot
  * thresholds and the codes.  weights (DEVICE, i64 [n_votes], or NULL): each vote's
  * weight, 0 for a vote that is not valid; pass B then runs agnes_tally_carried with
  * batch->weight = weights and AGNES_FLAG_WEIGHTS_CACHED.  The configurations, the
- * validity rules and AGNES_FLAG_ONE_INSTANCE are agnes_tally_carried's; the batch's
- * columns need no alignment; n_votes < 2^32 - 1.  Asynchronous on `stream`. */
+ * validity rules and AGNES_FLAG_ONE_INSTANCE are agnes_tally_carried's, except that
+ * the weights always come from the power table: a batch with caller weights
+ * (batch->weight != NULL) is AGNES_E_UNSUPPORTED.  The batch's columns need no
+ * alignment; n_votes < 2^32 - 1.  Asynchronous on `stream`. */
 int agnes_tally_partials(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
                          agnes_vote_count* counts, int64_t* weights, void* stream);
 

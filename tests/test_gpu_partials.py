@@ -104,6 +104,20 @@ def test_partials_equal_carried_pass_a(eng, one, segs, R, n_sets):
     assert (k1.cpu().numpy() == abi.CODE_INVALID).sum() == bad1
 
 
+def test_partials_refuse_caller_weights(eng):
+    """Pass A gathers the power table; a batch with caller weights (which carried
+    accepts without a valid validator or set) is refused, not silently mis-tallied."""
+    from agnes_amd.lib import AgnesError
+    hb = _batch(5, 20, 40, 2)
+    eng.upload_power(ol.gen_power(5, 1, 40, abi.POWER_UNIFORM, 1, 100))
+    db = DeviceBatch.from_host(hb, eng.device)
+    w = torch.ones(hb.n_votes, dtype=torch.int64, device=eng.device)
+    counts = torch.empty((hb.n_instances, 4, 3), dtype=torch.int64, device=eng.device)
+    with pytest.raises(AgnesError) as ex:
+        eng.tally_partials(abi.Config(abi.MODE_REFERENCE, 0, 2, 0), dataclasses.replace(db, weight=w), counts)
+    assert ex.value.rc == abi.E_UNSUPPORTED
+
+
 @pytest.mark.parametrize("dedup", [False, True])
 def test_c5_split_with_partials_equals_checker(eng, dedup):
     """tally_one_instance[_dedup] with pass A as the reduction and pass B over the

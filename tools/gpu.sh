@@ -1,14 +1,15 @@
 #!/bin/bash
-# Run one command on the GPU box via gpurun; clears the named output files first,
-# retries ONLY when gpurun reports an infrastructure-transient status (nothing ran).
-# usage: tools/gpu.sh TIMEOUT "command" [files to clear...]
-T=$1; CMD=$2; shift 2
-for f in "$@"; do rm -f "/root/repo/gpurun_out/$f"; done
-for attempt in 1 2 3 4 5 6 7 8; do
+# Run one command on the GPU box via gpurun; retries ONLY when gpurun reports an
+# infrastructure-transient status (nothing ran, nothing charged): no box free, back-off.
+# usage: tools/gpu.sh TIMEOUT "command" [max attempts]
+T=$1; CMD=$2; MAXA=${3:-30}
+for attempt in $(seq 1 $MAXA); do
   /usr/local/graft/bin/gpurun --timeout "$T" -- "$CMD" > /root/repo/gpurun_out/call.log 2>&1
   rc=$?
-  if grep -q "status=transient\|backing off\|busy" /root/repo/gpurun_out/call.log; then
-    echo "[gpu.sh] transient (attempt $attempt), waiting"; sleep 90; continue
+  if grep -q "status=transient\|backing off\|no free box\|busy" /root/repo/gpurun_out/call.log; then
+    w=$(grep -o "retry in [0-9]*s" /root/repo/gpurun_out/call.log | grep -o "[0-9]*" | head -1); w=${w:-120}
+    [ "$w" -lt 60 ] && w=60
+    echo "[gpu.sh] transient (attempt $attempt), waiting ${w}s"; sleep $w; continue
   fi
   break
 done
