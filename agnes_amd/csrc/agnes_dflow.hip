@@ -54,8 +54,28 @@
  * machine runs in the apply pass over the codes (agnes_apply.hip).
  */
 #include <type_traits>
+#include <vector>
+#include <cstdio>
 
 #include "agnes_fast.h"
+
+/* AGNES_DFLOW_CHECK (development builds only): every global access bounds-checked; a
+ * violation is printed and the access skipped */
+#ifndef AGNES_DFLOW_CHECK
+#define AGNES_DFLOW_CHECK 0
+#endif
+#if AGNES_DFLOW_CHECK
+#include <cstdio>
+__device__ unsigned agnes_dflow_nbad;
+__device__ __noinline__ bool agnes_dflow_bad(int tag, unsigned long long x, unsigned long long y) {
+    if (atomicAdd(&agnes_dflow_nbad, 1u) < 48u)
+        printf("dflow OOB tag %d x %llu lim %llu block %u thread %u\n", tag, x, y, blockIdx.x, threadIdx.x);
+    return false;
+}
+#define DCHK(c, tag, x, y) ((c) || agnes_dflow_bad(tag, (unsigned long long)(x), (unsigned long long)(y)))
+#else
+#define DCHK(c, tag, x, y) true
+#endif
 
 namespace agnes {
 namespace dflow {
@@ -266,14 +286,14 @@ __global__ __launch_bounds__(256) void dflow(agnes_tally_args a, uint32_t lds_pe
         const uint32_t m = h.e0 - h.s0;
         uint32_t lo = 0, hi = 0, hs = 0;
         if (m > 0u && lane <= m) {
-            const uint64_t o = a.vb.offsets[h.s0 + lane];
+            const uint64_t o = DCHK(h.s0 + lane <= n, 1, h.s0 + lane, n) ? a.vb.offsets[h.s0 + lane] : 0ull;
             const uint64_t oc = o < NV ? o : NV;
             lo = (uint32_t)oc;
             hi = (uint32_t)(oc >> 32);
         }
         if (lane < m) {
             const uint32_t k = h.s0 + lane;
-            hs = a.vb.instance_set ? a.vb.instance_set[k] : (ns ? k % ns : 0u);
+            hs = a.vb.instance_set ? (DCHK(k < n, 2, k, n) ? a.vb.instance_set[k] : 0u) : (ns ? k % ns : 0u);
         }
         h.olo = lo;
         h.ohi = hi;
@@ -289,7 +309,7 @@ __global__ __launch_bounds__(256) void dflow(agnes_tally_args a, uint32_t lds_pe
         const uint64_t len = il && oe > ob ? oe - ob : 0ull;
         h.ln = len < (1ull << 31) ? (uint32_t)len : (1u << 31);
         uint32_t q2 = 0, q1 = 0, mp = 0, fa = 2;
-        if (il && h.hs < ns) {
+        if (il && h.hs < ns && DCHK(h.hs < ns, 3, h.hs, ns)) {
             const agnes_set_info* const si = a.sets + h.hs;
             q2 = si->q2;
             q1 = si->q1;
@@ -338,7 +358,7 @@ __global__ __launch_bounds__(256) void dflow(agnes_tally_args a, uint32_t lds_pe
         lo = rfl(lo);
         lim = rfl(lim);
         __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): the slot's LDS reads are done */
-        if (lo == 0u && lim >= CH && c + CH <= NV) {
+        if (lo == 0u && lim >= CH && c + CH <= NV && DCHK(c + CH <= NV, 4, c + CH, NV)) {
             sdma_chunk(a.vb.instance + c, a.vb.value + c, a.vb.validator + c, a.vb.round + c, a.vb.type + c, o16, o4,
                        slotl);
         } else { /* a stream's first or last chunk: the 4-vote groups that hold active votes;
@@ -346,7 +366,7 @@ __global__ __launch_bounds__(256) void dflow(agnes_tally_args a, uint32_t lds_pe
             for (uint32_t hf = 0; hf < 2u; ++hf) {
                 const uint32_t g = 256u * hf + 4u * lane;
                 if (g + 4u > lo && g < lim) {
-                    if (c + g + 4u <= NV) {
+                    if (c + g + 4u <= NV && DCHK(c + g + 4u <= NV, 5, c + g + 4u, NV)) {
                         sdma16(a.vb.instance + c + 256u * hf, o16, slotl + F_INST + 1024u * hf);
                         sdma16(a.vb.value + c + 256u * hf, o16, slotl + F_VALUE + 1024u * hf);
                         sdma16(a.vb.validator + c + 256u * hf, o16, slotl + F_VAL + 1024u * hf);
@@ -381,11 +401,11 @@ __global__ __launch_bounds__(256) void dflow(agnes_tally_args a, uint32_t lds_pe
     uint32_t dc0 = 0, dc1 = 0, dc_act = 0; /* dc_act: byte mask (bit s: vote s) of the lane's votes to write */
     auto flush = [&]() {
         if (dc_at != ~0ull) {
-            if (dc_act == 0xFFu) {
+            if (dc_act == 0xFFu && DCHK(dc_at + o8 + 8u <= NV, 6, dc_at + o8 + 8u, NV)) {
                 sstore8(a.codes + rfl64(dc_at), o8, dc0, dc1);
             } else if (dc_act) {
                 for (uint32_t s = 0; s < LV; ++s)
-                    if ((dc_act >> s) & 1u) a.codes[dc_at + o8 + s] = (uint8_t)bsel(s < 4u ? dc0 : dc1, s);
+                    if (((dc_act >> s) & 1u) && DCHK(dc_at + o8 + s < NV, 7, dc_at + o8 + s, NV)) a.codes[dc_at + o8 + s] = (uint8_t)bsel(s < 4u ? dc0 : dc1, s);
             }
             dc_at = ~0ull;
         }
@@ -423,7 +443,7 @@ __global__ __launch_bounds__(256) void dflow(agnes_tally_args a, uint32_t lds_pe
         const uint64_t NE = ballot(lane < m && rn > rl) & mm64; /* instances with votes */
         const uint32_t relv = lane <= m ? rl : 0x7FFFFFFFu;
         /* the instance records */
-        if (lane < m) {
+        if (lane < m && DCHK(S.s0 + lane < n, 8, S.s0 + lane, n)) {
             uint32_t* const rk = IT + RW * lane;
             const bool set_ok = S.hs < ns;
             rk[R_Q2] = S.q2;
@@ -445,7 +465,8 @@ __global__ __launch_bounds__(256) void dflow(agnes_tally_args a, uint32_t lds_pe
                 rk[R_SK] = 0u;
             }
             if (S.def && rn > rl) {
-                a.list[atomicAdd(a.list_count, 1u)] = S.s0 + lane;
+                const uint32_t li = atomicAdd(a.list_count, 1u);
+                if (DCHK(li < n, 9, li, n)) a.list[li] = S.s0 + lane;
                 /* (agnes_tally_events) its records are counted after the LIST kernel's codes */
                 if (EVC) a.walk[atomicAdd(a.list_count + AGNES_WALK_COUNT, 1u)] = S.s0 + lane;
             }
@@ -560,7 +581,8 @@ __global__ __launch_bounds__(256) void dflow(agnes_tally_args a, uint32_t lds_pe
                     okb |= ok ? 1u << s : 0u;
                     defb |= (act && dfr) ? 1u << s : 0u;
                     const uint32_t idx = ok ? sr.y + val[s] : 0u;
-                    const uint32_t x = PC ? reinterpret_cast<const uint32_t*>(agnes_smem)[idx] : a.power32[idx];
+                    const uint32_t x = PC ? reinterpret_cast<const uint32_t*>(agnes_smem)[idx]
+                                          : (DCHK(idx < ns * nv, 10, idx, ns * nv) ? a.power32[idx] : 0u);
                     w[s] = ok ? x : 0u;
                     nilbc |= value[s] == AGNES_NIL ? 1u << s : 0u;
                     /* first-vote table index (checked-out votes: entry 0, a no-op max) */
@@ -1044,7 +1066,7 @@ __global__ __launch_bounds__(256) void dflow(agnes_tally_args a, uint32_t lds_pe
                             const uint32_t L0 = 63u - (uint32_t)__builtin_clzll(b);
                             vpos = 8u * L0 + rdl(vl, L0);
                         }
-                        if ((p1_at & LOCKF) && (vpos == NONE || (p1_at & ~LOCKF) > vpos)) vpos = p1_at & ~LOCKF; /* :198 set_valid */
+                        if (p1_at != NONE && (p1_at & LOCKF) && (vpos == NONE || (p1_at & ~LOCKF) > vpos)) vpos = p1_at & ~LOCKF; /* :198 set_valid */
                     }
                     /* the breakpoint votes' own messages */
                     for (uint32_t j = 0; j < nmsg; ++j) {
@@ -1090,7 +1112,7 @@ __global__ __launch_bounds__(256) void dflow(agnes_tally_args a, uint32_t lds_pe
         }
         if (SM) { /* the States back: round (RoundSkip), locked, valid, decision, step */
             __builtin_amdgcn_wave_barrier();
-            if (lane < m && !S.def) {
+            if (lane < m && !S.def && DCHK(S.s0 + lane < n, 11, S.s0 + lane, n)) {
                 const uint32_t* const rk = IT + RW * lane;
                 const uint32_t p1 = rk[R_P1], cc = rk[R_C], vp = rk[R_VP], sk = rk[R_SK], step = rk[R_STEP];
                 uint4* const sp = reinterpret_cast<uint4*>(a.states + S.s0 + lane);
@@ -1106,19 +1128,19 @@ __global__ __launch_bounds__(256) void dflow(agnes_tally_args a, uint32_t lds_pe
                     if (p1 != NONE && (p1 & LOCKF)) { /* locked = {round, v} at P1 */
                         s1.x = s0.z;
                         s1.y = s0.w;
-                        s2.z = a.vb.value[Sa + (p1 & ~LOCKF)];
+                        s2.z = DCHK(Sa + (p1 & ~LOCKF) < NV, 12, Sa + (p1 & ~LOCKF), NV) ? a.vb.value[Sa + (p1 & ~LOCKF)] : 0u;
                         flags |= 1u << 8;
                     }
                     if (vp != 0u) { /* valid = {round, v} of the last set_valid_value */
                         s1.z = s0.z;
                         s1.w = s0.w;
-                        s2.w = a.vb.value[Sa + vp - 1u];
+                        s2.w = DCHK(Sa + vp - 1u < NV, 13, Sa + vp - 1u, NV) ? a.vb.value[Sa + vp - 1u] : 0u;
                         flags |= 1u << 16;
                     }
                     if (cc != NONE) { /* the decision */
                         s2.x = rk[R_DR];
                         s2.y = 0u;
-                        n3.x = a.vb.value[Sa + cc];
+                        n3.x = DCHK(Sa + cc < NV, 14, Sa + cc, NV) ? a.vb.value[Sa + cc] : 0u;
                         flags |= 1u << 24;
                     }
                     n3.y = (flags & ~0xFFu) | step;
@@ -1142,7 +1164,8 @@ __global__ __launch_bounds__(256) void dflow(agnes_tally_args a, uint32_t lds_pe
                 hdr_one(H, k, O);
                 if (!O.stream) { /* >= 2^30 votes: the LIST kernel's */
                     if (lane == 0 && O.ln) {
-                        a.list[atomicAdd(a.list_count, 1u)] = O.s0;
+                        const uint32_t li = atomicAdd(a.list_count, 1u);
+                        if (DCHK(li < n, 15, li, n)) a.list[li] = O.s0;
                         if (EVC) a.walk[atomicAdd(a.list_count + AGNES_WALK_COUNT, 1u)] = O.s0;
                     }
                     continue;
@@ -1225,6 +1248,31 @@ static hipError_t launch_dflow_k(const agnes_tally_args* a, int num_cus, hipStre
     if (blocks == 0) blocks = 1;
     if (o->pc) hipLaunchKernelGGL((dflow<DEDUP, SKIP, true, EVC, SM>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
     else hipLaunchKernelGGL((dflow<DEDUP, SKIP, false, EVC, SM>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
+#if AGNES_DFLOW_CHECK
+    {
+        hipError_t e = hipStreamSynchronize(st);
+        fprintf(stderr, "dflow check: DEDUP %d SKIP %d EVC %d SM %d n %u votes %llu R %u nv %u ns %u lpw %u blocks %llu pc %d: %s\n",
+                (int)DEDUP, (int)SKIP, (int)EVC, (int)SM, n, (unsigned long long)a->vb.n_votes, a->max_rounds,
+                a->n_vals, a->n_sets, lpw, (unsigned long long)blocks, (int)o->pc, hipGetErrorString(e));
+        if (e != hipSuccess) return e;
+        unsigned nbad = 0;
+        (void)hipMemcpyFromSymbol(&nbad, HIP_SYMBOL(agnes_dflow_nbad), sizeof(nbad));
+        uint32_t cnt[1 + AGNES_QUEUE_WORDS] = {0};
+        (void)hipMemcpy(cnt, a->list_count, sizeof(uint32_t) * 2, hipMemcpyDeviceToHost);
+        fprintf(stderr, "dflow check: %u violations, list %u\n", nbad, cnt[0]);
+        if (cnt[0] > n) return hipErrorInvalidValue;
+        if (cnt[0]) {
+            std::vector<uint32_t> L(cnt[0]);
+            (void)hipMemcpy(L.data(), a->list, sizeof(uint32_t) * cnt[0], hipMemcpyDeviceToHost);
+            for (uint32_t i = 0; i < cnt[0]; ++i)
+                if (L[i] >= n) {
+                    fprintf(stderr, "dflow check: list[%u] = %u >= n\n", i, L[i]);
+                    return hipErrorInvalidValue;
+                }
+        }
+        if (nbad) return hipErrorInvalidValue;
+    }
+#endif
     return hipGetLastError();
 }
 

@@ -48,14 +48,14 @@ __device__ __forceinline__ void glds16(const void* g, unsigned char* l) {
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
-                 : "v"(g), "s"(lds_addr(l))
+                 : "v"(g), "s"(rfl(lds_addr(l)))
                  : "memory");
 }
 __device__ __forceinline__ void glds4(const void* g, unsigned char* l) {
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
-                 : "v"(g), "s"(lds_addr(l))
+                 : "v"(g), "s"(rfl(lds_addr(l)))
                  : "memory");
 }
 /* non-temporal forms (the streamed vote columns are read once: keep them out of L2) */
@@ -63,14 +63,14 @@ __device__ __forceinline__ void glds16nt(const void* g, unsigned char* l) {
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
-                 : "v"(g), "s"(lds_addr(l))
+                 : "v"(g), "s"(rfl(lds_addr(l)))
                  : "memory");
 }
 __device__ __forceinline__ void glds4nt(const void* g, unsigned char* l) {
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off nt\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
-                 : "v"(g), "s"(lds_addr(l))
+                 : "v"(g), "s"(rfl(lds_addr(l)))
                  : "memory");
 }
 /* every outstanding vector-memory op (the LDS-DMAs included) has retired */

@@ -52,8 +52,17 @@ constexpr uint32_t F_INST = 0, F_VALUE = 2048, F_VAL = 4096, F_ROUND = 6144, F_T
 /* instances per batch: header offsets in lanes 0..FB, per-instance data in lane k.  A
  * batch's stream ends in a partial chunk, so the bigger the batch the fewer idle lanes
  * (C2: 16 instances = 3,200 votes in 7 chunks, 32 = 6,400 in 13) */
+#ifndef AGNES_FLOW_TAIL_DIV
+#define AGNES_FLOW_TAIL_DIV 16 /* the queue's tail: 1/16 of the instances in SMALLB batches */
+#endif
+#ifndef AGNES_FLOW_BATCHES_PER_WAVE
+#define AGNES_FLOW_BATCHES_PER_WAVE 0 /* 0: always FB */
+#endif
+#ifndef AGNES_FLOW_SMALLB
+#define AGNES_FLOW_SMALLB 4
+#endif
 constexpr uint32_t FB = 32u;
-constexpr uint32_t SMALLB = 4u; /* batch size of the work queue's tail                  */
+constexpr uint32_t SMALLB = AGNES_FLOW_SMALLB; /* batch size of the work queue's tail       */
 /* instance record, 12 words: quorum threshold, power-row base, validators of its set
  * (0: no such set); the State machine's view: the roles its step keeps (one byte per
  * vote, 0 without the State machine), State.round in every byte, 0xFF bytes when it
@@ -218,11 +227,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
     const uint32_t qn = gridDim.x < QN ? gridDim.x : QN;
     const uint32_t qk = blockIdx.x % qn;
     uint32_t* const ctr = a.list_count + 1u + qk;
-    const uint64_t NB = (uint64_t)(n / FB) * 15u / 16u;
+    /* batch size: FB, or (launcher) fewer for a batch too small to give every wave
+     * several batches -- the makespan is a wave's last batch */
+    const uint32_t fb = a.batch && a.batch < FB ? a.batch : FB;
+    const uint32_t sb_ = SMALLB < fb ? SMALLB : fb;
+    const uint64_t NB = (uint64_t)(n / fb) * (AGNES_FLOW_TAIL_DIV - 1u) / AGNES_FLOW_TAIL_DIV;
     auto range_of = [&](uint32_t t, uint32_t& s0, uint32_t& e0) {
         const uint64_t b = (uint64_t)t * qn + qk;
-        const uint64_t s = b < NB ? b * FB : NB * FB + (b - NB) * SMALLB;
-        const uint64_t e = s + (b < NB ? FB : SMALLB);
+        const uint64_t s = b < NB ? b * fb : NB * fb + (b - NB) * sb_;
+        const uint64_t e = s + (b < NB ? fb : sb_);
         s0 = s < n ? (uint32_t)s : n;
         e0 = e < n ? (uint32_t)e : n;
     };
@@ -1045,6 +1058,12 @@ static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStrea
     b.power_cache = o->pc ? (uint32_t)pcb : 0u;
     const uint64_t lds = wave_lds + b.power_cache;
     const void* fn = fns[o->pc ? 1 : 0];
+    {   /* batches of FB, fewer when that leaves a wave under AGNES_FLOW_BATCHES_PER_WAVE */
+        const uint64_t waves = (uint64_t)(num_cus > 0 ? num_cus : 256) * (uint64_t)o->per_cu * AGNES_WAVES_PER_BLOCK;
+        uint64_t fbx = AGNES_FLOW_BATCHES_PER_WAVE ? (uint64_t)n / (waves * AGNES_FLOW_BATCHES_PER_WAVE) : agnes::flow::FB;
+        fbx = fbx < 4u ? 4u : (fbx > agnes::flow::FB ? agnes::flow::FB : fbx);
+        b.batch = (uint32_t)fbx;
+    }
     if (lds > 48u * 1024u) {
         hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;

@@ -54,6 +54,7 @@ typedef struct agnes_tally_args {
     uint32_t power_cache; /* bytes of block LDS holding the u32 power table (0: gather from HBM) */
     uint32_t one_inst;    /* AGNES_FLAG_ONE_INSTANCE: every segment is a slice of instance one_id */
     uint32_t one_id;
+    uint32_t batch;       /* flow: instances per work-queue batch (0: the kernel's FB) */
     uint64_t* ev_counts;  /* optional [n_instances]: the flow kernel writes each instance's event
                              record count (agnes_tally_events); instances it hands to the walk
                              list are left to agnes_launch_event_count_list */
