@@ -33,7 +33,7 @@ struct agnes_ctx {
     hipStream_t last_stream = nullptr;
     bool used = false;               /* a call has enqueued work on last_stream */
     hipEvent_t order_ev = nullptr;   /* orders a call on another stream after it */
-    bool all_fast = false;     /* every set inside the u32 fast domain */
+    uint32_t sets_dom = 0;     /* 2: every set inside the u32 fast domain, 1: inside the u64 one, 0: neither */
     uint32_t* d_list = nullptr; /* [list_cap] deferred instances, [list_cap] walk list */
     uint32_t list_cap = 0;
     uint64_t* d_scan = nullptr; /* edge-offset scan: block totals */
@@ -105,6 +105,13 @@ agnes_set_info set_info(const int64_t* pw, uint32_t n_vals, int64_t total) {
         si.q2 = t2 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)t2;
         si.q1 = t1 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)t1;
         si.maxpow = (uint32_t)mx;
+    }
+    const bool w64 = mn >= 0 && total >= 0 && total < (1ll << 61);
+    si.w64 = w64 ? 1u : 0u;
+    if (w64) {
+        si.q2w = (uint64_t)(2 * total) / 3u;
+        si.q1w = (uint64_t)total / 3u;
+        si.maxw = (uint64_t)mx;
     }
     return si;
 }
@@ -250,7 +257,7 @@ int agnes_upload_power(agnes_ctx* c, const int64_t* power, uint32_t n_sets, uint
     const uint64_t n = (uint64_t)n_sets * n_vals;
     std::vector<agnes_set_info> sets(n_sets);
     std::vector<uint32_t> p32(n);
-    bool all_fast = true;
+    bool all_fast = true, all_w64 = true;
     for (uint32_t s = 0; s < n_sets; ++s) {
         const int64_t* row = power + (uint64_t)s * n_vals;
         int64_t t = 0;
@@ -259,6 +266,7 @@ int agnes_upload_power(agnes_ctx* c, const int64_t* power, uint32_t n_sets, uint
             for (uint32_t v = 0; v < n_vals; ++v) t = wadd(t, row[v]);
         sets[s] = set_info(row, n_vals, t);
         all_fast = all_fast && sets[s].fast;
+        all_w64 = all_w64 && sets[s].w64;
         for (uint32_t v = 0; v < n_vals; ++v) p32[(uint64_t)s * n_vals + v] = (uint32_t)row[v];
     }
     const size_t pb = (size_t)(n ? n : 1);
@@ -273,7 +281,7 @@ int agnes_upload_power(agnes_ctx* c, const int64_t* power, uint32_t n_sets, uint
                         hipMemcpyHostToDevice));
     c->n_sets = n_sets;
     c->n_vals = n_vals;
-    c->all_fast = all_fast;
+    c->sets_dom = all_fast ? 2u : (all_w64 ? 1u : 0u);
     return AGNES_OK;
 }
 
@@ -285,7 +293,7 @@ int64_t agnes_lds_bytes_per_wave(const agnes_config* cfg, uint32_t n_vals) {
 
 static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b,
                       uint8_t* codes, const agnes_state* states_in, agnes_state* states,
-                      agnes_carry_rec* carry, const agnes_set_info* sets, uint32_t n_sets, bool sets_fast,
+                      agnes_carry_rec* carry, const agnes_set_info* sets, uint32_t n_sets, uint32_t sets_dom,
                       hipStream_t st, uint64_t* ev_counts = nullptr, bool* counted = nullptr) {
     if (!c || !cfg_ok(cfg) || !b || !b->offsets) return AGNES_E_INVALID;
     if (b->n_votes && (!codes || !b->instance || !b->round || !b->type || !b->value ||
@@ -301,7 +309,10 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     if (lpw < 0) return (int)lpw;
     AGNES_TRY(hipSetDevice(c->device));
     AGNES_ORDER(c, st);
-    const bool wide_all = b->weight != nullptr || carry != nullptr || !sets_fast;
+    /* i64 for every instance with caller weights, carried executors or a power set in
+     * neither fast domain; u64 sums (tally_fast<W64>) when a set is outside the u32 one */
+    const bool wide_all = b->weight != nullptr || carry != nullptr || sets_dom == 0u;
+    const bool w64 = !wide_all && sets_dom == 1u;
     if (!wide_all && (!c->d_list || c->list_cap < b->n_instances)) {
         /* [list_cap] deferred instances | [list_cap] walk list */
         AGNES_TRY(hipStreamSynchronize(st));
@@ -326,12 +337,13 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     a.one_inst = (cfg->flags & AGNES_FLAG_ONE_INSTANCE) ? 1u : 0u;
     a.one_id = cfg->reserved;
     a.codes = codes;
+    a.w64 = w64 ? 1u : 0u;
     a.states = (cfg->flags & AGNES_FLAG_STATE_MACHINE) ? states : nullptr;
     a.states_in = nullptr;
     if (a.states && states_in && states_in != states) {
         /* the sweep route reads the input States itself; the other routes work in place */
         const uint32_t route = (cfg->flags >> AGNES_ROUTE_SHIFT) & AGNES_ROUTE_MASK;
-        const bool sweep = !wide_all && route == AGNES_ROUTE_AUTO && cfg->mode == AGNES_MODE_REFERENCE &&
+        const bool sweep = !wide_all && !w64 && route == AGNES_ROUTE_AUTO && cfg->mode == AGNES_MODE_REFERENCE &&
                            !(cfg->flags & AGNES_FLAG_ROUND_SKIP) && cfg->max_rounds <= 15u;
         if (sweep) {
             a.states_in = states_in;
@@ -361,7 +373,7 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     /* agnes_tally_events: the flow route counts each instance's event records as it goes */
     if (ev_counts) {
         const uint32_t route = (cfg->flags >> AGNES_ROUTE_SHIFT) & AGNES_ROUTE_MASK;
-        const bool flow = !wide_all && route == AGNES_ROUTE_AUTO && cfg->mode == AGNES_MODE_REFERENCE &&
+        const bool flow = !wide_all && !w64 && route == AGNES_ROUTE_AUTO && cfg->mode == AGNES_MODE_REFERENCE &&
                           !(cfg->flags & AGNES_FLAG_ROUND_SKIP) && agnes_flow_counts_events(cfg->flags, cfg->max_rounds);
         /* DEDUP / RoundSkip on the stream kernel: it counts too (the LIST kernel's
          * instances go on the walk list, counted after their codes) */
@@ -377,14 +389,14 @@ int agnes_tally(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b
                 agnes_state* states, void* stream) {
     if (!c || !cfg || (cfg->flags & (AGNES_FLAG_ONE_INSTANCE | AGNES_FLAG_WEIGHTS_CACHED)))
         return AGNES_E_INVALID; /* agnes_tally_carried only */
-    return tally_impl(c, cfg, b, codes, nullptr, states, nullptr, c->d_sets, c->n_sets, c->all_fast,
+    return tally_impl(c, cfg, b, codes, nullptr, states, nullptr, c->d_sets, c->n_sets, c->sets_dom,
                       (hipStream_t)stream);
 }
 
 int agnes_tally_states(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint8_t* codes,
                        const agnes_state* states_in, agnes_state* states_out, void* stream) {
     if (!c || !cfg || (cfg->flags & (AGNES_FLAG_ONE_INSTANCE | AGNES_FLAG_WEIGHTS_CACHED))) return AGNES_E_INVALID;
-    return tally_impl(c, cfg, b, codes, states_in, states_out, nullptr, c->d_sets, c->n_sets, c->all_fast,
+    return tally_impl(c, cfg, b, codes, states_in, states_out, nullptr, c->d_sets, c->n_sets, c->sets_dom,
                       (hipStream_t)stream);
 }
 
@@ -397,7 +409,7 @@ int agnes_tally_carried(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_
     if (cfg->mode != AGNES_MODE_REFERENCE || (cfg->flags & (AGNES_FLAG_ROUND_SKIP | AGNES_FLAG_STATE_MACHINE)))
         return AGNES_E_UNSUPPORTED;
     return tally_impl(c, cfg, b, codes, nullptr, nullptr, reinterpret_cast<agnes_carry_rec*>(counts), c->d_sets,
-                      c->n_sets, c->all_fast, (hipStream_t)stream);
+                      c->n_sets, c->sets_dom, (hipStream_t)stream);
 }
 
 int agnes_tally_partials(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, agnes_vote_count* counts,
@@ -646,7 +658,7 @@ int agnes_tally_events(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_b
     if (cfg_ok(cfg) && cfg->max_rounds > 64u) return AGNES_E_UNSUPPORTED; /* the emit's value slots in LDS */
     const hipStream_t st = (hipStream_t)stream;
     bool counted = false;
-    const int rc = tally_impl(c, cfg, b, codes, states_in, states_out, nullptr, c->d_sets, c->n_sets, c->all_fast, st,
+    const int rc = tally_impl(c, cfg, b, codes, states_in, states_out, nullptr, c->d_sets, c->n_sets, c->sets_dom, st,
                               offsets + 1, &counted);
     if (rc != AGNES_OK) return rc;
     const uint64_t words = agnes_edges_scratch_words(b->n_instances);
@@ -747,12 +759,13 @@ int agnes_gen_votes_device(agnes_ctx* c, const agnes_gen_params* p, const uint64
 /* ---------------- scalar mirror ---------------- */
 
 /* One GPU-resident executor pair (prevotes, precommits) + a 1-vote batch.
- * device block: [set_info 24][carry 3x24][offsets 16][weight 8][pad][instance 16]
+ * device block: [set_info 56][pad][carry 3x24][offsets 16][weight 8][pad][instance 16]
  *               [value 16][validator 16][round 4][type 4][code 4]
  * (vote columns 16-byte aligned: the kernel reads 4 votes per lane) */
 namespace {
-constexpr size_t SX_SET = 0, SX_CARRY = 24, SX_OFF = 96, SX_W = 112, SX_INST = 128, SX_VAL = 144,
-                 SX_VIDX = 160, SX_ROUND = 176, SX_TYPE = 180, SX_CODE = 184, SX_BYTES = 192;
+constexpr size_t SX_SET = 0, SX_CARRY = 64, SX_OFF = 144, SX_W = 160, SX_INST = 176, SX_VAL = 192,
+                 SX_VIDX = 208, SX_ROUND = 224, SX_TYPE = 228, SX_CODE = 232, SX_BYTES = 240;
+static_assert(sizeof(agnes_set_info) <= SX_CARRY, "scalar block layout");
 
 struct ScalarExec {
     unsigned char* dev = nullptr;
@@ -767,6 +780,7 @@ bool sx_init(ScalarExec* x, int64_t total) {
     std::memset(host, 0, sizeof(host));
     agnes_set_info si = set_info(nullptr, 0, total);
     si.fast = 0; /* caller weights: always the wrapping i64 path */
+    si.w64 = 0;
     std::memcpy(host + SX_SET, &si, sizeof(si));
     const uint64_t off[2] = {0, 1};
     std::memcpy(host + SX_OFF, off, sizeof(off));

@@ -152,12 +152,12 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
     lo = lo < NV ? lo : NV;
     hi = hi < NV ? hi : NV;
     if (hi <= lo) return;
-    { /* the same u32-domain test as the tally kernels: the rest is the LIST kernel's */
+    { /* the same domain test (u32, or u64 for a.w64) as the tally kernels: the rest is the LIST kernel's */
         const uint32_t set = a.vb.instance_set ? a.vb.instance_set[i] : (ns ? i % ns : 0u);
         if (set < ns) {
             const agnes_set_info si = a.sets[set];
             const uint64_t len = hi - lo;
-            if (fast::defer_to_list(si.fast, si.maxpow, len)) return;
+            if (fast::defer_si(si, len, a.w64 != 0u)) return;
         }
     }
 

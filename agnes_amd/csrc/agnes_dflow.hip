@@ -1282,7 +1282,7 @@ bool agnes_dflow_supported(const agnes_tally_args* a) {
     const uintptr_t al16 = reinterpret_cast<uintptr_t>(a->vb.instance) | reinterpret_cast<uintptr_t>(a->vb.value) |
                            reinterpret_cast<uintptr_t>(a->vb.validator);
     const uintptr_t al4 = reinterpret_cast<uintptr_t>(a->vb.round) | reinterpret_cast<uintptr_t>(a->vb.type);
-    const bool gathered = a->vb.weight == nullptr && a->carry == nullptr;
+    const bool gathered = a->vb.weight == nullptr && a->carry == nullptr && !a->w64; /* u32 sums */
     return gathered && a->max_rounds >= 1u && a->max_rounds <= 8u && a->n_vals > 0u &&
            agnes::dflow::layout(a->max_rounds, a->n_vals, true, true).total <= 40u * 1024u && (al16 & 15u) == 0u &&
            (al4 & 3u) == 0u && (reinterpret_cast<uintptr_t>(a->codes) & 7u) == 0u && a->vb.validator != nullptr;

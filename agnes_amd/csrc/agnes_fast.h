@@ -32,6 +32,15 @@ __host__ __device__ __forceinline__ bool defer_to_list(uint32_t fast, uint32_t m
     return !fast || len >= (1ull << 30) || len * (uint64_t)maxpow >= (1ull << 31);
 }
 
+/* The u64 domain (agnes_tally_args.w64, sets with agnes_set_info.w64): non-negative
+ * powers, fewer than 2^30 votes and len * maxpow < 2^61, so every running sum stays
+ * below 2^61 and 3 * sum never wraps (round_votes.rs:31-33).  The instance test of the
+ * kernel's domain, u32 or u64: outside it, the i64 LIST kernel's. */
+__device__ __forceinline__ bool defer_si(const agnes_set_info& si, uint64_t len, bool w64) {
+    if (!w64) return defer_to_list(si.fast, si.maxpow, len);
+    return !si.w64 || len >= (1ull << 30) || __umul64hi(len, si.maxw) != 0ull || len * si.maxw >= (1ull << 61);
+}
+
 /* LDS-DMA prefetch buffer of one chunk: instance, value, validator (1 KiB each,
  * lane l's 16 B at 16 l), round, type (256 B each, lane l's 4 B at 4 l) */
 constexpr uint32_t PF_INST = 0, PF_VALUE = 1024, PF_VAL = 2048, PF_ROUND = 3072, PF_TYPE = 3328,

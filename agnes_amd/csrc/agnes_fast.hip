@@ -30,14 +30,17 @@
  * payload up backwards in the instance's stream.
  */
 
+#include <type_traits>
+
 #include "agnes_fast.h"
 
 namespace agnes {
 namespace fast {
 
 __host__ __device__ inline void layout(uint32_t mode, bool skip, bool pf, uint32_t R, uint32_t nv,
-                                       uint32_t* o_fv, uint32_t* o_fs, uint32_t* o_pf, uint32_t* total) {
-    uint32_t o = (uint32_t)align16(20ull * R); /* vw[2R] vn[2R] skw[R] */
+                                       uint32_t* o_fv, uint32_t* o_fs, uint32_t* o_pf, uint32_t* total,
+                                       bool w64 = false) {
+    uint32_t o = (uint32_t)align16((w64 ? 40ull : 20ull) * R); /* vw[2R] vn[2R] skw[R] (u32, or u64 sums) */
     *o_fv = o;
     if (mode == AGNES_MODE_DEDUP) o = (uint32_t)align16(o + 8ull * R * nv);
     *o_fs = o;
@@ -62,8 +65,16 @@ struct Chunk {
     uint32_t ok;       /* bit s: ... and passes validation */
 };
 
-template <uint32_t MODE, bool SKIP, bool SM, bool PC, bool PF>
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return rfl(x); }
+__device__ __forceinline__ uint64_t uni(uint64_t x) { return rfl64(x); }
+
+/* W64: the u64 domain (agnes_fast.h defer_si): the same kernel with u64 sums, weights
+ * gathered from the i64 power table (no u32 LDS copy: PC is false) */
+template <uint32_t MODE, bool SKIP, bool SM, bool PC, bool PF, bool W64>
 __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t lds_per_wave) {
+    static_assert(!(PC && W64), "the LDS power table holds u32 powers");
+    using Acc = typename std::conditional<W64, uint64_t, uint32_t>::type;  /* running sums */
+    using SAcc = typename std::conditional<W64, int64_t, int32_t>::type;   /* thresholds   */
     const uint32_t lane = lane_id();
     const uint32_t wave = rfl(threadIdx.x >> 6);
     const uint32_t R = a.max_rounds;
@@ -109,11 +120,11 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
     (void)gw;
 
     uint32_t o_fv, o_fs, o_pf, o_tot;
-    layout(MODE, SKIP, PF, R, nv, &o_fv, &o_fs, &o_pf, &o_tot);
+    layout(MODE, SKIP, PF, R, nv, &o_fv, &o_fs, &o_pf, &o_tot, W64);
     unsigned char* base = agnes_smem + a.power_cache + wave * lds_per_wave;
-    uint32_t* vw = reinterpret_cast<uint32_t*>(base); /* [2R] value weight carried across chunks */
-    uint32_t* vn = vw + 2u * R;                        /* [2R] nil weight                       */
-    uint32_t* skw = vn + 2u * R;                       /* [R]  RoundSkip weight                 */
+    Acc* vw = reinterpret_cast<Acc*>(base); /* [2R] value weight carried across chunks */
+    Acc* vn = vw + 2u * R;                  /* [2R] nil weight                       */
+    Acc* skw = vn + 2u * R;                 /* [R]  RoundSkip weight                 */
     uint32_t* first_v = reinterpret_cast<uint32_t*>(base + o_fv);
     uint32_t* first_s = reinterpret_cast<uint32_t*>(base + o_fs);
     unsigned char* const pfb = base + o_pf;
@@ -249,18 +260,26 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
         I.set_ok = set < ns;
         I.pbase = set * nv;
         I.q2 = I.q1 = 0;
+        Acc Q2 = 0, Q1 = 0; /* the quorum / +1/3 thresholds in the sums' width */
         const uint64_t len = I.end - I.beg;
         if (I.set_ok) {
             const agnes_set_info si = a.sets[set];
-            /* sums provably < 2^31 (u32 arithmetic), else the i64 LIST kernel */
-            if (defer_to_list(si.fast, si.maxpow, len)) {
+            /* sums provably < 2^31 (u32 arithmetic; W64: < 2^61), else the i64 LIST kernel */
+            if (defer_si(si, len, W64)) {
                 if (lane == 0) a.list[atomicAdd(a.list_count, 1u)] = I.i;
                 run = false;
             }
-            /* sums < 2^31: a threshold >= 2^31 - 1 is never crossed, clamp it so the
-             * per-lane thresholds below stay in int32 range */
-            I.q2 = si.q2 < 0x7FFFFFFFu ? si.q2 : 0x7FFFFFFFu;
-            I.q1 = si.q1 < 0x7FFFFFFFu ? si.q1 : 0x7FFFFFFFu;
+            if (W64) {
+                Q2 = (Acc)si.q2w;
+                Q1 = (Acc)si.q1w;
+            } else {
+                /* sums < 2^31: a threshold >= 2^31 - 1 is never crossed, clamp it so the
+                 * per-lane thresholds below stay in int32 range */
+                I.q2 = si.q2 < 0x7FFFFFFFu ? si.q2 : 0x7FFFFFFFu;
+                I.q1 = si.q1 < 0x7FFFFFFFu ? si.q1 : 0x7FFFFFFFu;
+                Q2 = (Acc)I.q2;
+                Q1 = (Acc)I.q1;
+            }
         }
         if (len == 0) run = false;
         if (run) {
@@ -295,11 +314,12 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
             load_chunk(I, c, x, val, t4);
             const uint32_t p0 = 4u * lane;
             /* K1: w = power[set][validator] (consensus_executor.rs:62-63 -> validators.rs:7) */
-            uint32_t w[VPL];
+            Acc w[VPL];
 #pragma unroll
             for (uint32_t s = 0; s < VPL; ++s) {
                 const uint32_t idx = I.pbase + (((x.ok >> s) & 1u) ? val[s] : 0u);
-                w[s] = PC ? reinterpret_cast<const uint32_t*>(agnes_smem)[idx] : a.power32[idx];
+                if (W64) w[s] = (Acc)a.power[idx];
+                else w[s] = PC ? reinterpret_cast<const uint32_t*>(agnes_smem)[idx] : a.power32[idx];
             }
             bad += __builtin_popcount(x.pos & ~x.ok);
             /* after the gather: the previous chunk's stores, the header two instances
@@ -364,15 +384,15 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
 
             /* per-vote code: INVALID / REJECTED, else the tally event filled below */
             uint32_t code[VPL];
-            uint32_t wv[VPL], wn[VPL];
+            Acc wv[VPL], wn[VPL];
 #pragma unroll
             for (uint32_t s = 0; s < VPL; ++s) {
                 const bool a_ = (acc >> s) & 1u;
                 code[s] = !((x.ok >> s) & 1u) ? AGNES_CODE_INVALID : (a_ ? 0u : AGNES_CODE_REJECTED);
                 if (!a_) x.key[s] = 0xFFFFFFFFu;
                 const bool isnil = x.value[s] == AGNES_NIL;
-                wv[s] = isnil ? 0u : w[s];
-                wn[s] = isnil ? w[s] : 0u;
+                wv[s] = isnil ? (Acc)0 : w[s];
+                wn[s] = isnil ? w[s] : (Acc)0;
             }
             const bool ld_carry = c != c0;
             const bool st_carry = c + CHUNK < I.end;
@@ -388,35 +408,35 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
                 const uint32_t kl = (uint32_t)__builtin_ctzll(lm);
                 const uint32_t ks = (uint32_t)__builtin_ctz(rdl(rem, kl));
                 const uint32_t K = rdl(sel4(x.key, ks), kl);
-                uint32_t av[VPL], an[VPL];
+                Acc av[VPL], an[VPL];
                 uint32_t inb = 0;
 #pragma unroll
                 for (uint32_t s = 0; s < VPL; ++s) {
                     const bool in = x.key[s] == K;
                     inb |= (uint32_t)in << s;
-                    av[s] = in ? wv[s] : 0u;
-                    an[s] = in ? wn[s] : 0u;
+                    av[s] = in ? wv[s] : (Acc)0;
+                    an[s] = in ? wn[s] : (Acc)0;
                 }
                 rem &= ~inb;
                 /* lane-local inclusive prefixes and one wave scan of the lane totals */
                 av[1] += av[0]; av[2] += av[1]; av[3] += av[2];
                 an[1] += an[0]; an[2] += an[1]; an[3] += an[2];
-                const uint32_t iv = scan(av[3]), in_ = scan(an[3]);
-                const uint32_t cv = ld_carry ? vw[K] : 0u, cn = ld_carry ? vn[K] : 0u;
+                const Acc iv = scan(av[3]), in_ = scan(an[3]);
+                const Acc cv = ld_carry ? vw[K] : (Acc)0, cn = ld_carry ? vn[K] : (Acc)0;
                 /* a quiet key: even the bucket's running sums after its last vote of the
                  * chunk stay at or below q2, so every vote of it is Init (code NONE, already
                  * in code[]) -- the common case for the few early next-round votes, and for a
                  * round's first chunk.  Uniform; the sums stay below 2^31 in this domain. */
-                if (rfl(cv + cn) + rdl(iv, 63u) + rdl(in_, 63u) > I.q2) {
+                if (uni(cv + cn) + rdl(iv, 63u) + rdl(in_, 63u) > Q2) {
                 /* sum > q2  <=>  lane-local prefix > q2 - carry - exclusive wave prefix */
-                const int32_t tv = (int32_t)(I.q2 - cv - (iv - av[3]));
-                const int32_t tn = (int32_t)(I.q2 - cn - (in_ - an[3]));
-                const int32_t ta = (int32_t)(I.q2 - cv - cn - (iv - av[3]) - (in_ - an[3]));
+                const SAcc tv = (SAcc)(Q2 - cv - (iv - av[3]));
+                const SAcc tn = (SAcc)(Q2 - cn - (in_ - an[3]));
+                const SAcc ta = (SAcc)(Q2 - cv - cn - (iv - av[3]) - (in_ - an[3]));
                 if (K & 1u) { /* precommits: Value -> PrecommitValue, Nil -> None, Any -> PrecommitAny */
 #pragma unroll
                     for (uint32_t s = 0; s < VPL; ++s) {
-                        const bool qv = (int32_t)av[s] > tv, qn = (int32_t)an[s] > tn,
-                                   qa = (int32_t)(av[s] + an[s]) > ta;
+                        const bool qv = (SAcc)av[s] > tv, qn = (SAcc)an[s] > tn,
+                                   qa = (SAcc)(av[s] + an[s]) > ta;
                         const uint32_t ev = qv ? AGNES_CODE_PRECOMMIT_VALUE
                                           : (qn ? AGNES_CODE_NONE : (qa ? AGNES_CODE_PRECOMMIT_ANY : AGNES_CODE_NONE));
                         code[s] = ((inb >> s) & 1u) ? ev : code[s];
@@ -424,8 +444,8 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
                 } else { /* prevotes: PolkaValue / PolkaNil / PolkaAny */
 #pragma unroll
                     for (uint32_t s = 0; s < VPL; ++s) {
-                        const bool qv = (int32_t)av[s] > tv, qn = (int32_t)an[s] > tn,
-                                   qa = (int32_t)(av[s] + an[s]) > ta;
+                        const bool qv = (SAcc)av[s] > tv, qn = (SAcc)an[s] > tn,
+                                   qa = (SAcc)(av[s] + an[s]) > ta;
                         const uint32_t ev = qv ? AGNES_CODE_POLKA_VALUE
                                           : (qn ? AGNES_CODE_POLKA_NIL : (qa ? AGNES_CODE_POLKA_ANY : AGNES_CODE_NONE));
                         code[s] = ((inb >> s) & 1u) ? ev : code[s];
@@ -449,22 +469,23 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
                     const uint32_t kl = (uint32_t)__builtin_ctzll(lm);
                     const uint32_t ks = (uint32_t)__builtin_ctz(rdl(rs, kl));
                     const uint32_t kr = rdl(sel4(x.key, ks), kl) >> 1;
-                    uint32_t as[VPL], inb = 0;
+                    Acc as[VPL];
+                    uint32_t inb = 0;
 #pragma unroll
                     for (uint32_t s = 0; s < VPL; ++s) {
                         const bool in = (x.key[s] >> 1) == kr && ((rs >> s) & 1u);
                         inb |= (uint32_t)in << s;
-                        as[s] = (in && ((sfirst >> s) & 1u)) ? w[s] : 0u;
+                        as[s] = (in && ((sfirst >> s) & 1u)) ? w[s] : (Acc)0;
                     }
                     rs &= ~inb;
                     as[1] += as[0]; as[2] += as[1]; as[3] += as[2];
-                    const uint32_t is = scan(as[3]);
-                    const uint32_t cs = ld_carry ? skw[kr] : 0u;
-                    if (rfl(cs) + rdl(is, 63u) > I.q1) { /* else quiet: no vote of the round crosses +1/3 */
-                        const int32_t ts = (int32_t)(I.q1 - cs - (is - as[3]));
+                    const Acc is = scan(as[3]);
+                    const Acc cs = ld_carry ? skw[kr] : (Acc)0;
+                    if (uni(cs) + rdl(is, 63u) > Q1) { /* else quiet: no vote of the round crosses +1/3 */
+                        const SAcc ts = (SAcc)(Q1 - cs - (is - as[3]));
 #pragma unroll
                         for (uint32_t s = 0; s < VPL; ++s)
-                            if (((inb >> s) & 1u) && (int32_t)as[s] > ts) code[s] |= AGNES_CODE_SKIP;
+                            if (((inb >> s) & 1u) && (SAcc)as[s] > ts) code[s] |= AGNES_CODE_SKIP;
                     }
                     if (st_carry && lane == 63u) skw[kr] = cs + is;
                     __builtin_amdgcn_wave_barrier();
@@ -683,22 +704,25 @@ int64_t agnes_fast_lds_per_wave(uint32_t mode, uint32_t flags, uint32_t max_roun
     return (int64_t)tot;
 }
 
-static uint32_t fast_lds(uint32_t mode, uint32_t flags, bool pf, uint32_t R, uint32_t nv) {
+static uint32_t fast_lds(uint32_t mode, uint32_t flags, bool pf, uint32_t R, uint32_t nv, bool w64 = false) {
     uint32_t fv, fs, o_pf, tot;
-    agnes::fast::layout(mode, (flags & AGNES_FLAG_ROUND_SKIP) != 0, pf, R, nv, &fv, &fs, &o_pf, &tot);
+    agnes::fast::layout(mode, (flags & AGNES_FLAG_ROUND_SKIP) != 0, pf, R, nv, &fv, &fs, &o_pf, &tot, w64);
     return tot;
 }
 
-template <uint32_t MODE, bool SKIP, bool SM>
+/* variant v = PC | PF << 1 of the kernel (W64: no PC variant; v & 1 is never chosen) */
+template <uint32_t MODE, bool SKIP, bool SM, bool W64, int V>
+static const void* fast_fn() {
+    return reinterpret_cast<const void*>(&agnes::fast::tally_fast<MODE, SKIP, SM, (V & 1) != 0 && !W64, (V & 2) != 0, W64>);
+}
+
+template <uint32_t MODE, bool SKIP, bool SM, bool W64>
 static hipError_t launch_fast_k(const agnes_tally_args* a, int num_cus, hipStream_t st) {
     const uint32_t n = a->vb.n_instances;
     if (n == 0) return hipSuccess;
     using agnes::fast::tally_fast;
-    const void* fns[4] = {
-        reinterpret_cast<const void*>(&tally_fast<MODE, SKIP, SM, false, false>),
-        reinterpret_cast<const void*>(&tally_fast<MODE, SKIP, SM, true, false>),
-        reinterpret_cast<const void*>(&tally_fast<MODE, SKIP, SM, false, true>),
-        reinterpret_cast<const void*>(&tally_fast<MODE, SKIP, SM, true, true>)};
+    const void* fns[4] = {fast_fn<MODE, SKIP, SM, W64, 0>(), fast_fn<MODE, SKIP, SM, W64, 1>(),
+                          fast_fn<MODE, SKIP, SM, W64, 2>(), fast_fn<MODE, SKIP, SM, W64, 3>()};
     const uint64_t pcb = agnes::align16(4ull * a->n_sets * a->n_vals);
     /* variant v = PC | PF << 1: blocks per CU from the occupancy query; prefer the
      * LDS-DMA prefetch, then the LDS power table, each only where it costs no
@@ -711,13 +735,13 @@ static hipError_t launch_fast_k(const agnes_tally_args* a, int num_cus, hipStrea
         if (c.fn == fns[0] && c.R == a->max_rounds && c.nv == a->n_vals && c.flags == a->flags && c.pcb == pcb)
             o = &c;
     auto lds_of = [&](int v) -> uint64_t {
-        return (uint64_t)fast_lds(MODE, a->flags, (v & 2) != 0, a->max_rounds, a->n_vals) * AGNES_WAVES_PER_BLOCK +
+        return (uint64_t)fast_lds(MODE, a->flags, (v & 2) != 0, a->max_rounds, a->n_vals, W64) * AGNES_WAVES_PER_BLOCK +
                ((v & 1) ? pcb : 0u);
     };
     if (!o) {
         auto per_cu = [&](int v) -> int {
             const uint64_t lds = lds_of(v);
-            if (lds > 160u * 1024u || ((v & 1) && pcb > 32u * 1024u)) return 0;
+            if (lds > 160u * 1024u || ((v & 1) && (W64 || pcb > 32u * 1024u))) return 0;
             if (lds > 48u * 1024u &&
                 hipFuncSetAttribute(fns[v], hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
                 return 0;
@@ -740,7 +764,7 @@ static hipError_t launch_fast_k(const agnes_tally_args* a, int num_cus, hipStrea
     agnes_tally_args b = *a;
     b.set_cache = 0;
     b.power_cache = (o->v & 1) ? (uint32_t)pcb : 0u;
-    const uint32_t lpw = fast_lds(MODE, a->flags, (o->v & 2) != 0, a->max_rounds, a->n_vals);
+    const uint32_t lpw = fast_lds(MODE, a->flags, (o->v & 2) != 0, a->max_rounds, a->n_vals, W64);
     const uint64_t lds = lds_of(o->v);
     if (lds > 48u * 1024u) {
         hipError_t e = hipFuncSetAttribute(fns[o->v], hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -751,22 +775,28 @@ static hipError_t launch_fast_k(const agnes_tally_args* a, int num_cus, hipStrea
     const uint64_t cap = ncu * (uint64_t)o->per_cu;
     if (blocks > cap) blocks = cap;
     const dim3 g((uint32_t)blocks), blk(256);
+    constexpr bool P1 = !W64; /* the PC variants (never chosen for W64) */
     switch (o->v) {
-    case 0: hipLaunchKernelGGL((tally_fast<MODE, SKIP, SM, false, false>), g, blk, (size_t)lds, st, b, lpw); break;
-    case 1: hipLaunchKernelGGL((tally_fast<MODE, SKIP, SM, true, false>), g, blk, (size_t)lds, st, b, lpw); break;
-    case 2: hipLaunchKernelGGL((tally_fast<MODE, SKIP, SM, false, true>), g, blk, (size_t)lds, st, b, lpw); break;
-    default: hipLaunchKernelGGL((tally_fast<MODE, SKIP, SM, true, true>), g, blk, (size_t)lds, st, b, lpw); break;
+    case 0: hipLaunchKernelGGL((tally_fast<MODE, SKIP, SM, false, false, W64>), g, blk, (size_t)lds, st, b, lpw); break;
+    case 1: hipLaunchKernelGGL((tally_fast<MODE, SKIP, SM, P1, false, W64>), g, blk, (size_t)lds, st, b, lpw); break;
+    case 2: hipLaunchKernelGGL((tally_fast<MODE, SKIP, SM, false, true, W64>), g, blk, (size_t)lds, st, b, lpw); break;
+    default: hipLaunchKernelGGL((tally_fast<MODE, SKIP, SM, P1, true, W64>), g, blk, (size_t)lds, st, b, lpw); break;
     }
     return hipGetLastError();
+}
+
+template <uint32_t MODE, bool SKIP, bool SM>
+static hipError_t launch_fast_w(const agnes_tally_args* a, int num_cus, hipStream_t st) {
+    return a->w64 ? launch_fast_k<MODE, SKIP, SM, true>(a, num_cus, st) : launch_fast_k<MODE, SKIP, SM, false>(a, num_cus, st);
 }
 
 hipError_t agnes_launch_tally_fast(const agnes_tally_args* a, uint32_t mode, int num_cus, hipStream_t st) {
     const bool skip = (a->flags & AGNES_FLAG_ROUND_SKIP) != 0;
     const bool sm = (a->flags & AGNES_FLAG_STATE_MACHINE) != 0 && a->states != nullptr;
     if (mode == AGNES_MODE_DEDUP) {
-        if (skip) return sm ? launch_fast_k<1, true, true>(a, num_cus, st) : launch_fast_k<1, true, false>(a, num_cus, st);
-        return sm ? launch_fast_k<1, false, true>(a, num_cus, st) : launch_fast_k<1, false, false>(a, num_cus, st);
+        if (skip) return sm ? launch_fast_w<1, true, true>(a, num_cus, st) : launch_fast_w<1, true, false>(a, num_cus, st);
+        return sm ? launch_fast_w<1, false, true>(a, num_cus, st) : launch_fast_w<1, false, false>(a, num_cus, st);
     }
-    if (skip) return sm ? launch_fast_k<0, true, true>(a, num_cus, st) : launch_fast_k<0, true, false>(a, num_cus, st);
-    return sm ? launch_fast_k<0, false, true>(a, num_cus, st) : launch_fast_k<0, false, false>(a, num_cus, st);
+    if (skip) return sm ? launch_fast_w<0, true, true>(a, num_cus, st) : launch_fast_w<0, true, false>(a, num_cus, st);
+    return sm ? launch_fast_w<0, false, true>(a, num_cus, st) : launch_fast_w<0, false, false>(a, num_cus, st);
 }

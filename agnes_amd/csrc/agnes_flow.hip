@@ -56,7 +56,7 @@ constexpr uint32_t F_INST = 0, F_VALUE = 2048, F_VAL = 4096, F_ROUND = 6144, F_T
 #define AGNES_FLOW_TAIL_DIV 16 /* the queue's tail: 1/16 of the instances in SMALLB batches */
 #endif
 #ifndef AGNES_FLOW_BATCHES_PER_WAVE
-#define AGNES_FLOW_BATCHES_PER_WAVE 0 /* 0: always FB */
+#define AGNES_FLOW_BATCHES_PER_WAVE 4 /* batches per wave the batch size leaves (0: always FB); c3shard A/B 4 vs FB: flow 0.362 vs 0.444 ms */
 #endif
 #ifndef AGNES_FLOW_SMALLB
 #define AGNES_FLOW_SMALLB 4

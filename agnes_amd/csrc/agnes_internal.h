@@ -21,6 +21,14 @@ typedef struct agnes_set_info {
     uint32_t q1;
     uint32_t maxpow;
     uint32_t fast;
+    /* the u64 domain (w64 == 1): every power >= 0 and 0 <= total < 2^61.  For sums
+     * s < 2^61 `3*s > 2*total` is `s > q2w` (q2w = floor(2*total/3)) and `3*s > total`
+     * is `s > q1w`, without the i64 wrap (round_votes.rs:31-33) */
+    uint32_t w64;
+    uint32_t pad;
+    uint64_t q2w;
+    uint64_t q1w;
+    uint64_t maxw;
 } agnes_set_info;
 
 /* Carried VoteCount of one (instance, round, type): round_votes.rs:15-19 */
@@ -55,6 +63,8 @@ typedef struct agnes_tally_args {
     uint32_t one_inst;    /* AGNES_FLAG_ONE_INSTANCE: every segment is a slice of instance one_id */
     uint32_t one_id;
     uint32_t batch;       /* flow: instances per work-queue batch (0: the kernel's FB) */
+    uint32_t w64;         /* the u64 fast domain (agnes_set_info.w64 sets outside the u32 one):
+                             tally_fast with u64 sums, the apply pass tests the same deferral */
     uint64_t* ev_counts;  /* optional [n_instances]: the flow kernel writes each instance's event
                              record count (agnes_tally_events); instances it hands to the walk
                              list are left to agnes_launch_event_count_list */

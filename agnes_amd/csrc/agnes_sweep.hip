@@ -637,7 +637,8 @@ __global__ __launch_bounds__(256) void sweep(agnes_tally_args a, uint32_t lds_pe
 /* launcher                                                            */
 
 bool agnes_sweep_supported(const agnes_tally_args* a) {
-    return a->max_rounds <= 15u; /* keys round * 2 + type < 31: one bit each in a u32 */
+    /* keys round * 2 + type < 31: one bit each in a u32; u32 sums only */
+    return a->max_rounds <= 15u && !a->w64;
 }
 
 template <bool SM>

@@ -5,6 +5,7 @@ batch, bit-exact codes, final States and invalid counts.  Slow: each case tallie
 between host and device.
 
   C2  1M instances x 100 validators x 1 round (the bench's c2 batch), State machine
+  C2w the same with i64 stakes U[2^28, 2^34] (the bench's c2w batch, u64 sums)
   C3  a 125k-instance shard of 1M x 150 validators x 1..4 rounds, 1024 power sets
   C4  125k instances, Zipf power, 10 % duplicates + 10 % equivocations + 5 %
       next-round votes, DEDUP + RoundSkip + State machine
@@ -67,6 +68,17 @@ def test_full_c2(eng):
     p = abi.gen_params(seed=0xA6E5, n_instances=1_000_000, n_vals=100, rounds_min=1, rounds_max=1,
                        nil_permille=200)
     power = ol.gen_power(0xA6E5, 1, 100, abi.POWER_UNIFORM, 1, 1000)
+    codes, st = _compare(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 1), p, power, 1)
+    assert st["decided"].sum() > 0 and ((codes >> abi.CODE_MSG_SHIFT) != 0).any()
+
+
+def test_full_c2w(eng):
+    """The bench's c2w batch: the C2 shape with i64 stakes U[2^28, 2^34] (set total
+    ~8.6e11 > 2^32), through the u64-sum route (agnes_set_info.w64)."""
+    p = abi.gen_params(seed=0xA6E5, n_instances=1_000_000, n_vals=100, rounds_min=1, rounds_max=1,
+                       nil_permille=200)
+    power = ol.gen_power(0xA6E5, 1, 100, abi.POWER_UNIFORM, 1 << 28, 1 << 34)
+    assert power.sum() > (1 << 32)
     codes, st = _compare(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 1), p, power, 1)
     assert st["decided"].sum() > 0 and ((codes >> abi.CODE_MSG_SHIFT) != 0).any()
 

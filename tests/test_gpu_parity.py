@@ -207,6 +207,16 @@ CONFIGS = {
                                   nil_permille=400),
                              (abi.POWER_UNIFORM, -30, 100, 3),
                              (abi.MODE_DEDUP, abi.FLAG_ROUND_SKIP | abi.FLAG_STATE_MACHINE, 3)),
+    # the u64 domain (agnes_set_info.w64): powers past 2^31, set totals < 2^61 -> tally_fast
+    # with u64 sums; w64_deferred's longer instances reach len * maxpow >= 2^61 (LIST kernel)
+    "c2w_small": (dict(n_instances=2000, n_vals=100, rounds_min=1, rounds_max=1, nil_permille=200),
+                  (abi.POWER_UNIFORM, 1 << 28, 1 << 34, 1), (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 1)),
+    "w64_dedup_skip": (dict(n_instances=1500, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300,
+                            dup_permille=100, equiv_permille=100, higher_permille=50),
+                       (abi.POWER_ZIPF, 1 << 30, 1 << 40, 16),
+                       (abi.MODE_DEDUP, abi.FLAG_ROUND_SKIP | abi.FLAG_STATE_MACHINE, 5)),
+    "w64_deferred": (dict(n_instances=600, n_vals=300, rounds_min=1, rounds_max=2, nil_permille=250),
+                     (abi.POWER_UNIFORM, 1 << 50, 1 << 52, 2), (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 2)),
     "many_rounds": (dict(n_instances=200, n_vals=20, rounds_min=30, rounds_max=60,
                          nil_permille=300, higher_permille=100),
                     (abi.POWER_UNIFORM, 1, 100, 5),
@@ -503,7 +513,7 @@ def test_c3_shard_parity(eng):
 
 
 @pytest.mark.parametrize("route", list(ROUTES))
-@pytest.mark.parametrize("name", ["c2_sm", "c3_small", "c4_small"])
+@pytest.mark.parametrize("name", ["c2_sm", "c3_small", "c4_small", "c2w_small", "w64_dedup_skip"])
 def test_routes_generated(eng, route, name):
     p, hb, power, cfg = _make(name)
     cfg = abi.config(cfg.mode, cfg.flags | ROUTES[route], cfg.max_rounds)
