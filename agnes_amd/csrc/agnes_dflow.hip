@@ -118,6 +118,12 @@ constexpr uint32_t EV_HI = AGNES_CODE_NONE | (AGNES_CODE_PRECOMMIT_ANY << 8) | (
 #define AGNES_DFLOW_ALIAS 0
 #endif
 constexpr bool ALIAS = AGNES_DFLOW_ALIAS != 0;
+/* AGNES_DFLOW_ABL (timing ablations only, results wrong): bit 0 no F pass, 1 no sort /
+ * sorted pass, 2 no RS, 3 no K4, 4 no codes stage */
+#ifndef AGNES_DFLOW_ABL
+#define AGNES_DFLOW_ABL 0
+#endif
+constexpr uint32_t ABL = AGNES_DFLOW_ABL;
 
 /* per-wave LDS layout */
 struct Lay {
@@ -631,7 +637,7 @@ __global__ __launch_bounds__(256) void dflow(agnes_tally_args a, uint32_t lds_pe
             /* ---- per group of up to NSEG segments ---- */
             /* F: first-vote flags, one pass per segment */
             uint32_t accb = 0, sfbc = 0; /* bits per vote: accepted, first of (round, validator) */
-            if (DEDUP || SKIP) {
+            if ((DEDUP || SKIP) && !(ABL & 1u)) {
                 for (uint32_t i = 0; i < nseg; ++i) {
                     const uint32_t k = rdl(segk, i);
                     const uint32_t mok = (bits_of(eq_bytes(sg0, i)) | (bits_of(eq_bytes(sg1, i)) << 4)) & okb;
@@ -683,6 +689,7 @@ __global__ __launch_bounds__(256) void dflow(agnes_tally_args a, uint32_t lds_pe
                 const uint32_t inb = bits_of(range_bytes(sg0, g0, g0 + gn)) | (bits_of(range_bytes(sg1, g0, g0 + gn)) << 4);
                 accb = accall & inb;
 
+                if (!(ABL & 2u)) {
                 /* S: counting sort of the group's accepted votes by key */
                 uint64_t Cn = 0;
                 uint32_t rk0 = 0, rk1 = 0; /* rank of each vote among the lane's votes of its key, bytes */
@@ -801,8 +808,9 @@ __global__ __launch_bounds__(256) void dflow(agnes_tally_args a, uint32_t lds_pe
                 }
                 __builtin_amdgcn_wave_barrier();
 
+                }
                 /* RS: the RoundSkip crossing of every (segment, round) of the group */
-                if (SKIP) {
+                if (SKIP && !(ABL & 4u)) {
                     const uint32_t sr = lane >> 3, r = lane & 7u;
                     uint32_t xpos = NONE;
                     bool cross = false;
@@ -862,7 +870,7 @@ __global__ __launch_bounds__(256) void dflow(agnes_tally_args a, uint32_t lds_pe
                 __builtin_amdgcn_wave_barrier();
 
                 /* codes of the group's votes: to_event by (type, level), SKIP, REJECTED */
-                {
+                if (!(ABL & 16u)) {
                     const uint2 lv = *reinterpret_cast<const uint2*>(LO + o8);
                     const uint32_t ev0 = __builtin_amdgcn_perm(EV_HI, EV_LO,
                                                                (lv.x & 0x03030303u) | ((t8[0] & 0x01010101u) << 2));
@@ -921,7 +929,7 @@ __global__ __launch_bounds__(256) void dflow(agnes_tally_args a, uint32_t lds_pe
              * breakpoints are resolved in order on the scalar path; every other vote's message
              * follows from the State between them: TimeoutPrevote (PolkaAny at State.round in
              * Prevote, :196), TimeoutPrecommit (PrecommitAny at State.round, :208) ---- */
-            if (SM) {
+            if (SM && !(ABL & 8u)) {
                 uint32_t lane = lane_id();
                 asm volatile("" : "+v"(lane));
                 const uint32_t o8 = 8u * lane;
@@ -972,6 +980,7 @@ __global__ __launch_bounds__(256) void dflow(agnes_tally_args a, uint32_t lds_pe
                     }
                     uint32_t kxv = 0xFFFFu; /* lane r: round r's crossing in this chunk */
                     if (SKIP && lane < R) kxv = KX[8u * i + lane];
+                    if (ABL && kxv >= CH) kxv = 0xFFFFu; /* (ablations: stale crossings) */
                     /* breakpoints in order: lane j of bpp / bps = position / State after it */
                     uint32_t nbp = 0, bpp = NONE, bps = 0;
                     uint32_t p1_at = NONE, c_at = NONE, dr = 0, sk = 0;
@@ -1128,19 +1137,19 @@ __global__ __launch_bounds__(256) void dflow(agnes_tally_args a, uint32_t lds_pe
                     if (p1 != NONE && (p1 & LOCKF)) { /* locked = {round, v} at P1 */
                         s1.x = s0.z;
                         s1.y = s0.w;
-                        s2.z = DCHK(Sa + (p1 & ~LOCKF) < NV, 12, Sa + (p1 & ~LOCKF), NV) ? a.vb.value[Sa + (p1 & ~LOCKF)] : 0u;
+                        s2.z = (!ABL || (Sa + (p1 & ~LOCKF) < NV)) && DCHK(Sa + (p1 & ~LOCKF) < NV, 12, Sa + (p1 & ~LOCKF), NV) ? a.vb.value[Sa + (p1 & ~LOCKF)] : 0u;
                         flags |= 1u << 8;
                     }
                     if (vp != 0u) { /* valid = {round, v} of the last set_valid_value */
                         s1.z = s0.z;
                         s1.w = s0.w;
-                        s2.w = DCHK(Sa + vp - 1u < NV, 13, Sa + vp - 1u, NV) ? a.vb.value[Sa + vp - 1u] : 0u;
+                        s2.w = (!ABL || (Sa + vp - 1u < NV)) && DCHK(Sa + vp - 1u < NV, 13, Sa + vp - 1u, NV) ? a.vb.value[Sa + vp - 1u] : 0u;
                         flags |= 1u << 16;
                     }
                     if (cc != NONE) { /* the decision */
                         s2.x = rk[R_DR];
                         s2.y = 0u;
-                        n3.x = DCHK(Sa + cc < NV, 14, Sa + cc, NV) ? a.vb.value[Sa + cc] : 0u;
+                        n3.x = (!ABL || (Sa + cc < NV)) && DCHK(Sa + cc < NV, 14, Sa + cc, NV) ? a.vb.value[Sa + cc] : 0u;
                         flags |= 1u << 24;
                     }
                     n3.y = (flags & ~0xFFu) | step;

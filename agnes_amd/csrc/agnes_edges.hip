@@ -112,7 +112,10 @@ __global__ __launch_bounds__(64) void edge_walk(EdgeArgs a) {
 /* window of the aligned path: 64 B per column (four 16-B loads of one 128-B line
  * issued together, so the line is fetched once although the wave's 64 lanes read
  * 64 different lines) */
-constexpr uint32_t EW = 64u;
+#ifndef AGNES_EDGE_W
+#define AGNES_EDGE_W 64
+#endif
+constexpr uint32_t EW = AGNES_EDGE_W;
 
 /* ---- exclusive offsets: inclusive scan of offs[1..n] in place, three kernels ---- */
 constexpr uint32_t SCAN_T = 256u, SCAN_PER = 4u, SCAN_BLK = SCAN_T * SCAN_PER;

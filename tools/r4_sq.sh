@@ -9,9 +9,9 @@ for spec in ${LIBS:-alias=agnes_amd/_exp/lib_alias.so cur=-}; do
   if [ "$path" = "-" ]; then run="python3 bench.py"; else run="python3 tools/withlib.py $path bench.py"; fi
   i=0
   for P in "$P1" "$P2"; do
-    i=$((i+1)); rm -rf gpurun_out/sq/${name}_$i
-    timeout -s KILL 180 rocprofv3 --pmc $P --output-format csv -d gpurun_out/sq/${name}_$i -o p -- $run --config ${CFG:-c4} --no-cpu-baseline --steps 3 --warmup 1 \
-      > gpurun_out/sq/${name}_$i.log 2>&1 || { tail -20 gpurun_out/sq/${name}_$i.log; exit 1; }
+    i=$((i+1)); rm -rf gpurun_out/sq/${name}_${CFG:-c4}_$i
+    timeout -s KILL 180 rocprofv3 --pmc $P --output-format csv -d gpurun_out/sq/${name}_${CFG:-c4}_$i -o p -- $run --config ${CFG:-c4} --no-cpu-baseline --steps 3 --warmup 1 \
+      > gpurun_out/sq/${name}_${CFG:-c4}_$i.log 2>&1 || { tail -20 gpurun_out/sq/${name}_${CFG:-c4}_$i.log; exit 1; }
   done
-  echo "== $name"; python3 tools/pmc_sum.py gpurun_out/sq/${name}_1 "${KSUB:-}" ; python3 tools/pmc_sum.py gpurun_out/sq/${name}_2 "${KSUB:-}"
+  echo "== $name"; python3 tools/pmc_sum.py gpurun_out/sq/${name}_${CFG:-c4}_1 "${KSUB:-}" ; python3 tools/pmc_sum.py gpurun_out/sq/${name}_${CFG:-c4}_2 "${KSUB:-}"
 done
