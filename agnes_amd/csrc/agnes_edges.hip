@@ -60,13 +60,19 @@ __device__ __forceinline__ void load_win(const uint8_t* col, uint64_t w, uint64_
     }
 }
 
-template <bool EMIT, uint32_t W>
+/* REG: up to 8 executors (keys < 8, max_rounds <= 4): their bytes live in one u64
+ * register (byte key), not in LDS — the read-modify-write of a vote's executor byte
+ * is then a 64-bit shift and xor, not an LDS round trip the next vote of the same
+ * executor waits on */
+template <bool EMIT, uint32_t W, bool REG>
 __global__ __launch_bounds__(64) void edge_walk(EdgeArgs a) {
     uint32_t* const tab = reinterpret_cast<uint32_t*>(agnes_smem);
     const uint32_t lane = threadIdx.x;
     const uint32_t i = blockIdx.x * 64u + lane;
     if (i >= a.vb.n_instances) return;
-    for (uint32_t s = 0; s < a.nslots; ++s) tab[s * 64u + lane] = 0u; /* VoteCount::new: level 0 */
+    uint64_t st = 0; /* (REG) VoteCount::new: level 0 */
+    if (!REG)
+        for (uint32_t s = 0; s < a.nslots; ++s) tab[s * 64u + lane] = 0u; /* VoteCount::new: level 0 */
     const uint64_t NV = a.vb.n_votes;
     uint64_t lo = a.vb.offsets[i], hi = a.vb.offsets[i + 1u];
     lo = lo < NV ? lo : NV;
@@ -92,8 +98,9 @@ __global__ __launch_bounds__(64) void edge_walk(EdgeArgs a) {
                 continue;
             /* the executor's byte: level (bits 0..3) | last message (bits 4..7) */
             uint32_t* const p = tab + (key >> 2) * 64u + lane;
-            const uint32_t x = *p, sh = 8u * (key & 3u);
-            const uint32_t old = (x >> sh) & 0xFFu, msg = cb >> AGNES_CODE_MSG_SHIFT;
+            const uint32_t x = REG ? 0u : *p, sh = REG ? 8u * key : 8u * (key & 3u);
+            const uint32_t old = REG ? (uint32_t)(st >> sh) & 0xFFu : (x >> sh) & 0xFFu;
+            const uint32_t msg = cb >> AGNES_CODE_MSG_SHIFT;
             const uint32_t nb = (cb & 0xFu) | (msg ? msg << AGNES_CODE_MSG_SHIFT : old & 0xF0u);
             if (nb != old) {
                 if (EMIT) {
@@ -102,7 +109,8 @@ __global__ __launch_bounds__(64) void edge_walk(EdgeArgs a) {
                         make_uint4((uint32_t)j, (uint32_t)(j >> 32), i, tail);
                 }
                 ++cnt;
-                *p = x ^ ((old ^ nb) << sh);
+                if (REG) st ^= (uint64_t)(old ^ nb) << sh;
+                else *p = x ^ ((old ^ nb) << sh);
             }
         }
     }
@@ -207,21 +215,32 @@ hipError_t agnes_launch_edges(const agnes_vote_batch* vb, const uint8_t* codes, 
     const bool w16 = ((reinterpret_cast<uintptr_t>(codes) | reinterpret_cast<uintptr_t>(vb->round) |
                        reinterpret_cast<uintptr_t>(vb->type)) & 15u) == 0u;
     const dim3 grid((n + 63u) / 64u), blk(64);
-    const size_t lds = (size_t)a.nslots * 64u * sizeof(uint32_t);
+    const bool reg = a.keys <= 8u; /* every executor byte in one u64 register */
+    const size_t lds = reg ? 0u : (size_t)a.nslots * 64u * sizeof(uint32_t);
     if (!out) { /* pass 1: counts, then the exclusive scan */
         hipError_t e = hipMemsetAsync(offs, 0, sizeof(uint64_t), st);
         if (e != hipSuccess || n == 0) return e;
         {
             AgnesKt kt("edge_count", st);
-            if (w16) hipLaunchKernelGGL((edge_walk<false, EW>), grid, blk, lds, st, a);
-            else hipLaunchKernelGGL((edge_walk<false, 4u>), grid, blk, lds, st, a);
+            if (reg) {
+                if (w16) hipLaunchKernelGGL((edge_walk<false, EW, true>), grid, blk, lds, st, a);
+                else hipLaunchKernelGGL((edge_walk<false, 4u, true>), grid, blk, lds, st, a);
+            } else {
+                if (w16) hipLaunchKernelGGL((edge_walk<false, EW, false>), grid, blk, lds, st, a);
+                else hipLaunchKernelGGL((edge_walk<false, 4u, false>), grid, blk, lds, st, a);
+            }
         }
         AgnesKt kt("edge_scan", st);
         return agnes_launch_offsets_scan(offs, n, scratch, st);
     }
     if (n == 0) return hipSuccess;
     AgnesKt kt("edge_emit", st);
-    if (w16) hipLaunchKernelGGL((edge_walk<true, EW>), grid, blk, lds, st, a);
-    else hipLaunchKernelGGL((edge_walk<true, 4u>), grid, blk, lds, st, a);
+    if (reg) {
+        if (w16) hipLaunchKernelGGL((edge_walk<true, EW, true>), grid, blk, lds, st, a);
+        else hipLaunchKernelGGL((edge_walk<true, 4u, true>), grid, blk, lds, st, a);
+    } else {
+        if (w16) hipLaunchKernelGGL((edge_walk<true, EW, false>), grid, blk, lds, st, a);
+        else hipLaunchKernelGGL((edge_walk<true, 4u, false>), grid, blk, lds, st, a);
+    }
     return hipGetLastError();
 }
