@@ -38,6 +38,8 @@ struct agnes_ctx {
     uint32_t list_cap = 0;
     uint64_t* d_scan = nullptr; /* edge-offset scan: block totals */
     uint64_t scan_cap = 0;
+    void* d_dd = nullptr;       /* agnes_dedup_first: bucket counts, scan scratch, (key, index) pairs */
+    uint64_t dd_cap = 0;
     int32_t* d_edtab = nullptr; /* Ed25519 fixed-base table (agnes_wire_ingest), built on first use */
 };
 
@@ -240,6 +242,7 @@ void agnes_ctx_destroy(agnes_ctx* c) {
     if (c->d_err) (void)hipFree(c->d_err);
     if (c->d_list) (void)hipFree(c->d_list);
     if (c->d_scan) (void)hipFree(c->d_scan);
+    if (c->d_dd) (void)hipFree(c->d_dd);
     if (c->d_edtab) (void)hipFree(c->d_edtab);
     if (c->order_ev) (void)hipEventDestroy(c->order_ev);
     delete c;
@@ -706,6 +709,20 @@ static int dedup_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     AGNES_ORDER(c, (hipStream_t)stream);
     if (b->instance_set) return AGNES_E_UNSUPPORTED; /* one instance: its set is reserved % n_sets */
     const uint32_t set = cfg->reserved % (c->n_sets ? c->n_sets : 1u);
+    if (!type_out && b->n_votes && agnes_dedup_bucketed(b->n_votes, cfg->max_rounds, c->n_vals)) {
+        /* the first-index table by a counting sort over key buckets: no global atomics */
+        const uint64_t need = agnes_dedup_scratch_bytes(b->n_votes, cfg->max_rounds, c->n_vals);
+        if (need > c->dd_cap) {
+            if (c->d_dd) AGNES_TRY(hipFree(c->d_dd));
+            c->d_dd = nullptr;
+            c->dd_cap = 0;
+            AGNES_TRY(hipMalloc(&c->d_dd, need));
+            c->dd_cap = need;
+        }
+        return status_of(agnes_launch_dedup_first_bucketed(b, cfg->reserved, cfg->max_rounds, c->n_vals,
+                                                           set < c->n_sets, base, first, c->d_dd,
+                                                           (hipStream_t)stream));
+    }
     return status_of(agnes_launch_dedup(b, cfg->reserved, cfg->max_rounds, c->n_vals, set < c->n_sets, base,
                                         first, type_out, (hipStream_t)stream));
 }

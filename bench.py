@@ -43,7 +43,7 @@ KERNEL_BYTES_PER_VOTE = {
     "tally_list": 15,    # the i64 kernel over the instances the u32 kernels hand over (c2w: all)
     "sweep_walk": 15,
     "apply_codes": 2,    # code + round u8 in (+ the message bytes written back)
-    "dedup_first": 10,   # C5 DEDUP: instance, validator u32 + round, type u8 in (+ 8 B atomic per key)
+    "dedup_first": 10,   # C5 DEDUP: instance, validator u32 + round, type u8 in (bucket sort: + 2x8 B pairs)
     "dedup_mask": 11,    # the same in, the masked type u8 out
     "partials": 22,      # C5 pass A: the 14 B in + the i64 weight column out (the power table
                          # gather hits the cache-resident table: not compulsory HBM traffic)
@@ -66,7 +66,7 @@ KERNEL_SYMBOLS = {
     "tally_list": "agnes::tally_kernel<true, MODE, SKIP, SM, LIST=true>",
     "apply_codes": "agnes::apply::apply_codes<RoundSkip>",
     "partials": "agnes::partials::partials_kernel",
-    "dedup_first": "agnes::dedup::first_kernel",
+    "dedup_first": "agnes::dedup::bucket_{count,prefix,scatter,min}",
     "dedup_mask": "agnes::dedup::mask_kernel",
 }
 

@@ -452,3 +452,44 @@ def test_gpu_dedup_slices_with_bases(eng):
     dd.first(cfg, hb, 0, f)
     assert np.array_equal(fw.cpu().numpy(), f)
     assert np.array_equal(t, dd.mask(cfg, hb, 0, f))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shift", [0, 1, 3])
+def test_gpu_dedup_first_table_prefilled(eng, shift):
+    """agnes_dedup_first (the counting sort over key buckets and LDS minima) and
+    agnes_dedup_mask: the table equals the checker's min over valid votes, with
+    entries the caller set lower kept (the API lowers, it does not overwrite), many
+    buckets (200k keys) and many count blocks (~2.6e5 votes), invalid votes of every
+    kind ignored; shift > 0 hands columns `shift` votes past their allocation (not
+    16-B aligned: the one-vote-per-thread kernels), and the mask equals the checker's."""
+    from agnes_amd.engine import DeviceBatch
+    hb, power, cfg = _dedup_instance(seed=41, n_vals=100_000, R=1)
+    hb.type[::997] = 3
+    hb.round[::1009] = 9
+    hb.validator[::1013] = 10 ** 7
+    eng.upload_power(power)
+    K = 2 * cfg.max_rounds * power.shape[1]
+    base = 123_456_789
+    f0 = np.full(K, ad.INT64_MAX, np.int64)
+    f0[::7] = np.arange(0, K, 7) % 5000   # lower than any base + j: must survive
+    fw = torch.from_numpy(f0.copy()).to(eng.device)
+    db = DeviceBatch.from_host(hb, eng.device)
+    n = hb.n_votes - shift
+    if shift:
+        db = dataclasses.replace(db, instance=db.instance[shift:], round=db.round[shift:], type=db.type[shift:],
+                                 value=db.value[shift:], validator=db.validator[shift:],
+                                 offsets=torch.tensor([0, n], dtype=torch.int64, device=eng.device), n_votes=n)
+    eng.dedup_first(cfg, db, base, fw)
+    tm = torch.empty(n + 4, dtype=torch.uint8, device=eng.device)[shift:shift + n]
+    eng.dedup_mask(cfg, db, base, fw, tm)
+    torch.cuda.synchronize()
+    sl = types.SimpleNamespace(instance=hb.instance[shift:], round=hb.round[shift:], type=hb.type[shift:],
+                               validator=hb.validator[shift:])
+    want = f0.copy()
+    dd = DedupFake(*power.shape)
+    dd.first(cfg, sl, base, want)
+    got = fw.cpu().numpy()
+    assert np.array_equal(got, want)
+    assert (got[1::7] < ad.INT64_MAX).any() and (got[1::7] >= base).all()
+    assert np.array_equal(tm.cpu().numpy(), dd.mask(cfg, sl, base, want))

@@ -27,7 +27,7 @@ KERNELS = {
     "tally_wide": r"agnes::tally_kernel<true, \w+, \w+, \w+, false,",
     "partials": r"agnes::partials::partials_kernel",
     "fold": r"agnes::fold::fold_",
-    "dedup_first": r"agnes::dedup::first_kernel",
+    "dedup_first": r"agnes::dedup::(first_kernel|bucket_)",
     "dedup_mask": r"agnes::dedup::mask_kernel",
     "dedup_reject": r"agnes::dedup::reject_kernel",
     "edge_count": r"agnes::edges::edge_walk<false,",
@@ -46,8 +46,11 @@ def per_launch(path, counter):
             continue
         for k, pat in KERNELS.items():
             if re.search(pat, r["Kernel_Name"]):
-                vals.setdefault(k, []).append(float(r["Counter_Value"]))
-    return {k: (statistics.median(v), len(v)) for k, v in vals.items()}
+                vals.setdefault(k, {}).setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
+    # an engine step of several kernels (dedup_first: count, prefix, scatter, min): the
+    # sum of each kernel's median per launch
+    return {k: (sum(statistics.median(v) for v in by.values()), max(len(v) for v in by.values()))
+            for k, by in vals.items()}
 
 
 def main():
