@@ -700,8 +700,9 @@ int agnes_events(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* 
 
 /* ---------------- DEDUP for a split instance ---------------- */
 
+/* fused: agnes_dedup_first_mask (first and type_out from one counting sort) */
 static int dedup_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint64_t base,
-                      uint64_t* first, uint8_t* type_out, void* stream) {
+                      uint64_t* first, uint8_t* type_out, void* stream, bool fused = false) {
     if (!c || !cfg_ok(cfg) || !b || !first) return AGNES_E_INVALID;
     if (b->n_votes && (!b->instance || !b->round || !b->type || !b->validator)) return AGNES_E_INVALID;
     if (c->n_vals == 0) return AGNES_E_INVALID; /* no power table: no validator range */
@@ -709,7 +710,7 @@ static int dedup_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     AGNES_ORDER(c, (hipStream_t)stream);
     if (b->instance_set) return AGNES_E_UNSUPPORTED; /* one instance: its set is reserved % n_sets */
     const uint32_t set = cfg->reserved % (c->n_sets ? c->n_sets : 1u);
-    if (!type_out && b->n_votes && agnes_dedup_bucketed(b->n_votes, cfg->max_rounds, c->n_vals)) {
+    if ((!type_out || fused) && b->n_votes && agnes_dedup_bucketed(b->n_votes, cfg->max_rounds, c->n_vals)) {
         /* the first-index table by a counting sort over key buckets: no global atomics */
         const uint64_t need = agnes_dedup_scratch_bytes(b->n_votes, cfg->max_rounds, c->n_vals);
         if (need > c->dd_cap) {
@@ -720,8 +721,13 @@ static int dedup_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
             c->dd_cap = need;
         }
         return status_of(agnes_launch_dedup_first_bucketed(b, cfg->reserved, cfg->max_rounds, c->n_vals,
-                                                           set < c->n_sets, base, first, c->d_dd,
-                                                           (hipStream_t)stream));
+                                                           set < c->n_sets, base, first, fused ? type_out : nullptr,
+                                                           c->d_dd, (hipStream_t)stream));
+    }
+    if (fused) { /* outside the bucketed domain: the two passes */
+        const int rc = status_of(agnes_launch_dedup(b, cfg->reserved, cfg->max_rounds, c->n_vals, set < c->n_sets,
+                                                    base, first, nullptr, (hipStream_t)stream));
+        if (rc != AGNES_OK) return rc;
     }
     return status_of(agnes_launch_dedup(b, cfg->reserved, cfg->max_rounds, c->n_vals, set < c->n_sets, base,
                                         first, type_out, (hipStream_t)stream));
@@ -737,6 +743,13 @@ int agnes_dedup_mask(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_bat
     if (!type_out && b && b->n_votes) return AGNES_E_INVALID;
     if (b && b->n_votes == 0) return AGNES_OK;
     return dedup_impl(c, cfg, b, base, const_cast<uint64_t*>(first), type_out, stream);
+}
+
+int agnes_dedup_first_mask(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint64_t base,
+                           uint64_t* first, uint8_t* type_out, void* stream) {
+    if (!type_out && b && b->n_votes) return AGNES_E_INVALID;
+    if (b && b->n_votes == 0) return AGNES_OK;
+    return dedup_impl(c, cfg, b, base, first, type_out, stream, true);
 }
 
 int agnes_dedup_reject(agnes_ctx* c, const uint8_t* type_masked, uint64_t n, uint8_t* codes, void* stream) {

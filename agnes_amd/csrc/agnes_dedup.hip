@@ -222,9 +222,13 @@ __global__ __launch_bounds__(256) void bucket_prefix(uint32_t G, uint32_t* cnt, 
     if (t == 0u) rowtot[blockIdx.x] = carry;
 }
 
-template <bool V4>
+/* MASK (agnes_dedup_first_mask): also the mask's defaults, AGNES_TYPE_MASKED for a
+ * valid vote (the min pass writes the firsts' types over it) and 0xFF for an invalid
+ * one; the pair then carries the vote's type in bit 13 */
+template <bool V4, bool MASK>
 __global__ __launch_bounds__(256) void bucket_scatter(DedupArgs a, uint32_t nb, uint32_t G, const uint32_t* cnt,
-                                                      const uint32_t* rowtot, uint32_t* bstart, uint2* pairs) {
+                                                      const uint32_t* rowtot, uint32_t* bstart, uint2* pairs,
+                                                      uint8_t* type_out) {
     __shared__ uint32_t cur[MAX_NB + 1u];
     const uint32_t g = blockIdx.x;
     for (uint32_t b = threadIdx.x; b < nb; b += 256u) cur[b] = rowtot[b];
@@ -243,15 +247,27 @@ __global__ __launch_bounds__(256) void bucket_scatter(DedupArgs a, uint32_t nb, 
         for (uint32_t s = 0; s < 4u; ++s) {
             if ((ok >> s) & 1u) {
                 const uint32_t p = atomicAdd(&cur[(uint32_t)(key[s] / KB)], 1u);
-                pairs[p] = make_uint2((uint32_t)(key[s] % KB), (uint32_t)(j + s));
+                /* key % KB = (r * 2 + t) * n_vals + x mod KB; the type from the key is not
+                 * recoverable here, so MASK reads it (bit 13) */
+                const uint32_t tb = MASK ? ((uint32_t)a.type[j + s] << 13) : 0u;
+                pairs[p] = make_uint2((uint32_t)(key[s] % KB) | tb, (uint32_t)(j + s));
             }
+        }
+        if (MASK) {
+            uint32_t o = 0;
+#pragma unroll
+            for (uint32_t s = 0; s < 4u; ++s) o |= (((ok >> s) & 1u) ? AGNES_TYPE_MASKED : 0xFFu) << (8u * s);
+            if (V4 && j + 4u <= a.n_votes) *reinterpret_cast<uint32_t*>(type_out + j) = o;
+            else
+                for (uint32_t s = 0; s < 4u && j + s < j1; ++s) type_out[j + s] = (uint8_t)(o >> (8u * s));
         }
     }
 }
 
 constexpr uint32_t MT = 1024u; /* threads of a min block (one block per CU) */
+template <bool MASK>
 __global__ __launch_bounds__(MT) void bucket_min(uint64_t n_keys, const uint32_t* bstart, const uint2* pairs,
-                                                 uint64_t base, unsigned long long* first) {
+                                                 uint64_t base, unsigned long long* first, uint8_t* type_out) {
     __shared__ uint32_t tab[KB];
     const uint32_t b = blockIdx.x;
     for (uint32_t k = threadIdx.x; k < KB; k += MT) tab[k] = 0xFFFFFFFFu;
@@ -259,7 +275,7 @@ __global__ __launch_bounds__(MT) void bucket_min(uint64_t n_keys, const uint32_t
     const uint32_t e0 = bstart[b], e1 = bstart[b + 1u];
     for (uint32_t e = e0 + threadIdx.x; e < e1; e += MT) {
         const uint2 q = pairs[e];
-        atomicMin(&tab[q.x], q.y);
+        atomicMin(&tab[q.x & (KB - 1u)], q.y);
     }
     __syncthreads();
     const uint64_t k0 = (uint64_t)b * KB;
@@ -268,6 +284,14 @@ __global__ __launch_bounds__(MT) void bucket_min(uint64_t n_keys, const uint32_t
         if (x != 0xFFFFFFFFu) {
             const unsigned long long v = base + x, old = first[k0 + k];
             if (v < old) first[k0 + k] = v;
+            if (MASK && v > old) tab[k] = 0xFFFFFFFFu; /* a lower entry the caller left: no first here */
+        }
+    }
+    if (MASK) { /* the firsts' types over the scatter's AGNES_TYPE_MASKED */
+        __syncthreads();
+        for (uint32_t e = e0 + threadIdx.x; e < e1; e += MT) {
+            const uint2 q = pairs[e];
+            if (tab[q.x & (KB - 1u)] == q.y) type_out[q.y] = (uint8_t)(q.x >> 13);
         }
     }
 }
@@ -327,7 +351,7 @@ uint64_t agnes_dedup_scratch_bytes(uint64_t n_votes, uint32_t max_rounds, uint32
 
 hipError_t agnes_launch_dedup_first_bucketed(const agnes_vote_batch* vb, uint32_t inst_id, uint32_t max_rounds,
                                              uint32_t n_vals, bool set_ok, uint64_t base, uint64_t* first,
-                                             void* scratch, hipStream_t st) {
+                                             uint8_t* type_out, void* scratch, hipStream_t st) {
     using namespace agnes::dedup;
     if (vb->n_votes == 0) return hipSuccess;
     const DedupArgs a{vb->instance, vb->round, vb->type, vb->validator, vb->n_votes,
@@ -341,15 +365,21 @@ hipError_t agnes_launch_dedup_first_bucketed(const agnes_vote_batch* vb, uint32_
     uint32_t* const rowtot = reinterpret_cast<uint32_t*>(sp + o1);
     uint32_t* const bstart = reinterpret_cast<uint32_t*>(sp + o2);
     uint2* const pairs = reinterpret_cast<uint2*>(sp + o3);
-    const bool v4 = dedup_v4(vb);
-    AgnesKt kt("dedup_first", st);
+    const bool v4 = dedup_v4(vb) && (reinterpret_cast<uintptr_t>(type_out) & 3u) == 0u;
+    unsigned long long* const f = reinterpret_cast<unsigned long long*>(first);
+    AgnesKt kt(type_out ? "dedup_first_mask" : "dedup_first", st);
     if (v4) hipLaunchKernelGGL(bucket_count<true>, dim3(G), dim3(256), 0, st, a, nb, G, cnt);
     else hipLaunchKernelGGL(bucket_count<false>, dim3(G), dim3(256), 0, st, a, nb, G, cnt);
     hipLaunchKernelGGL(bucket_prefix, dim3(nb), dim3(256), 0, st, G, cnt, rowtot);
-    if (v4) hipLaunchKernelGGL(bucket_scatter<true>, dim3(G), dim3(256), 0, st, a, nb, G, cnt, rowtot, bstart, pairs);
-    else hipLaunchKernelGGL(bucket_scatter<false>, dim3(G), dim3(256), 0, st, a, nb, G, cnt, rowtot, bstart, pairs);
-    hipLaunchKernelGGL(bucket_min, dim3(nb), dim3(MT), 0, st, n_keys, bstart, pairs, base,
-                       reinterpret_cast<unsigned long long*>(first));
+    if (type_out) {
+        if (v4) hipLaunchKernelGGL((bucket_scatter<true, true>), dim3(G), dim3(256), 0, st, a, nb, G, cnt, rowtot, bstart, pairs, type_out);
+        else hipLaunchKernelGGL((bucket_scatter<false, true>), dim3(G), dim3(256), 0, st, a, nb, G, cnt, rowtot, bstart, pairs, type_out);
+        hipLaunchKernelGGL(bucket_min<true>, dim3(nb), dim3(MT), 0, st, n_keys, bstart, pairs, base, f, type_out);
+    } else {
+        if (v4) hipLaunchKernelGGL((bucket_scatter<true, false>), dim3(G), dim3(256), 0, st, a, nb, G, cnt, rowtot, bstart, pairs, type_out);
+        else hipLaunchKernelGGL((bucket_scatter<false, false>), dim3(G), dim3(256), 0, st, a, nb, G, cnt, rowtot, bstart, pairs, type_out);
+        hipLaunchKernelGGL(bucket_min<false>, dim3(nb), dim3(MT), 0, st, n_keys, bstart, pairs, base, f, type_out);
+    }
     return hipGetLastError();
 }
 

@@ -180,9 +180,11 @@ hipError_t agnes_launch_dedup(const agnes_vote_batch* vb, uint32_t inst_id, uint
  * LDS minima): when agnes_dedup_bucketed; scratch: agnes_dedup_scratch_bytes */
 bool agnes_dedup_bucketed(uint64_t n_votes, uint32_t max_rounds, uint32_t n_vals);
 uint64_t agnes_dedup_scratch_bytes(uint64_t n_votes, uint32_t max_rounds, uint32_t n_vals);
+/* type_out != nullptr (agnes_dedup_first_mask): also the mask, for a batch that is the
+ * whole stream (no other slice's votes min-combined into first afterwards) */
 hipError_t agnes_launch_dedup_first_bucketed(const agnes_vote_batch* vb, uint32_t inst_id, uint32_t max_rounds,
                                              uint32_t n_vals, bool set_ok, uint64_t base, uint64_t* first,
-                                             void* scratch, hipStream_t stream);
+                                             uint8_t* type_out, void* scratch, hipStream_t stream);
 hipError_t agnes_launch_dedup_reject(const uint8_t* type_masked, uint64_t n, uint8_t* codes, hipStream_t stream);
 
 #define AGNES_WAVES_PER_BLOCK 4

@@ -334,7 +334,7 @@ def one_instance_states(sm_scan, sm_apply, sm_finish, marks: torch.Tensor, group
 
 def tally_one_instance_dedup(tally_carried, dedup_first, dedup_mask, dedup_reject, n_votes: int,
                              n_vals: int, cfg: abi.Config, n_segments: int, device, base: int = 0,
-                             group=None, offsets=None, fold=None, partials=None):
+                             group=None, offsets=None, fold=None, partials=None, dedup_first_mask=None):
     """C5 in DEDUP mode ("DEDUP mode adds an all-reduce(min) on
     first_index").  A vote's slice cannot see whether an earlier slice (or rank)
     already counted its (round, type, validator), so the first vote of every key is
@@ -353,14 +353,19 @@ def tally_one_instance_dedup(tally_carried, dedup_first, dedup_mask, dedup_rejec
     tally_one_instance's, for a HIP-graph capture).  A stream
     continued across calls would also carry `first`; not offered here.
     The instance's id is cfg.reserved, for the DEDUP checks and for the carried
-    tally alike (one source)."""
+    tally alike (one source).  With one rank, dedup_first_mask(base, first) (the
+    fused agnes_dedup_first_mask), when given, replaces the first / mask pair."""
     first = torch.full((2 * cfg.max_rounds * n_vals,), INT64_MAX, dtype=torch.int64, device=device)
-    dedup_first(base, first)
-    if dist.is_initialized() and dist.get_world_size(group) > 1:
-        t = first.to(_device_for(group))
-        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)         # the DEDUP exchange step
-        first = t.to(device)
-    dedup_mask(base, first)
+    multi = dist.is_initialized() and dist.get_world_size(group) > 1
+    if dedup_first_mask is not None and not multi:
+        dedup_first_mask(base, first)
+    else:
+        dedup_first(base, first)
+        if multi:
+            t = first.to(_device_for(group))
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)         # the DEDUP exchange step
+            first = t.to(device)
+        dedup_mask(base, first)
     ref = abi.Config(abi.MODE_REFERENCE, cfg.flags, cfg.max_rounds, cfg.reserved)
     out = tally_one_instance(tally_carried, n_votes, ref, n_segments, device, cfg.reserved, group,
                              offsets=offsets, fold=fold, partials=partials)

@@ -325,6 +325,18 @@ class Engine:
         check(self.lib.agnes_dedup_mask(self.ctx, C.byref(cfg), C.byref(b), base, _ptr(first), _ptr(type_out),
                                         _stream_handle(stream)), "agnes_dedup_mask")
 
+    def dedup_first_mask(self, cfg: abi.Config, batch: DeviceBatch, base: int, first: torch.Tensor,
+                         type_out: torch.Tensor, stream=None):
+        """agnes_dedup_first_mask: dedup_first + dedup_mask in one call, for a batch holding
+        every vote of the instance (one rank)."""
+        if first.dtype != torch.int64 or first.numel() < 2 * cfg.max_rounds * self.n_vals:
+            raise ValueError("first must be an int64 [2 * max_rounds * n_vals] tensor")
+        if type_out.dtype != torch.uint8 or type_out.numel() < batch.n_votes:
+            raise ValueError("type_out must be a uint8 tensor of n_votes")
+        b = batch.c()
+        check(self.lib.agnes_dedup_first_mask(self.ctx, C.byref(cfg), C.byref(b), base, _ptr(first), _ptr(type_out),
+                                              _stream_handle(stream)), "agnes_dedup_first_mask")
+
     def dedup_reject(self, type_masked: torch.Tensor, codes: torch.Tensor, n_votes: int, stream=None):
         check(self.lib.agnes_dedup_reject(self.ctx, _ptr(type_masked), n_votes, _ptr(codes),
                                           _stream_handle(stream)), "agnes_dedup_reject")

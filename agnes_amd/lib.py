@@ -96,6 +96,8 @@ def load():
         "agnes_dedup_first": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), C.c_uint64, P, P], C.c_int),
         "agnes_dedup_mask": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), C.c_uint64, P, P, P],
                              C.c_int),
+        "agnes_dedup_first_mask": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), C.c_uint64, P, P, P],
+                                   C.c_int),
         "agnes_dedup_reject": ([P, P, C.c_uint64, P, P], C.c_int),
         "agnes_gen_instance_votes": ([C.POINTER(abi.GenParams), C.c_uint32], C.c_uint64),
         "agnes_gen_offsets": ([C.POINTER(abi.GenParams), P], C.c_int),

@@ -45,6 +45,7 @@ KERNEL_BYTES_PER_VOTE = {
     "apply_codes": 2,    # code + round u8 in (+ the message bytes written back)
     "dedup_first": 10,   # C5 DEDUP: instance, validator u32 + round, type u8 in (bucket sort: + 2x8 B pairs)
     "dedup_mask": 11,    # the same in, the masked type u8 out
+    "dedup_first_mask": 11,  # one rank: both in one counting sort (10 B in, the masked type out)
     "partials": 22,      # C5 pass A: the 14 B in + the i64 weight column out (the power table
                          # gather hits the cache-resident table: not compulsory HBM traffic)
 }
@@ -68,6 +69,7 @@ KERNEL_SYMBOLS = {
     "partials": "agnes::partials::partials_kernel",
     "dedup_first": "agnes::dedup::bucket_{count,prefix,scatter,min}",
     "dedup_mask": "agnes::dedup::mask_kernel",
+    "dedup_first_mask": "agnes::dedup::bucket_{count,prefix,scatter,min}<MASK>",
 }
 
 WORKLOADS = {
@@ -564,7 +566,8 @@ def bench_one_instance(args, w, eng, rank, world):
                 tc, lambda base, f: eng.dedup_first(cfg, src, base, f),
                 lambda base, f: eng.dedup_mask(cfg, src, base, f, tmask),
                 lambda: eng.dedup_reject(tmask, codes, hi - lo), hi - lo, p.n_vals, cfg, segs,
-                eng.device, base=lo, offsets=off, fold=eng.fold_counts, partials=pa)
+                eng.device, base=lo, offsets=off, fold=eng.fold_counts, partials=pa,
+                dedup_first_mask=lambda base, f: eng.dedup_first_mask(cfg, src, base, f, tmask))
         return adist.tally_one_instance(tc, hi - lo, cfg, segs, eng.device, 0, None, offsets=off,
                                         fold=eng.fold_counts, partials=pa)
 

@@ -364,7 +364,7 @@ def test_gpu_tally_carried_rejects(eng):
         eng.tally_carried(abi.config(abi.MODE_DEDUP, 0, 1), db, codes, counts)
 
 
-def _gpu_dedup_run(eng, hb, power, cfg, segments, hip_fold=True):
+def _gpu_dedup_run(eng, hb, power, cfg, segments, hip_fold=True, fused=False):
     from agnes_amd.engine import DeviceBatch
     eng.upload_power(power)
     db = DeviceBatch.from_host(hb, eng.device)
@@ -377,18 +377,21 @@ def _gpu_dedup_run(eng, hb, power, cfg, segments, hip_fold=True):
                                 lambda base, f: eng.dedup_mask(cfg, db, base, f, tmask),
                                 lambda: eng.dedup_reject(tmask, codes, n),
                                 n, power.shape[1], cfg, segments, eng.device,
-                                fold=eng.fold_counts if hip_fold else None)
+                                fold=eng.fold_counts if hip_fold else None,
+                                dedup_first_mask=(lambda base, f: eng.dedup_first_mask(cfg, db, base, f, tmask))
+                                if fused else None)
     torch.cuda.synchronize()
     return codes.cpu().numpy()
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("segments,n_vals,R", [(1, 3000, 1), (16, 5000, 2), (300, 20000, 2),
                                                (64, 100000, 1)])
-def test_gpu_split_instance_dedup(eng, segments, n_vals, R):
+def test_gpu_split_instance_dedup(eng, segments, n_vals, R, fused):
     hb, power, cfg = _dedup_instance(seed=31 + segments, n_vals=n_vals, R=R)
     want, _, _ = ol.tally(cfg, hb, power)
-    got = _gpu_dedup_run(eng, hb, power, cfg, segments)
+    got = _gpu_dedup_run(eng, hb, power, cfg, segments, fused=fused)
     assert np.array_equal(got, want)
     assert (got == abi.CODE_REJECTED).any()
 
@@ -455,8 +458,9 @@ def test_gpu_dedup_slices_with_bases(eng):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("shift", [0, 1, 3])
-def test_gpu_dedup_first_table_prefilled(eng, shift):
+def test_gpu_dedup_first_table_prefilled(eng, shift, fused):
     """agnes_dedup_first (the counting sort over key buckets and LDS minima) and
     agnes_dedup_mask: the table equals the checker's min over valid votes, with
     entries the caller set lower kept (the API lowers, it does not overwrite), many
@@ -480,9 +484,12 @@ def test_gpu_dedup_first_table_prefilled(eng, shift):
         db = dataclasses.replace(db, instance=db.instance[shift:], round=db.round[shift:], type=db.type[shift:],
                                  value=db.value[shift:], validator=db.validator[shift:],
                                  offsets=torch.tensor([0, n], dtype=torch.int64, device=eng.device), n_votes=n)
-    eng.dedup_first(cfg, db, base, fw)
     tm = torch.empty(n + 4, dtype=torch.uint8, device=eng.device)[shift:shift + n]
-    eng.dedup_mask(cfg, db, base, fw, tm)
+    if fused:  # agnes_dedup_first_mask: the same table and mask from one counting sort
+        eng.dedup_first_mask(cfg, db, base, fw, tm)
+    else:
+        eng.dedup_first(cfg, db, base, fw)
+        eng.dedup_mask(cfg, db, base, fw, tm)
     torch.cuda.synchronize()
     sl = types.SimpleNamespace(instance=hb.instance[shift:], round=hb.round[shift:], type=hb.type[shift:],
                                validator=hb.validator[shift:])

@@ -100,7 +100,7 @@ def test_full_c4_shard(eng):
     assert (codes == abi.CODE_REJECTED).any()
 
 
-def _c5(eng, dedup):
+def _c5(eng, dedup, fused=False):
     n_vals = 1_000_000
     gen = dict(n_instances=1, n_vals=n_vals, rounds_min=1, rounds_max=1, nil_permille=200)
     if dedup:
@@ -123,7 +123,9 @@ def _c5(eng, dedup):
         ad.tally_one_instance_dedup(tc, lambda base, f: eng.dedup_first(cfg, db, base, f),
                                     lambda base, f: eng.dedup_mask(cfg, db, base, f, tmask),
                                     lambda: eng.dedup_reject(tmask, codes, n), n, n_vals, cfg, 1024,
-                                    eng.device)
+                                    eng.device,
+                                    dedup_first_mask=(lambda base, f: eng.dedup_first_mask(cfg, db, base, f, tmask))
+                                    if fused else None)
     else:
         ad.tally_one_instance(tc, n, cfg, 1024, eng.device)
     torch.cuda.synchronize()
@@ -141,6 +143,7 @@ def test_full_c5_reference(eng):
     assert (want & abi.CODE_EVENT_MASK).any()
 
 
-def test_full_c5_dedup(eng):
-    want = _c5(eng, True)
+@pytest.mark.parametrize("fused", [False, True])
+def test_full_c5_dedup(eng, fused):
+    want = _c5(eng, True, fused)
     assert (want == abi.CODE_REJECTED).sum() > len(want) // 20

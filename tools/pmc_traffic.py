@@ -28,6 +28,7 @@ KERNELS = {
     "partials": r"agnes::partials::partials_kernel",
     "fold": r"agnes::fold::fold_",
     "dedup_first": r"agnes::dedup::(first_kernel|bucket_)",
+    "dedup_first_mask": r"agnes::dedup::bucket_",
     "dedup_mask": r"agnes::dedup::mask_kernel",
     "dedup_reject": r"agnes::dedup::reject_kernel",
     "edge_count": r"agnes::edges::edge_walk<false,",
