@@ -346,7 +346,8 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     if (a.states && states_in && states_in != states) {
         /* the sweep route reads the input States itself; the other routes work in place */
         const uint32_t route = (cfg->flags >> AGNES_ROUTE_SHIFT) & AGNES_ROUTE_MASK;
-        const bool sweep = !wide_all && !w64 && route == AGNES_ROUTE_AUTO && cfg->mode == AGNES_MODE_REFERENCE &&
+        const bool sweep = !wide_all && (!w64 || cfg->max_rounds == 1u) && route == AGNES_ROUTE_AUTO &&
+                           cfg->mode == AGNES_MODE_REFERENCE &&
                            !(cfg->flags & AGNES_FLAG_ROUND_SKIP) && cfg->max_rounds <= 15u;
         if (sweep) {
             a.states_in = states_in;

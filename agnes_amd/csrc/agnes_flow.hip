@@ -73,6 +73,8 @@ constexpr uint32_t SMALLB = AGNES_FLOW_SMALLB; /* batch size of the work queue's
  * found (the vote's value is still in registers). */
 constexpr uint32_t R_Q2 = 0, R_PBASE = 1, R_NV = 2, R_EQ8 = 3, R_SMASK = 4, R_EQ = 5, R_VALL = 6, R_STEP = 7, R_P1 = 8,
                    R_C = 9, R_DF = 10, R_DR = 11, RECW = 12;
+/* (W64) the threshold's high word; 16-word records */
+constexpr uint32_t R_Q2H = 12, RECW64 = 16;
 constexpr uint32_t F_LOCK = 0x100u;
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 
@@ -90,11 +92,14 @@ constexpr uint32_t EV_LO = AGNES_CODE_NONE | (AGNES_CODE_POLKA_ANY << 8) | (AGNE
 constexpr uint32_t EV_HI = AGNES_CODE_NONE | (AGNES_CODE_PRECOMMIT_ANY << 8) | (AGNES_CODE_NONE << 16) |
                            (AGNES_CODE_PRECOMMIT_VALUE << 24);
 
-__host__ __device__ inline uint32_t carry_bytes(uint32_t R) { return (uint32_t)align16(32ull * R); }
-/* per-wave LDS: DMA slot | carried executors (2 copies x (vw[2R], vn[2R]) u32) |
- * instance records | (State machine) valid candidates, two batches' staged States */
-__host__ __device__ inline uint32_t lds_bytes(bool sm, uint32_t R, bool evc = false) {
-    return F_BYTES + carry_bytes(R) + FB * RECW * 4u + (sm ? FB * 8u + 2u * FB * 64u : 0u) + (evc ? FB * 4u : 0u);
+__host__ __device__ inline uint32_t carry_bytes(uint32_t R, bool w64 = false) {
+    return (uint32_t)align16((w64 ? 64ull : 32ull) * R);
+}
+/* per-wave LDS: DMA slot | carried executors (2 copies x (vw[2R], vn[2R]) u32, or u64
+ * for W64) | instance records | (State machine) valid candidates, two batches' staged States */
+__host__ __device__ inline uint32_t lds_bytes(bool sm, uint32_t R, bool evc = false, bool w64 = false) {
+    return F_BYTES + carry_bytes(R, w64) + FB * (w64 ? RECW64 : RECW) * 4u + (sm ? FB * 8u + 2u * FB * 64u : 0u) +
+           (evc ? FB * 4u : 0u);
 }
 
 /* a State out (plain stores: non-temporal ones measured slower on C2) */
@@ -182,7 +187,8 @@ struct Hdr {
     uint32_t olo, ohi;  /* lanes 0..m: offset                                     */
     uint32_t hs;        /* lane k < m: the power set of instance k                */
     uint32_t q2, mp;    /* lane k: set q2, maxpow; after stage 3 q2 = threshold   */
-    uint32_t fa, ln;    /* lane k: set fast flag (2: no such set), length         */
+    uint32_t q2h, mph;  /* (W64) their high words                                */
+    uint32_t fa, ln;    /* lane k: set fast flag (W64: w64 flag; 2: no such set), length */
     uint32_t stage;     /* 1, 2, 3 (ready)                                       */
     uint32_t stream;    /* stage 2: the offsets pass; stage 3: walked by this kernel */
 };
@@ -190,8 +196,12 @@ struct Hdr {
 /* EVC: also the number of event records of each instance of a flow batch (votes whose
  * code is Some(Event), 1..5: this route never sets the RoundSkip bit) into
  * a.ev_counts[instance] -- the count pass of the event stream (agnes_events.hip) */
-template <bool PC, bool SM, bool R1, bool EVC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void flow(agnes_tally_args a, uint32_t lds_per_wave) {
+/* W64 (one round, round 4): the u64 domain (agnes_fast.h defer_si) — weights from the
+ * i64 power table and the four buckets of K2 as u64 sums instead of 16-bit fields */
+template <bool PC, bool SM, bool R1, bool EVC, bool W64>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? 2 : 3))) void flow(agnes_tally_args a, uint32_t lds_per_wave) {
+    static_assert(!W64 || (R1 && !PC && !EVC), "W64: one round, no u32 power table, no record counts");
+    constexpr uint32_t RW = W64 ? RECW64 : RECW; /* record words */
 
     const uint32_t lane = lane_id();
     const uint32_t wave = rfl(threadIdx.x >> 6);
@@ -210,11 +220,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
     unsigned char* const slot = base;
     const uint32_t slotl = lds_addr(slot);
     uint32_t* const crow = reinterpret_cast<uint32_t*>(base + F_BYTES);
-    const uint32_t cw = 4u * R; /* one carry copy: vw[2R] then vn[2R] */
-    uint32_t* const itab = reinterpret_cast<uint32_t*>(base + F_BYTES + carry_bytes(R));
-    unsigned long long* const vtab = reinterpret_cast<unsigned long long*>(base + F_BYTES + carry_bytes(R) + FB * RECW * 4u);
-    unsigned char* const sb = base + F_BYTES + carry_bytes(R) + FB * RECW * 4u + FB * 8u;
-    uint32_t* const etab = reinterpret_cast<uint32_t*>(base + F_BYTES + carry_bytes(R) + FB * RECW * 4u +
+    const uint32_t cw = (W64 ? 8u : 4u) * R; /* one carry copy: vw[2R] then vn[2R] (u32 words) */
+    const uint32_t CB = carry_bytes(R, W64);
+    uint32_t* const itab = reinterpret_cast<uint32_t*>(base + F_BYTES + CB);
+    unsigned long long* const vtab = reinterpret_cast<unsigned long long*>(base + F_BYTES + CB + FB * RW * 4u);
+    unsigned char* const sb = base + F_BYTES + CB + FB * RW * 4u + FB * 8u;
+    uint32_t* const etab = reinterpret_cast<uint32_t*>(base + F_BYTES + CB + FB * RW * 4u +
                                                        (SM ? FB * 8u + 2u * FB * 64u : 0u)); /* (EVC) records */
     const agnes_state* const st_in = a.states_in ? a.states_in : a.states;
     uint32_t cpar = 0;
@@ -265,15 +276,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
         const uint64_t oe = u64of(shfl(h.olo, lane + 1u), shfl(h.ohi, lane + 1u));
         const uint64_t len = il && oe > ob ? oe - ob : 0ull;
         h.ln = len < (1ull << 31) ? (uint32_t)len : (1u << 31);
-        uint32_t q2 = 0, mp = 0, fa = 2;
+        uint32_t q2 = 0, mp = 0, fa = 2, q2h = 0, mph = 0;
         if (il && h.hs < ns) {
             const agnes_set_info* const si = a.sets + h.hs;
-            q2 = si->q2;
-            mp = si->maxpow;
-            fa = si->fast;
+            if (W64) {
+                q2 = (uint32_t)si->q2w;
+                q2h = (uint32_t)(si->q2w >> 32);
+                mp = (uint32_t)si->maxw;
+                mph = (uint32_t)(si->maxw >> 32);
+                fa = si->w64;
+            } else {
+                q2 = si->q2;
+                mp = si->maxpow;
+                fa = si->fast;
+            }
         }
         h.q2 = q2;
         h.mp = mp;
+        h.q2h = q2h;
+        h.mph = mph;
         h.fa = fa;
         const bool badl = (lane <= m && (h.olo & 3u) != 0u) || (lane < m && oe < ob);
         const uint64_t O0 = u64of(rdl(h.olo, 0u), rdl(h.ohi, 0u)), Om = u64of(rdl(h.olo, m), rdl(h.ohi, m));
@@ -287,7 +308,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
         uint32_t q2 = 0;
         if (il) {
             const uint64_t len = h.ln;
-            if (h.fa != 2u) {
+            if (W64 && h.fa != 2u) {
+                /* u64 sums below 2^61 (defer_si's test): thresholds in two words */
+                const uint64_t mw = u64of(h.mp, h.mph);
+                fl = h.fa != 0u && len < (1ull << 30) && __umul64hi(len, mw) == 0ull && len * mw < (1ull << 61);
+                q2 = h.q2;
+            } else if (h.fa != 2u) {
                 const uint64_t wmax = len * (uint64_t)h.mp; /* no sum of the instance exceeds it */
                 /* u32 sums, per-lane bucket prefixes < 2^15 (8 votes x maxpow), signed thresholds */
                 fl = h.fa != 0u && len < (1ull << 30) && wmax < (1ull << 30) && h.mp < 4096u;
@@ -350,7 +376,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
      * locked / decision values are in them already, the valid one is in vtab) */
     auto finalize = [&](uint32_t mm, uint32_t s0, const unsigned char* sbp) {
         if (lane < mm) {
-            const uint32_t* const rk = itab + RECW * lane;
+            const uint32_t* const rk = itab + RW * lane;
             const uint32_t p1 = rk[R_P1], cc = rk[R_C], df = rk[R_DF];
             const unsigned long long vv = vtab[lane];
             uint32_t* const sp = reinterpret_cast<uint32_t*>(const_cast<unsigned char*>(sbp) + 64u * lane);
@@ -396,7 +422,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
         } else {
             /* the instance records' constants (written at the first chunk's top, once the
              * batch before has been finalized from its records) */
-            const uint32_t q2k = H.q2;
+            const uint32_t q2k = H.q2, q2hk = H.q2h;
             const uint32_t setk = H.hs;
             /* the stream: instance starts relative to its first vote */
             const uint64_t S0 = u64of(rdl(H.olo, 0u), rdl(H.ohi, 0u));
@@ -422,8 +448,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                  * K2-K4 work (same-box A/B: flow -1 % on C2 and C3) */
                 __builtin_amdgcn_s_setprio(1);
                 if (rc == 0u && lane < m) { /* instance records */
-                    uint32_t* const rk = itab + RECW * lane;
+                    uint32_t* const rk = itab + RW * lane;
                     rk[R_Q2] = q2k;
+                    if (W64) rk[R_Q2H] = q2hk;
                     rk[R_PBASE] = setk < ns ? setk * nv : 0u;
                     rk[R_NV] = setk < ns ? nv : 0u;
                     rk[R_SMASK] = 0u; /* no State machine: no role */
@@ -441,7 +468,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                         const uint32_t step = sp[13] & 0xFFu;
                         uint32_t smask = __builtin_amdgcn_perm(SM_HI, SM_LO, rep4(step < 7u ? step : 7u));
                         if (rnd < 0 || rnd > 255) smask &= X_C * 0x01010101u; /* no vote round equals State.round */
-                        uint32_t* const rk = itab + RECW * lane;
+                        uint32_t* const rk = itab + RW * lane;
                         rk[R_SMASK] = smask;
                         rk[R_EQ8] = (rnd >= 0 && rnd <= 255) ? (uint32_t)rnd : 0x100u;
                         rk[R_EQ] = rep4((uint32_t)rnd);
@@ -495,8 +522,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                     sA = wA >> 8;
                     kB = wB & 0xFFu;
                 }
-                const uint4 recA = *reinterpret_cast<const uint4*>(itab + RECW * kA); /* q2, pbase, nv, State.round (0x100: none) */
-                const uint4 recB = multi ? *reinterpret_cast<const uint4*>(itab + RECW * kB) : recA;
+                const uint4 recA = *reinterpret_cast<const uint4*>(itab + RW * kA); /* q2, pbase, nv, State.round (0x100: none) */
+                const uint4 recB = multi ? *reinterpret_cast<const uint4*>(itab + RW * kB) : recA;
 
                 /* the next chunk by LDS-DMA (this stream's, or the next batch's first) */
                 auto next_dma = [&]() {
@@ -583,7 +610,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                     }
                 }
                 uint32_t w[LV];
-                {
+                uint64_t wq[W64 ? LV : 1u]; /* (W64) the weights from the i64 table */
+                if constexpr (W64) {
+                    const uint32_t pbA = recA.y, pbB = recB.y;
+#pragma unroll
+                    for (uint32_t s = 0; s < LV; ++s) {
+                        const bool o = (((s < 4u ? okb0 : okb1) >> (8u * (s & 3u))) & 1u) != 0u;
+                        const uint32_t idx = o ? (s < 4u ? pbA : pbB) + val[s] : 0u;
+                        const uint64_t x = (uint64_t)a.power[idx];
+                        wq[s] = o ? x : 0ull;
+                    }
+                } else {
                     /* K1: w = power[set][validator] (consensus_executor.rs:62-63 ->
                      * validators.rs:7); a vote that checked out weighs 0 */
                     const uint32_t pbA = recA.y, pbB = recB.y;
@@ -605,7 +642,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                 }
                 /* a gather from HBM retires before the DMA below is issued: a wait on it
                  * behind the DMA would wait for the DMA too (in-order vmcnt) */
-                if (!PC) asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]),
+                if (W64) asm volatile("" ::"v"(wq[0]), "v"(wq[1]), "v"(wq[2]), "v"(wq[3]), "v"(wq[4]), "v"(wq[5]),
+                                      "v"(wq[6]), "v"(wq[7]));
+                else if (!PC) asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]),
                                       "v"(w[6]), "v"(w[7]));
                 next_dma();
                 flush(); /* the previous chunk's codes */
@@ -816,7 +855,110 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
                     }
                     __builtin_amdgcn_wave_barrier();
                 };
-                if (R1) {
+                if constexpr (W64) {
+                    /* one round, u64 sums: the four buckets as separate lane-serial prefixes
+                     * (prevote / precommit x value / nil), the vote's own type's sums after it
+                     * kept per vote, four u64 DPP scans, thresholds q2 - base in int64 */
+                    /* pass 1: the lane's bucket totals (and through vote 3); the per-vote sums are
+                     * recomputed in pass 2 rather than held (VGPRs) */
+                    uint64_t Svp = 0, Snp = 0, Svc = 0, Snc = 0, P3vp = 0, P3np = 0, P3vc = 0, P3nc = 0;
+#pragma unroll
+                    for (uint32_t s = 0; s < LV; ++s) {
+                        const uint32_t bs = 8u * (s & 3u);
+                        const bool pc = (((s < 4u ? t8[0] : t8[1]) >> bs) & 1u) != 0u;
+                        const bool nil = (((s < 4u ? nb0 : nb1) >> bs) & 0x10u) != 0u;
+                        const uint64_t x = wq[s];
+                        Svp += (!pc && !nil) ? x : 0ull;
+                        Snp += (!pc && nil) ? x : 0ull;
+                        Svc += (pc && !nil) ? x : 0ull;
+                        Snc += (pc && nil) ? x : 0ull;
+                        if (s == 3u) { P3vp = Svp; P3np = Snp; P3vc = Svc; P3nc = Snc; }
+                    }
+                    const uint64_t Tvp = split ? Svp - P3vp : Svp, Tnp = split ? Snp - P3np : Snp;
+                    const uint64_t Tvc = split ? Svc - P3vc : Svc, Tnc = split ? Snc - P3nc : Snc;
+                    const uint64_t Ivp = scan(Tvp), Inp = scan(Tnp), Ivc = scan(Tvc), Inc = scan(Tnc);
+                    const uint64_t Evp = Ivp - Tvp, Enp = Inp - Tnp, Evc = Ivc - Tvc, Enc = Inc - Tnc;
+                    const uint64_t* const A64 = reinterpret_cast<const uint64_t*>(A); /* vp vc np nc */
+                    uint64_t cvp = 0, cnp = 0, cvc = 0, cnc = 0;
+                    if (cont0) {
+                        cvp = A64[0];
+                        cvc = A64[1];
+                        cnp = A64[2];
+                        cnc = A64[3];
+                    }
+                    uint64_t bvp = Evp, bnp = Enp, bvc = Evc, bnc = Enc;
+                    if (multi) {
+                        bvp -= shfl(Evp, sA);
+                        bnp -= shfl(Enp, sA);
+                        bvc -= shfl(Evc, sA);
+                        bnc -= shfl(Enc, sA);
+                    }
+                    if (cA) {
+                        bvp += cvp;
+                        bnp += cnp;
+                        bvc += cvc;
+                        bnc += cnc;
+                    }
+                    const uint64_t qA = u64of(recA.x, itab[RW * kA + R_Q2H]);
+                    const int64_t tvpA = (int64_t)(qA - bvp), tnpA = (int64_t)(qA - bnp), tapA = (int64_t)(qA - bvp - bnp);
+                    const int64_t tvcA = (int64_t)(qA - bvc), tncA = (int64_t)(qA - bnc), tacA = (int64_t)(qA - bvc - bnc);
+                    int64_t tvpB = tvpA, tnpB = tnpA, tapB = tapA, tvcB = tvcA, tncB = tncA, tacB = tacA;
+                    if (multi && split) { /* unit B starts its segment: the lane prefix holds unit A's part */
+                        const uint64_t qB = u64of(recB.x, itab[RW * kB + R_Q2H]);
+                        tvpB = (int64_t)(qB + P3vp);
+                        tnpB = (int64_t)(qB + P3np);
+                        tapB = (int64_t)(qB + P3vp + P3np);
+                        tvcB = (int64_t)(qB + P3vc);
+                        tncB = (int64_t)(qB + P3nc);
+                        tacB = (int64_t)(qB + P3vc + P3nc);
+                    }
+                    uint32_t l0 = 0, l1 = 0;
+                    uint64_t Rvp = 0, Rnp = 0, Rvc = 0, Rnc = 0; /* pass 2: the running sums again */
+#pragma unroll
+                    for (uint32_t s = 0; s < LV; ++s) {
+                        const uint32_t bs = 8u * (s & 3u);
+                        const bool pc = (((s < 4u ? t8[0] : t8[1]) >> bs) & 1u) != 0u;
+                        const bool nil = (((s < 4u ? nb0 : nb1) >> bs) & 0x10u) != 0u;
+                        const uint64_t x = wq[s];
+                        Rvp += (!pc && !nil) ? x : 0ull;
+                        Rnp += (!pc && nil) ? x : 0ull;
+                        Rvc += (pc && !nil) ? x : 0ull;
+                        Rnc += (pc && nil) ? x : 0ull;
+                        const int64_t tv = s < 4u ? (pc ? tvcA : tvpA) : (pc ? tvcB : tvpB);
+                        const int64_t tn = s < 4u ? (pc ? tncA : tnpA) : (pc ? tncB : tnpB);
+                        const int64_t ta = s < 4u ? (pc ? tacA : tapA) : (pc ? tacB : tapB);
+                        const int64_t sv = (int64_t)(pc ? Rvc : Rvp), sn = (int64_t)(pc ? Rnc : Rnp);
+                        uint32_t l = sv + sn > ta ? 1u : 0u;
+                        l = sn > tn ? 2u : l;
+                        l = sv > tv ? 3u : l;
+                        if (s < 4u) l0 |= l << bs;
+                        else l1 |= l << bs;
+                    }
+                    if (SM) { /* as the u32 pass: a negative threshold = crossed before the unit */
+                        cf |= (tvpA < 0 || tnpA < 0) ? 1u : 0u;
+                        cf |= tvcA < 0 ? 2u : 0u;
+                        if (!split) {
+                            cf |= ((int64_t)P3vp > tvpA || (int64_t)P3np > tnpA) ? 4u : 0u;
+                            cf |= (int64_t)P3vc > tvcA ? 8u : 0u;
+                        }
+                    }
+                    lv0 |= l0;
+                    lv1 |= l1;
+                    if (lastc) { /* the last segment's executors after the chunk (lane 0 writes) */
+                        const uint64_t nvp = rdl(Ivp, 63u) - rdl(Evp, slast) + (cL ? cvp : 0ull);
+                        const uint64_t nnp = rdl(Inp, 63u) - rdl(Enp, slast) + (cL ? cnp : 0ull);
+                        const uint64_t nvc = rdl(Ivc, 63u) - rdl(Evc, slast) + (cL ? cvc : 0ull);
+                        const uint64_t nnc = rdl(Inc, 63u) - rdl(Enc, slast) + (cL ? cnc : 0ull);
+                        if (lane == 0u) {
+                            uint64_t* const B64 = reinterpret_cast<uint64_t*>(B);
+                            B64[0] = nvp;
+                            B64[1] = nvc;
+                            B64[2] = nnp;
+                            B64[3] = nnc;
+                        }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                } else if (R1) {
                     pass(std::false_type{}, 0u);
                 } else if (runs) {
                     pass(std::true_type{}, 0u);
@@ -846,8 +988,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
 
                 /* ---- K4: State::apply(v.round, event) in stream order ---- */
                 if (SM) {
-                    uint32_t* const rA = itab + RECW * kA;
-                    uint32_t* const rB = itab + RECW * kB;
+                    uint32_t* const rA = itab + RW * kA;
+                    uint32_t* const rB = itab + RW * kB;
                     /* State.round bytes, valid-from-start, P1, C */
                     const uint4 eA = *reinterpret_cast<const uint4*>(rA + R_SMASK); /* smask, eq, vall, step */
                     const uint4 eB = *reinterpret_cast<const uint4*>(rB + R_SMASK);
@@ -1016,14 +1158,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void f
 /* ------------------------------------------------------------------ */
 /* launcher                                                            */
 
-template <bool SM, bool R1, bool EVC>
+template <bool SM, bool R1, bool EVC, bool W64>
 static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStream_t st) {
     const uint32_t n = a->vb.n_instances;
     if (n == 0) return hipSuccess;
     using agnes::flow::flow;
-    const void* fns[2] = {reinterpret_cast<const void*>(&flow<false, SM, R1, EVC>),
-                          reinterpret_cast<const void*>(&flow<true, SM, R1, EVC>)};
-    const uint32_t lpw = agnes::flow::lds_bytes(SM, a->max_rounds, EVC);
+    const void* fns[2] = {reinterpret_cast<const void*>(&flow<false, SM, R1, EVC, W64>),
+                          reinterpret_cast<const void*>(&flow<!W64, SM, R1, EVC, W64>)};
+    const uint32_t lpw = agnes::flow::lds_bytes(SM, a->max_rounds, EVC, W64);
     const uint64_t wave_lds = (uint64_t)lpw * AGNES_WAVES_PER_BLOCK;
     const uint64_t pcb = agnes::align16(4ull * a->n_sets * a->n_vals);
     /* blocks per CU from the occupancy query; the LDS power table only where it
@@ -1045,7 +1187,7 @@ static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStrea
             return k;
         };
         const int k0 = per_cu(fns[0], wave_lds);
-        const int k1 = pcb <= 32u * 1024u ? per_cu(fns[1], wave_lds + pcb) : 0;
+        const int k1 = (!W64 && pcb <= 32u * 1024u) ? per_cu(fns[1], wave_lds + pcb) : 0; /* (W64: no u32 table) */
         o = &occ[occ_next++ % 8];
         *o = Occ{fns[0], wave_lds, pcb, k0 > 0 ? k0 : 1, false};
         if (k1 > 0 && k1 >= k0) {
@@ -1073,8 +1215,8 @@ static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStrea
     const uint64_t cap = ncu * (uint64_t)o->per_cu;
     if (blocks > cap) blocks = cap;
     if (blocks == 0) blocks = 1;
-    if (o->pc) hipLaunchKernelGGL((flow<true, SM, R1, EVC>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
-    else hipLaunchKernelGGL((flow<false, SM, R1, EVC>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
+    if (o->pc) hipLaunchKernelGGL((flow<!W64, SM, R1, EVC, W64>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
+    else hipLaunchKernelGGL((flow<false, SM, R1, EVC, W64>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
     return hipGetLastError();
 }
 
@@ -1083,7 +1225,7 @@ bool agnes_flow_supported(const agnes_tally_args* a) {
      * without the State machine, 12 with it: its VGPRs allow 3 waves per SIMD) */
     const bool sm = (a->flags & AGNES_FLAG_STATE_MACHINE) != 0 && a->states != nullptr;
     return a->max_rounds <= 15u &&
-           agnes::flow::lds_bytes(sm, a->max_rounds, a->ev_counts != nullptr) * (sm ? 12u : 16u) <= 160u * 1024u;
+           agnes::flow::lds_bytes(sm, a->max_rounds, a->ev_counts != nullptr, a->w64 != 0u) * (sm ? 12u : 16u) <= 160u * 1024u;
 }
 
 bool agnes_flow_counts_events(uint32_t flags, uint32_t max_rounds) {
@@ -1093,12 +1235,16 @@ bool agnes_flow_counts_events(uint32_t flags, uint32_t max_rounds) {
 
 hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t st) {
     const bool sm = (a->flags & AGNES_FLAG_STATE_MACHINE) != 0 && a->states != nullptr;
+    if (a->w64) { /* the u64 domain: one round, no record counts (agnes_sweep_supported) */
+        if (a->max_rounds != 1u || a->ev_counts) return hipErrorInvalidValue;
+        return sm ? launch_flow_k<true, true, false, true>(a, num_cus, st) : launch_flow_k<false, true, false, true>(a, num_cus, st);
+    }
     if (a->ev_counts) {
         if (a->max_rounds == 1u)
-            return sm ? launch_flow_k<true, true, true>(a, num_cus, st) : launch_flow_k<false, true, true>(a, num_cus, st);
-        return sm ? launch_flow_k<true, false, true>(a, num_cus, st) : launch_flow_k<false, false, true>(a, num_cus, st);
+            return sm ? launch_flow_k<true, true, true, false>(a, num_cus, st) : launch_flow_k<false, true, true, false>(a, num_cus, st);
+        return sm ? launch_flow_k<true, false, true, false>(a, num_cus, st) : launch_flow_k<false, false, true, false>(a, num_cus, st);
     }
     if (a->max_rounds == 1u)
-        return sm ? launch_flow_k<true, true, false>(a, num_cus, st) : launch_flow_k<false, true, false>(a, num_cus, st);
-    return sm ? launch_flow_k<true, false, false>(a, num_cus, st) : launch_flow_k<false, false, false>(a, num_cus, st);
+        return sm ? launch_flow_k<true, true, false, false>(a, num_cus, st) : launch_flow_k<false, true, false, false>(a, num_cus, st);
+    return sm ? launch_flow_k<true, false, false, false>(a, num_cus, st) : launch_flow_k<false, false, false, false>(a, num_cus, st);
 }
