@@ -159,3 +159,30 @@ def test_edges_arbitrary_code_bytes(eng, R):
         torch.cuda.synchronize()
         _check(cfg, hb, codes, offs.cpu().numpy().view(np.uint64),
                recs.cpu().numpy().reshape(-1).view(abi.EDGE_DTYPE))
+
+
+@pytest.mark.parametrize("R", [1, 4])
+def test_edges_offsets_going_back(eng, R):
+    """Offsets that go back inside a batch (an instance whose end lies before its start,
+    ranges that overlap): the stream kernel walks such a batch instance by instance and
+    equals the checker; runs in order, runs revisited (shuffled rounds) and unaligned
+    (1-B shifted) columns alike."""
+    rng = np.random.default_rng(100 + R)
+    lengths = rng.integers(0, 300, 3000)
+    off = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)
+    n = int(off[-1])
+    inst = np.repeat(np.arange(len(lengths)), lengths)
+    rnd = np.sort(rng.integers(0, R + 1, n)) if R == 1 else rng.integers(0, R + 1, n)
+    # every 37th instance's start moved past its end, every 41st's start back into the one before
+    bad = off.copy()
+    bad[37:-1:37] = np.minimum(bad[37:-1:37] + 400, n)
+    bad[41:-1:41] = np.maximum(bad[41:-1:41] - 100, 0)
+    hb = ol.batch_from_lists(inst, rnd, rng.integers(0, 3, n), np.zeros(n), np.zeros(n), bad.astype(np.uint64))
+    codes = rng.integers(0, 256, n).astype(np.uint8)
+    codes[rng.random(n) < 0.7] &= 0x0F
+    cfg = abi.config(abi.MODE_REFERENCE, 0, R)
+    db = DeviceBatch.from_host(hb, eng.device)
+    dc = torch.from_numpy(codes).to(eng.device)
+    offs, recs = eng.edges(cfg, db, dc)
+    torch.cuda.synchronize()
+    _check(cfg, hb, codes, offs.cpu().numpy().view(np.uint64), recs.cpu().numpy().reshape(-1).view(abi.EDGE_DTYPE))
