@@ -39,6 +39,9 @@ KERNELS = {
 }
 
 
+MULTI = {"dedup_first", "dedup_first_mask"}  # engine steps made of several kernels
+
+
 def per_launch(path, counter):
     """{engine kernel: (median KB per launch, launches)}"""
     vals = {}
@@ -49,9 +52,16 @@ def per_launch(path, counter):
             if re.search(pat, r["Kernel_Name"]):
                 vals.setdefault(k, {}).setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
     # an engine step of several kernels (dedup_first: count, prefix, scatter, min): the
-    # sum of each kernel's median per launch
-    return {k: (sum(statistics.median(v) for v in by.values()), max(len(v) for v in by.values()))
-            for k, by in vals.items()}
+    # sum of each kernel's median per launch; any other entry: the median over its
+    # launches (instantiations of one kernel, e.g. flow with and without record counts)
+    out = {}
+    for k, by in vals.items():
+        if k in MULTI:
+            out[k] = (sum(statistics.median(v) for v in by.values()), max(len(v) for v in by.values()))
+        else:
+            allv = [x for v in by.values() for x in v]
+            out[k] = (statistics.median(allv), len(allv))
+    return out
 
 
 def main():
