@@ -899,47 +899,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? 2 : 3
                         bvc += cvc;
                         bnc += cnc;
                     }
+                    /* pass 2: each vote's own running sums as absolute u64 values (the base
+                     * before the lane plus the lane prefix; unit B of a split lane starts its
+                     * instance from zero) against q2 — no per-vote thresholds held */
                     const uint64_t qA = u64of(recA.x, itab[RW * kA + R_Q2H]);
-                    const int64_t tvpA = (int64_t)(qA - bvp), tnpA = (int64_t)(qA - bnp), tapA = (int64_t)(qA - bvp - bnp);
-                    const int64_t tvcA = (int64_t)(qA - bvc), tncA = (int64_t)(qA - bnc), tacA = (int64_t)(qA - bvc - bnc);
-                    int64_t tvpB = tvpA, tnpB = tnpA, tapB = tapA, tvcB = tvcA, tncB = tncA, tacB = tacA;
-                    if (multi && split) { /* unit B starts its segment: the lane prefix holds unit A's part */
-                        const uint64_t qB = u64of(recB.x, itab[RW * kB + R_Q2H]);
-                        tvpB = (int64_t)(qB + P3vp);
-                        tnpB = (int64_t)(qB + P3np);
-                        tapB = (int64_t)(qB + P3vp + P3np);
-                        tvcB = (int64_t)(qB + P3vc);
-                        tncB = (int64_t)(qB + P3nc);
-                        tacB = (int64_t)(qB + P3vc + P3nc);
-                    }
+                    const uint64_t qB = (multi && split) ? u64of(recB.x, itab[RW * kB + R_Q2H]) : qA;
                     uint32_t l0 = 0, l1 = 0;
-                    uint64_t Rvp = 0, Rnp = 0, Rvc = 0, Rnc = 0; /* pass 2: the running sums again */
+                    uint64_t Avp = bvp, Anp = bnp, Avc = bvc, Anc = bnc, q = qA;
 #pragma unroll
                     for (uint32_t s = 0; s < LV; ++s) {
+                        if (s == 4u && multi && split) {
+                            Avp = Anp = Avc = Anc = 0ull;
+                            q = qB;
+                        }
                         const uint32_t bs = 8u * (s & 3u);
                         const bool pc = (((s < 4u ? t8[0] : t8[1]) >> bs) & 1u) != 0u;
                         const bool nil = (((s < 4u ? nb0 : nb1) >> bs) & 0x10u) != 0u;
                         const uint64_t x = wq[s];
-                        Rvp += (!pc && !nil) ? x : 0ull;
-                        Rnp += (!pc && nil) ? x : 0ull;
-                        Rvc += (pc && !nil) ? x : 0ull;
-                        Rnc += (pc && nil) ? x : 0ull;
-                        const int64_t tv = s < 4u ? (pc ? tvcA : tvpA) : (pc ? tvcB : tvpB);
-                        const int64_t tn = s < 4u ? (pc ? tncA : tnpA) : (pc ? tncB : tnpB);
-                        const int64_t ta = s < 4u ? (pc ? tacA : tapA) : (pc ? tacB : tapB);
-                        const int64_t sv = (int64_t)(pc ? Rvc : Rvp), sn = (int64_t)(pc ? Rnc : Rnp);
-                        uint32_t l = sv + sn > ta ? 1u : 0u;
-                        l = sn > tn ? 2u : l;
-                        l = sv > tv ? 3u : l;
+                        Avp += (!pc && !nil) ? x : 0ull;
+                        Anp += (!pc && nil) ? x : 0ull;
+                        Avc += (pc && !nil) ? x : 0ull;
+                        Anc += (pc && nil) ? x : 0ull;
+                        const uint64_t sv = pc ? Avc : Avp, sn = pc ? Anc : Anp;
+                        uint32_t l = sv + sn > q ? 1u : 0u;
+                        l = sn > q ? 2u : l;
+                        l = sv > q ? 3u : l;
                         if (s < 4u) l0 |= l << bs;
                         else l1 |= l << bs;
                     }
-                    if (SM) { /* as the u32 pass: a negative threshold = crossed before the unit */
-                        cf |= (tvpA < 0 || tnpA < 0) ? 1u : 0u;
-                        cf |= tvcA < 0 ? 2u : 0u;
+                    if (SM) { /* crossed before the unit: the sums before it already past q2 */
+                        cf |= (bvp > qA || bnp > qA) ? 1u : 0u;
+                        cf |= bvc > qA ? 2u : 0u;
                         if (!split) {
-                            cf |= ((int64_t)P3vp > tvpA || (int64_t)P3np > tnpA) ? 4u : 0u;
-                            cf |= (int64_t)P3vc > tvcA ? 8u : 0u;
+                            cf |= (bvp + P3vp > qA || bnp + P3np > qA) ? 4u : 0u;
+                            cf |= bvc + P3vc > qA ? 8u : 0u;
                         }
                     }
                     lv0 |= l0;
