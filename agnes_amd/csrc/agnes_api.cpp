@@ -122,7 +122,7 @@ bool cfg_ok(const agnes_config* cfg) {
     return cfg && cfg->max_rounds >= 1 && cfg->max_rounds <= 256 && cfg->mode <= AGNES_MODE_DEDUP &&
            (cfg->flags & ~(AGNES_FLAG_ROUND_SKIP | AGNES_FLAG_STATE_MACHINE | AGNES_FLAG_DISTINCT_VALUES |
                            AGNES_FLAG_ONE_INSTANCE | AGNES_FLAG_WEIGHTS_CACHED |
-                           (AGNES_ROUTE_MASK << AGNES_ROUTE_SHIFT) |
+                           (AGNES_ROUTE_MASK << AGNES_ROUTE_SHIFT) | AGNES_FLAG_ROUTE_STREAM |
                            AGNES_FLAG_EPOCH_BITS(0x1F))) == 0;
 }
 

@@ -1297,13 +1297,15 @@ bool agnes_dflow_supported(const agnes_tally_args* a) {
            (al4 & 3u) == 0u && (reinterpret_cast<uintptr_t>(a->codes) & 7u) == 0u && a->vb.validator != nullptr;
 }
 
-/* the AUTO route takes the stream kernel (off until its GPU parity run is green) */
+/* the stream kernel on the AUTO route when asked for (AGNES_FLAG_ROUTE_STREAM); a build
+ * with AGNES_DFLOW_AUTO=1 takes it for every supported batch (A/B experiments) */
 #ifndef AGNES_DFLOW_AUTO
 #define AGNES_DFLOW_AUTO 0
 #endif
 bool agnes_dflow_route(const agnes_tally_args* a) {
     const uint32_t route = (a->flags >> AGNES_ROUTE_SHIFT) & AGNES_ROUTE_MASK;
-    return AGNES_DFLOW_AUTO && route == AGNES_ROUTE_AUTO && agnes_dflow_supported(a);
+    return (AGNES_DFLOW_AUTO || (a->flags & AGNES_FLAG_ROUTE_STREAM) != 0u) && route == AGNES_ROUTE_AUTO &&
+           agnes_dflow_supported(a);
 }
 
 template <bool DEDUP, bool SKIP>
