@@ -725,7 +725,8 @@ static int dedup_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
                                                            set < c->n_sets, base, first, fused ? type_out : nullptr,
                                                            c->d_dd, (hipStream_t)stream));
     }
-    if (fused) { /* outside the bucketed domain: the two passes */
+    if (fused) { /* outside the bucketed domain: the two passes over a filled table */
+        AGNES_TRY(agnes_launch_dedup_fill(first, 2ull * cfg->max_rounds * c->n_vals, (hipStream_t)stream));
         const int rc = status_of(agnes_launch_dedup(b, cfg->reserved, cfg->max_rounds, c->n_vals, set < c->n_sets,
                                                     base, first, nullptr, (hipStream_t)stream));
         if (rc != AGNES_OK) return rc;

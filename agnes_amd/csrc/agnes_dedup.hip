@@ -123,6 +123,11 @@ __global__ __launch_bounds__(256) void mask_kernel(DedupArgs a, const unsigned l
     }
 }
 
+__global__ __launch_bounds__(256) void fill_kernel(uint64_t* first, uint64_t n) { /* INT64_MAX: no vote yet */
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) first[k] = 0x7FFFFFFFFFFFFFFFull;
+}
+
 __global__ __launch_bounds__(256) void reject_kernel(const uint8_t* type_masked, uint64_t n, uint8_t* codes) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride)
@@ -281,10 +286,11 @@ __global__ __launch_bounds__(MT) void bucket_min(uint64_t n_keys, const uint32_t
     const uint64_t k0 = (uint64_t)b * KB;
     for (uint32_t k = threadIdx.x; k < KB && k0 + k < n_keys; k += MT) {
         const uint32_t x = tab[k];
-        if (x != 0xFFFFFFFFu) {
+        if (MASK) { /* agnes_dedup_first_mask: the table written whole (no caller fill, no read) */
+            first[k0 + k] = x != 0xFFFFFFFFu ? base + x : 0x7FFFFFFFFFFFFFFFull;
+        } else if (x != 0xFFFFFFFFu) { /* agnes_dedup_first: lowered */
             const unsigned long long v = base + x, old = first[k0 + k];
             if (v < old) first[k0 + k] = v;
-            if (MASK && v > old) tab[k] = 0xFFFFFFFFu; /* a lower entry the caller left: no first here */
         }
     }
     if (MASK) { /* the firsts' types over the scatter's AGNES_TYPE_MASKED */
@@ -380,6 +386,12 @@ hipError_t agnes_launch_dedup_first_bucketed(const agnes_vote_batch* vb, uint32_
         else hipLaunchKernelGGL((bucket_scatter<false, false>), dim3(G), dim3(256), 0, st, a, nb, G, cnt, rowtot, bstart, pairs, type_out);
         hipLaunchKernelGGL(bucket_min<false>, dim3(nb), dim3(MT), 0, st, n_keys, bstart, pairs, base, f, type_out);
     }
+    return hipGetLastError();
+}
+
+hipError_t agnes_launch_dedup_fill(uint64_t* first, uint64_t n, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(agnes::dedup::fill_kernel, dedup_grid(n), dim3(256), 0, st, first, n);
     return hipGetLastError();
 }
 

@@ -185,6 +185,8 @@ uint64_t agnes_dedup_scratch_bytes(uint64_t n_votes, uint32_t max_rounds, uint32
 hipError_t agnes_launch_dedup_first_bucketed(const agnes_vote_batch* vb, uint32_t inst_id, uint32_t max_rounds,
                                              uint32_t n_vals, bool set_ok, uint64_t base, uint64_t* first,
                                              uint8_t* type_out, void* scratch, hipStream_t stream);
+/* first[0 .. n) := INT64_MAX */
+hipError_t agnes_launch_dedup_fill(uint64_t* first, uint64_t n, hipStream_t stream);
 hipError_t agnes_launch_dedup_reject(const uint8_t* type_masked, uint64_t n, uint8_t* codes, hipStream_t stream);
 
 #define AGNES_WAVES_PER_BLOCK 4

@@ -355,11 +355,12 @@ def tally_one_instance_dedup(tally_carried, dedup_first, dedup_mask, dedup_rejec
     The instance's id is cfg.reserved, for the DEDUP checks and for the carried
     tally alike (one source).  With one rank, dedup_first_mask(base, first) (the
     fused agnes_dedup_first_mask), when given, replaces the first / mask pair."""
-    first = torch.full((2 * cfg.max_rounds * n_vals,), INT64_MAX, dtype=torch.int64, device=device)
     multi = dist.is_initialized() and dist.get_world_size(group) > 1
     if dedup_first_mask is not None and not multi:
+        first = torch.empty((2 * cfg.max_rounds * n_vals,), dtype=torch.int64, device=device)  # written whole
         dedup_first_mask(base, first)
     else:
+        first = torch.full((2 * cfg.max_rounds * n_vals,), INT64_MAX, dtype=torch.int64, device=device)
         dedup_first(base, first)
         if multi:
             t = first.to(_device_for(group))

@@ -406,7 +406,9 @@ int agnes_dedup_mask(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_b
                      const uint64_t* first, uint8_t* type_out, void* stream);
 /* agnes_dedup_first + agnes_dedup_mask in one call (round 4), for a batch that holds
  * every vote of the instance (one rank: no other slice's table is min-combined into
- * `first` between the two): the same `first` and `type_out` as the two calls. */
+ * `first` between the two): `type_out` as the two calls give it; `first` is an output
+ * here, written whole (INT64_MAX for a key without a valid vote), so it needs no
+ * caller initialisation — the two calls' table on an INT64_MAX-filled `first`. */
 int agnes_dedup_first_mask(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch, uint64_t base,
                            uint64_t* first, uint8_t* type_out, void* stream);
 int agnes_dedup_reject(agnes_ctx* ctx, const uint8_t* type_masked, uint64_t n_votes, uint8_t* codes,

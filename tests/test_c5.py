@@ -459,8 +459,8 @@ def test_gpu_dedup_slices_with_bases(eng):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("fused", [False, True])
-@pytest.mark.parametrize("shift", [0, 1, 3])
-def test_gpu_dedup_first_table_prefilled(eng, shift, fused):
+@pytest.mark.parametrize("shift,max_rounds", [(0, 1), (1, 1), (3, 1), (0, 64)])
+def test_gpu_dedup_first_table_prefilled(eng, shift, max_rounds, fused):
     """agnes_dedup_first (the counting sort over key buckets and LDS minima) and
     agnes_dedup_mask: the table equals the checker's min over valid votes, with
     entries the caller set lower kept (the API lowers, it does not overwrite), many
@@ -469,6 +469,9 @@ def test_gpu_dedup_first_table_prefilled(eng, shift, fused):
     16-B aligned: the one-vote-per-thread kernels), and the mask equals the checker's."""
     from agnes_amd.engine import DeviceBatch
     hb, power, cfg = _dedup_instance(seed=41, n_vals=100_000, R=1)
+    # max_rounds 64: 12.8M keys, more buckets than the sort handles -> the atomic kernel
+    # (and, fused, a filled table and the mask pass)
+    cfg = abi.config(abi.MODE_DEDUP, 0, max_rounds)
     hb.type[::997] = 3
     hb.round[::1009] = 9
     hb.validator[::1013] = 10 ** 7
@@ -485,7 +488,9 @@ def test_gpu_dedup_first_table_prefilled(eng, shift, fused):
                                  value=db.value[shift:], validator=db.validator[shift:],
                                  offsets=torch.tensor([0, n], dtype=torch.int64, device=eng.device), n_votes=n)
     tm = torch.empty(n + 4, dtype=torch.uint8, device=eng.device)[shift:shift + n]
-    if fused:  # agnes_dedup_first_mask: the same table and mask from one counting sort
+    if fused:  # agnes_dedup_first_mask: the table written whole (the prefill is not kept) and the mask
+        f0 = np.full(K, ad.INT64_MAX, np.int64)
+        fw.fill_(-7)
         eng.dedup_first_mask(cfg, db, base, fw, tm)
     else:
         eng.dedup_first(cfg, db, base, fw)
@@ -499,4 +504,5 @@ def test_gpu_dedup_first_table_prefilled(eng, shift, fused):
     got = fw.cpu().numpy()
     assert np.array_equal(got, want)
     assert (got[1::7] < ad.INT64_MAX).any() and (got[1::7] >= base).all()
+    assert (got == ad.INT64_MAX).any()  # keys without a valid vote
     assert np.array_equal(tm.cpu().numpy(), dd.mask(cfg, sl, base, want))
