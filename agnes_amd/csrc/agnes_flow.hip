@@ -198,9 +198,15 @@ struct Hdr {
  * a.ev_counts[instance] -- the count pass of the event stream (agnes_events.hip) */
 /* W64 (one round, round 4): the u64 domain (agnes_fast.h defer_si) — weights from the
  * i64 power table and the four buckets of K2 as u64 sums instead of 16-bit fields */
+#ifndef AGNES_FLOW_W64_WPE
+#define AGNES_FLOW_W64_WPE 2
+#endif
+#ifndef AGNES_FLOW_WPE
+#define AGNES_FLOW_WPE 3
+#endif
 template <bool PC, bool SM, bool R1, bool EVC, bool W64>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? 2 : 3))) void flow(agnes_tally_args a, uint32_t lds_per_wave) {
-    static_assert(!W64 || (R1 && !PC && !EVC), "W64: one round, no u32 power table, no record counts");
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES_FLOW_W64_WPE : AGNES_FLOW_WPE))) void flow(agnes_tally_args a, uint32_t lds_per_wave) {
+    static_assert(!W64 || (R1 && !EVC), "W64: one round, no record counts");
     constexpr uint32_t RW = W64 ? RECW64 : RECW; /* record words */
 
     const uint32_t lane = lane_id();
@@ -209,11 +215,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? 2 : 3
     const uint64_t NV = a.vb.n_votes;
     const uint32_t o32 = 32u * lane, o16 = 16u * lane, o8 = 8u * lane, o4 = 4u * lane;
 
-    /* block-shared u32 power table (launcher-staged only when it costs no occupancy) */
+    /* block-shared power table, u32 (W64: the i64 one) — launcher-staged only when it
+     * costs no occupancy */
     if (PC) {
-        uint32_t* pc = reinterpret_cast<uint32_t*>(agnes_smem);
         const uint32_t np = ns * nv;
-        for (uint32_t k = threadIdx.x; k < np; k += blockDim.x) pc[k] = a.power32[k];
+        if (W64) {
+            uint64_t* pc = reinterpret_cast<uint64_t*>(agnes_smem);
+            for (uint32_t k = threadIdx.x; k < np; k += blockDim.x) pc[k] = (uint64_t)a.power[k];
+        } else {
+            uint32_t* pc = reinterpret_cast<uint32_t*>(agnes_smem);
+            for (uint32_t k = threadIdx.x; k < np; k += blockDim.x) pc[k] = a.power32[k];
+        }
         __syncthreads();
     }
     unsigned char* const base = agnes_smem + a.power_cache + wave * lds_per_wave;
@@ -617,7 +629,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? 2 : 3
                     for (uint32_t s = 0; s < LV; ++s) {
                         const bool o = (((s < 4u ? okb0 : okb1) >> (8u * (s & 3u))) & 1u) != 0u;
                         const uint32_t idx = o ? (s < 4u ? pbA : pbB) + val[s] : 0u;
-                        const uint64_t x = (uint64_t)a.power[idx];
+                        const uint64_t x = PC ? reinterpret_cast<const uint64_t*>(agnes_smem)[idx] : (uint64_t)a.power[idx];
                         wq[s] = o ? x : 0ull;
                     }
                 } else {
@@ -642,7 +654,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? 2 : 3
                 }
                 /* a gather from HBM retires before the DMA below is issued: a wait on it
                  * behind the DMA would wait for the DMA too (in-order vmcnt) */
-                if (W64) asm volatile("" ::"v"(wq[0]), "v"(wq[1]), "v"(wq[2]), "v"(wq[3]), "v"(wq[4]), "v"(wq[5]),
+                if (W64 && !PC) asm volatile("" ::"v"(wq[0]), "v"(wq[1]), "v"(wq[2]), "v"(wq[3]), "v"(wq[4]), "v"(wq[5]),
                                       "v"(wq[6]), "v"(wq[7]));
                 else if (!PC) asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]),
                                       "v"(w[6]), "v"(w[7]));
@@ -1157,10 +1169,10 @@ static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStrea
     if (n == 0) return hipSuccess;
     using agnes::flow::flow;
     const void* fns[2] = {reinterpret_cast<const void*>(&flow<false, SM, R1, EVC, W64>),
-                          reinterpret_cast<const void*>(&flow<!W64, SM, R1, EVC, W64>)};
+                          reinterpret_cast<const void*>(&flow<true, SM, R1, EVC, W64>)};
     const uint32_t lpw = agnes::flow::lds_bytes(SM, a->max_rounds, EVC, W64);
     const uint64_t wave_lds = (uint64_t)lpw * AGNES_WAVES_PER_BLOCK;
-    const uint64_t pcb = agnes::align16(4ull * a->n_sets * a->n_vals);
+    const uint64_t pcb = agnes::align16((W64 ? 8ull : 4ull) * a->n_sets * a->n_vals);
     /* blocks per CU from the occupancy query; the LDS power table only where it
      * costs no occupancy.  Cached per (kernel, LDS shape). */
     struct Occ { const void* fn; uint64_t wave_lds, pcb; int per_cu; bool pc; };
@@ -1180,7 +1192,7 @@ static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStrea
             return k;
         };
         const int k0 = per_cu(fns[0], wave_lds);
-        const int k1 = (!W64 && pcb <= 32u * 1024u) ? per_cu(fns[1], wave_lds + pcb) : 0; /* (W64: no u32 table) */
+        const int k1 = pcb <= 32u * 1024u ? per_cu(fns[1], wave_lds + pcb) : 0;
         o = &occ[occ_next++ % 8];
         *o = Occ{fns[0], wave_lds, pcb, k0 > 0 ? k0 : 1, false};
         if (k1 > 0 && k1 >= k0) {
@@ -1208,7 +1220,7 @@ static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStrea
     const uint64_t cap = ncu * (uint64_t)o->per_cu;
     if (blocks > cap) blocks = cap;
     if (blocks == 0) blocks = 1;
-    if (o->pc) hipLaunchKernelGGL((flow<!W64, SM, R1, EVC, W64>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
+    if (o->pc) hipLaunchKernelGGL((flow<true, SM, R1, EVC, W64>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
     else hipLaunchKernelGGL((flow<false, SM, R1, EVC, W64>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
     return hipGetLastError();
 }

@@ -217,6 +217,12 @@ CONFIGS = {
                             dup_permille=100, equiv_permille=100, higher_permille=50),
                        (abi.POWER_ZIPF, 1 << 30, 1 << 40, 16),
                        (abi.MODE_DEDUP, abi.FLAG_ROUND_SKIP | abi.FLAG_STATE_MACHINE, 5)),
+    # flow<W64> stages the i64 table in LDS when it fits (c2w_small, c2w_plain); 64 sets x
+    # 100 validators x 8 B do not fit, so c2w_sets gathers from HBM
+    "c2w_sets": (dict(n_instances=3000, n_vals=100, rounds_min=1, rounds_max=1, nil_permille=200),
+                 (abi.POWER_UNIFORM, 1 << 28, 1 << 34, 64), (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 1)),
+    "c2w_plain": (dict(n_instances=2500, n_vals=90, rounds_min=1, rounds_max=1, nil_permille=350),
+                  (abi.POWER_ZIPF, 1 << 31, 1 << 36, 3), (abi.MODE_REFERENCE, 0, 1)),
     "w64_deferred": (dict(n_instances=600, n_vals=300, rounds_min=1, rounds_max=2, nil_permille=250),
                      (abi.POWER_UNIFORM, 1 << 50, 1 << 52, 2), (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 2)),
     "many_rounds": (dict(n_instances=200, n_vals=20, rounds_min=30, rounds_max=60,
