@@ -36,6 +36,8 @@ MODE_REFERENCE, MODE_DEDUP = 0, 1
 FLAG_ROUND_SKIP, FLAG_STATE_MACHINE, FLAG_DISTINCT_VALUES = 0x1, 0x2, 0x4
 FLAG_ONE_INSTANCE = 0x8  # agnes_tally_carried: segments are slices of one instance (id cfg.reserved)
 FLAG_WEIGHTS_CACHED = 0x10  # agnes_tally_carried: batch.weight = agnes_tally_partials' weights (validated as without)
+TYPE_MASKED = 0xFE  # agnes_dedup_mask's type byte of a later duplicate (AGNES_TYPE_MASKED)
+FLAG_MASKED_REJECTED = 0x20  # agnes_tally_carried: AGNES_TYPE_MASKED votes -> REJECTED in the pass (agnes_dedup_reject inside)
 # route override (agnes.h AGNES_ROUTE_*): diagnostics / route-equivalence tests
 ROUTE_SHIFT, ROUTE_AUTO, ROUTE_INSTANCE, ROUTE_SPLIT, ROUTE_WIDE = 8, 0, 1, 2, 3
 EPOCH_BITS_SHIFT = 16

@@ -121,7 +121,7 @@ agnes_set_info set_info(const int64_t* pw, uint32_t n_vals, int64_t total) {
 bool cfg_ok(const agnes_config* cfg) {
     return cfg && cfg->max_rounds >= 1 && cfg->max_rounds <= 256 && cfg->mode <= AGNES_MODE_DEDUP &&
            (cfg->flags & ~(AGNES_FLAG_ROUND_SKIP | AGNES_FLAG_STATE_MACHINE | AGNES_FLAG_DISTINCT_VALUES |
-                           AGNES_FLAG_ONE_INSTANCE | AGNES_FLAG_WEIGHTS_CACHED |
+                           AGNES_FLAG_ONE_INSTANCE | AGNES_FLAG_WEIGHTS_CACHED | AGNES_FLAG_MASKED_REJECTED |
                            (AGNES_ROUTE_MASK << AGNES_ROUTE_SHIFT) | AGNES_FLAG_ROUTE_STREAM |
                            AGNES_FLAG_EPOCH_BITS(0x1F))) == 0;
 }
@@ -391,7 +391,7 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
 
 int agnes_tally(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint8_t* codes,
                 agnes_state* states, void* stream) {
-    if (!c || !cfg || (cfg->flags & (AGNES_FLAG_ONE_INSTANCE | AGNES_FLAG_WEIGHTS_CACHED)))
+    if (!c || !cfg || (cfg->flags & (AGNES_FLAG_ONE_INSTANCE | AGNES_FLAG_WEIGHTS_CACHED | AGNES_FLAG_MASKED_REJECTED)))
         return AGNES_E_INVALID; /* agnes_tally_carried only */
     return tally_impl(c, cfg, b, codes, nullptr, states, nullptr, c->d_sets, c->n_sets, c->sets_dom,
                       (hipStream_t)stream);
@@ -399,7 +399,8 @@ int agnes_tally(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b
 
 int agnes_tally_states(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint8_t* codes,
                        const agnes_state* states_in, agnes_state* states_out, void* stream) {
-    if (!c || !cfg || (cfg->flags & (AGNES_FLAG_ONE_INSTANCE | AGNES_FLAG_WEIGHTS_CACHED))) return AGNES_E_INVALID;
+    if (!c || !cfg || (cfg->flags & (AGNES_FLAG_ONE_INSTANCE | AGNES_FLAG_WEIGHTS_CACHED | AGNES_FLAG_MASKED_REJECTED)))
+        return AGNES_E_INVALID;
     return tally_impl(c, cfg, b, codes, states_in, states_out, nullptr, c->d_sets, c->n_sets, c->sets_dom,
                       (hipStream_t)stream);
 }
@@ -656,7 +657,7 @@ uint64_t agnes_events_capacity(const agnes_config* cfg, const agnes_vote_batch* 
 int agnes_tally_events(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint8_t* codes,
                        const agnes_state* states_in, agnes_state* states_out, uint64_t* offsets,
                        agnes_vote_event* out, void* stream) {
-    if (!c || !cfg || !b || (cfg->flags & (AGNES_FLAG_ONE_INSTANCE | AGNES_FLAG_WEIGHTS_CACHED))) return AGNES_E_INVALID;
+    if (!c || !cfg || !b || (cfg->flags & (AGNES_FLAG_ONE_INSTANCE | AGNES_FLAG_WEIGHTS_CACHED | AGNES_FLAG_MASKED_REJECTED))) return AGNES_E_INVALID;
     if (!offsets || !out || ((uintptr_t)out & 7u)) return AGNES_E_INVALID;
     if (b->n_votes && (!b->value || ((uintptr_t)b->value & 3u))) return AGNES_E_INVALID;
     if (cfg_ok(cfg) && cfg->max_rounds > 64u) return AGNES_E_UNSUPPORTED; /* the emit's value slots in LDS */

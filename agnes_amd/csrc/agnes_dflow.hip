@@ -242,7 +242,7 @@ __global__ __launch_bounds__(256) void dflow(agnes_tally_args a, uint32_t lds_pe
     const uint32_t wave = rfl(threadIdx.x >> 6);
     const uint32_t R = a.max_rounds, nv = a.n_vals, ns = a.n_sets, n = a.vb.n_instances;
     const uint64_t NV = a.vb.n_votes;
-    const uint32_t o32 = 32u * lane, o16 = 16u * lane, o8 = 8u * lane, o4 = 4u * lane;
+    const uint32_t o16 = 16u * lane, o8 = 8u * lane, o4 = 4u * lane;
     const Lay L = layout(R, nv, EVC, SM);
     constexpr uint32_t RW = SM ? RECW : R_STEP + 2u; /* record words */
 

@@ -705,10 +705,13 @@ __device__ __forceinline__ uint32_t process_chunk(const agnes_tally_args& a, con
         }
     }
 
-    /* votes that are not tallied */
+    /* votes that are not tallied (AGNES_FLAG_MASKED_REJECTED, carried calls: a vote the
+     * DEDUP mask took out is REJECTED, what agnes_dedup_reject would write after us) */
+    const bool mrej = WIDE && (a.flags & AGNES_FLAG_MASKED_REJECTED) != 0u;
 #pragma unroll
     for (uint32_t s = 0; s < VPL; ++s) {
-        if (!((f_ok >> s) & 1u)) codes |= AGNES_CODE_INVALID << (8u * s);
+        if (!((f_ok >> s) & 1u))
+            codes |= (mrej && P.tt[s] == AGNES_TYPE_MASKED ? AGNES_CODE_REJECTED : AGNES_CODE_INVALID) << (8u * s);
         else if (!((f_acc >> s) & 1u)) codes |= AGNES_CODE_REJECTED << (8u * s);
     }
 

@@ -348,7 +348,8 @@ def tally_one_instance_dedup(tally_carried, dedup_first, dedup_mask, dedup_rejec
                                 masked (agnes_dedup_mask); tally_carried must read
                                 THAT column: a masked vote counts as nothing;
       tally_one_instance        the REFERENCE split tally of the masked stream;
-      dedup_reject()            the masked votes' codes -> REJECTED.
+      dedup_reject()            the masked votes' codes -> REJECTED (None: the carried
+                                tally writes REJECTED itself, FLAG_MASKED_REJECTED).
     The codes equal tallying the whole instance as one DEDUP stream (offsets: as
     tally_one_instance's, for a HIP-graph capture).  A stream
     continued across calls would also carry `first`; not offered here.
@@ -367,10 +368,12 @@ def tally_one_instance_dedup(tally_carried, dedup_first, dedup_mask, dedup_rejec
             dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)         # the DEDUP exchange step
             first = t.to(device)
         dedup_mask(base, first)
-    ref = abi.Config(abi.MODE_REFERENCE, cfg.flags, cfg.max_rounds, cfg.reserved)
+    flags = cfg.flags | (abi.FLAG_MASKED_REJECTED if dedup_reject is None else 0)
+    ref = abi.Config(abi.MODE_REFERENCE, flags, cfg.max_rounds, cfg.reserved)
     out = tally_one_instance(tally_carried, n_votes, ref, n_segments, device, cfg.reserved, group,
                              offsets=offsets, fold=fold, partials=partials)
-    dedup_reject()
+    if dedup_reject is not None:
+        dedup_reject()
     return out
 
 

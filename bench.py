@@ -565,7 +565,7 @@ def bench_one_instance(args, w, eng, rank, world):
             return adist.tally_one_instance_dedup(
                 tc, lambda base, f: eng.dedup_first(cfg, src, base, f),
                 lambda base, f: eng.dedup_mask(cfg, src, base, f, tmask),
-                lambda: eng.dedup_reject(tmask, codes, hi - lo), hi - lo, p.n_vals, cfg, segs,
+                None, hi - lo, p.n_vals, cfg, segs,  # pass B writes REJECTED (FLAG_MASKED_REJECTED)
                 eng.device, base=lo, offsets=off, fold=eng.fold_counts, partials=pa,
                 dedup_first_mask=lambda base, f: eng.dedup_first_mask(cfg, src, base, f, tmask))
         return adist.tally_one_instance(tc, hi - lo, cfg, segs, eng.device, 0, None, offsets=off,

@@ -194,6 +194,10 @@ typedef struct agnes_state {
                                            agnes_tally_partials wrote for this batch; the votes are
                                            validated (set, validator index) as without it and the
                                            power table is not gathered again (C5 pass B) */
+#define AGNES_FLAG_MASKED_REJECTED 0x20u /* agnes_tally_carried only: a vote whose type byte is
+                                           AGNES_TYPE_MASKED gets AGNES_CODE_REJECTED instead of
+                                           INVALID (still counted by agnes_last_error_count) —
+                                           agnes_dedup_reject's rewrite inside the pass (C5 DEDUP) */
 
 /* Route override, bits 8..9 of agnes_config.flags (diagnostics and the
  * route-equivalence tests: every route gives identical codes and States).
@@ -394,7 +398,9 @@ int agnes_fold_counts(agnes_ctx* ctx, agnes_vote_count* counts, uint32_t n_slice
  *                      nothing (round_votes.rs:48-56 never runs for it);
  *   agnes_dedup_reject after the carried tally: the codes of the masked votes
  *                      INVALID -> AGNES_CODE_REJECTED (the DEDUP codes of the
- *                      whole instance; agnes_last_error_count still counts them).
+ *                      whole instance; agnes_last_error_count still counts them);
+ *                      or the carried tally with AGNES_FLAG_MASKED_REJECTED writes
+ *                      REJECTED for them in the pass (one launch fewer).
  * Validity is the tally's: instance id == cfg->reserved, round < max_rounds,
  * type <= 1, validator < n_vals (set reserved % n_sets; batch->instance_set must be
  * NULL, else AGNES_E_UNSUPPORTED).

@@ -37,6 +37,7 @@ class CarriedFake:
         instance_set); counts: VOTE_COUNT_DTYPE [n_segments, 2 * max_rounds]."""
         R = cfg.max_rounds
         one = bool(cfg.flags & abi.FLAG_ONE_INSTANCE)
+        mrej = bool(cfg.flags & abi.FLAG_MASKED_REJECTED)
         n_sets, nv = self.power.shape
         off = np.asarray(b.offsets, dtype=np.int64)
         for k in range(len(off) - 1):
@@ -49,7 +50,7 @@ class CarriedFake:
             for j in range(int(off[k]), int(off[k + 1])):
                 r, t, val, x = int(b.round[j]), int(b.type[j]), int(b.value[j]), int(b.validator[j])
                 if int(b.instance[j]) != want or r >= R or t > 1 or s >= n_sets or x >= nv:
-                    codes[j] = abi.CODE_INVALID
+                    codes[j] = abi.CODE_REJECTED if mrej and t == abi.TYPE_MASKED else abi.CODE_INVALID
                     continue
                 w = int(self.power[s, x])
                 q = r * 2 + t
@@ -77,7 +78,7 @@ class DedupFake:
     first vote of each (round, type, validator) of one instance found across
     slices, the later ones masked out of the tally and coded REJECTED."""
 
-    MASKED = 0xFE
+    MASKED = abi.TYPE_MASKED
 
     def __init__(self, n_sets: int, n_vals: int):
         self.n_sets, self.n_vals = n_sets, n_vals

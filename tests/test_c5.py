@@ -165,7 +165,7 @@ def _dedup_instance(seed=5, n_vals=300, R=2, nil=250):
     return hb, power, abi.config(abi.MODE_DEDUP, 0, R)
 
 
-def _cpu_dedup_slice(hb, power, cfg, lo, hi, segments):
+def _cpu_dedup_slice(hb, power, cfg, lo, hi, segments, in_pass=False):
     """This rank's slice [lo, hi) through tally_one_instance_dedup on the CPU stand-ins."""
     dd = DedupFake(*power.shape)
     sl = types.SimpleNamespace(instance=hb.instance[lo:hi], round=hb.round[lo:hi], type=hb.type[lo:hi],
@@ -180,17 +180,18 @@ def _cpu_dedup_slice(hb, power, cfg, lo, hi, segments):
     fw, fl = ad.tally_one_instance_dedup(
         _fake_tc(CarriedFake(power), view, lo, hi, codes),
         lambda base, f: dd.first(cfg, sl, base, f.numpy()), mask,
-        lambda: dd.reject(view.type[lo:hi], codes), hi - lo, power.shape[1], cfg, segments,
+        None if in_pass else (lambda: dd.reject(view.type[lo:hi], codes)), hi - lo, power.shape[1], cfg, segments,
         torch.device("cpu"), base=lo)
     return codes, fw, fl
 
 
+@pytest.mark.parametrize("in_pass", [False, True])  # True: FLAG_MASKED_REJECTED, no reject call
 @pytest.mark.parametrize("segments", [1, 3, 16])
-def test_split_instance_dedup_equals_whole_cpu(segments):
+def test_split_instance_dedup_equals_whole_cpu(segments, in_pass):
     hb, power, cfg = _dedup_instance()
     want, _, _ = ol.tally(cfg, hb, power)
     assert (want == abi.CODE_REJECTED).sum() > hb.n_votes // 10  # the stream has duplicates
-    codes, _, _ = _cpu_dedup_slice(hb, power, cfg, 0, hb.n_votes, segments)
+    codes, _, _ = _cpu_dedup_slice(hb, power, cfg, 0, hb.n_votes, segments, in_pass)
     assert np.array_equal(codes, want)
 
 
@@ -225,7 +226,7 @@ def _dedup_worker(rank, world, port, q):
     try:
         hb, power, cfg = _dedup_instance(seed=8)
         lo, hi = _slice(hb.n_votes, rank, world)
-        codes, fw, fl = _cpu_dedup_slice(hb, power, cfg, lo, hi, 3)
+        codes, fw, fl = _cpu_dedup_slice(hb, power, cfg, lo, hi, 3, in_pass=rank == 1)  # both ways
         q.put((rank, codes.tobytes(), fw.numpy().tobytes(), fl.numpy().tobytes()))
     finally:
         dist.destroy_process_group()
@@ -364,7 +365,7 @@ def test_gpu_tally_carried_rejects(eng):
         eng.tally_carried(abi.config(abi.MODE_DEDUP, 0, 1), db, codes, counts)
 
 
-def _gpu_dedup_run(eng, hb, power, cfg, segments, hip_fold=True, fused=False):
+def _gpu_dedup_run(eng, hb, power, cfg, segments, hip_fold=True, fused=False, in_pass=False):
     from agnes_amd.engine import DeviceBatch
     eng.upload_power(power)
     db = DeviceBatch.from_host(hb, eng.device)
@@ -375,7 +376,7 @@ def _gpu_dedup_run(eng, hb, power, cfg, segments, hip_fold=True, fused=False):
     ad.tally_one_instance_dedup(_gpu_tc(eng, dbm, codes),
                                 lambda base, f: eng.dedup_first(cfg, db, base, f),
                                 lambda base, f: eng.dedup_mask(cfg, db, base, f, tmask),
-                                lambda: eng.dedup_reject(tmask, codes, n),
+                                None if in_pass else (lambda: eng.dedup_reject(tmask, codes, n)),
                                 n, power.shape[1], cfg, segments, eng.device,
                                 fold=eng.fold_counts if hip_fold else None,
                                 dedup_first_mask=(lambda base, f: eng.dedup_first_mask(cfg, db, base, f, tmask))
@@ -385,13 +386,14 @@ def _gpu_dedup_run(eng, hb, power, cfg, segments, hip_fold=True, fused=False):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("in_pass", [False, True])  # AGNES_FLAG_MASKED_REJECTED instead of agnes_dedup_reject
 @pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("segments,n_vals,R", [(1, 3000, 1), (16, 5000, 2), (300, 20000, 2),
                                                (64, 100000, 1)])
-def test_gpu_split_instance_dedup(eng, segments, n_vals, R, fused):
+def test_gpu_split_instance_dedup(eng, segments, n_vals, R, fused, in_pass):
     hb, power, cfg = _dedup_instance(seed=31 + segments, n_vals=n_vals, R=R)
     want, _, _ = ol.tally(cfg, hb, power)
-    got = _gpu_dedup_run(eng, hb, power, cfg, segments, fused=fused)
+    got = _gpu_dedup_run(eng, hb, power, cfg, segments, fused=fused, in_pass=in_pass)
     assert np.array_equal(got, want)
     assert (got == abi.CODE_REJECTED).any()
 

@@ -122,7 +122,7 @@ def _c5(eng, dedup, fused=False):
     if dedup:
         ad.tally_one_instance_dedup(tc, lambda base, f: eng.dedup_first(cfg, db, base, f),
                                     lambda base, f: eng.dedup_mask(cfg, db, base, f, tmask),
-                                    lambda: eng.dedup_reject(tmask, codes, n), n, n_vals, cfg, 1024,
+                                    None if fused else (lambda: eng.dedup_reject(tmask, codes, n)), n, n_vals, cfg, 1024,
                                     eng.device,
                                     dedup_first_mask=(lambda base, f: eng.dedup_first_mask(cfg, db, base, f, tmask))
                                     if fused else None)
