@@ -28,8 +28,8 @@ struct agnes_ctx {
     agnes_set_info* d_sets = nullptr;
     uint32_t n_sets = 0;
     uint32_t n_vals = 0;
-    unsigned long long* d_err = nullptr; /* the invalid-vote count, then AGNES_QUEUE_WORDS work-queue
-                                            counters (agnes_internal.h): one memset per call */
+    unsigned long long* d_err = nullptr; /* the invalid-vote count's stripes, then AGNES_QUEUE_WORDS
+                                            work-queue counters (agnes_internal.h): one memset per call */
     hipStream_t last_stream = nullptr;
     bool used = false;               /* a call has enqueued work on last_stream */
     hipEvent_t order_ev = nullptr;   /* orders a call on another stream after it */
@@ -326,7 +326,7 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
         c->list_cap = b->n_instances;
     }
     /* the invalid count and the work-queue counters: one memset */
-    AGNES_TRY(hipMemsetAsync(c->d_err, 0, wide_all ? sizeof(unsigned long long) : AGNES_COUNTER_BYTES, st));
+    AGNES_TRY(hipMemsetAsync(c->d_err, 0, wide_all ? AGNES_ERR_BYTES : AGNES_COUNTER_BYTES, st));
     agnes_tally_args a;
     std::memset(&a, 0, sizeof(a));
     a.vb = *b;
@@ -360,7 +360,7 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     a.n_invalid = c->d_err;
     a.list = c->d_list;
     a.walk = c->d_list ? c->d_list + (size_t)c->list_cap : nullptr;
-    a.list_count = c->d_list ? reinterpret_cast<uint32_t*>(c->d_err + 1) : nullptr;
+    a.list_count = c->d_list ? reinterpret_cast<uint32_t*>(c->d_err + AGNES_ERR_BYTES / 8) : nullptr;
     /* DEDUP / RoundSkip tables tag entries with (instance epoch, local vote index):
      * the local index of any vote is < n_votes, so it needs bit_length(n_votes - 1) bits */
     if (cfg->mode == AGNES_MODE_DEDUP || (cfg->flags & AGNES_FLAG_ROUND_SKIP)) {
@@ -442,9 +442,11 @@ int agnes_last_error_count(agnes_ctx* c, uint64_t* out) {
     if (!c || !out) return AGNES_E_INVALID;
     AGNES_TRY(hipSetDevice(c->device));
     AGNES_TRY(hipStreamSynchronize(c->last_stream));
-    unsigned long long v = 0;
-    AGNES_TRY(hipMemcpy(&v, c->d_err, sizeof(v), hipMemcpyDeviceToHost));
-    *out = v;
+    unsigned long long v[AGNES_ERR_BYTES / 8];
+    AGNES_TRY(hipMemcpy(v, c->d_err, sizeof(v), hipMemcpyDeviceToHost));
+    uint64_t sum = 0;
+    for (uint32_t k = 0; k < AGNES_ERR_STRIPES; ++k) sum += v[k * (AGNES_ERR_STRIDE / 8u)];
+    *out = sum;
     return AGNES_OK;
 }
 
@@ -470,7 +472,7 @@ int agnes_apply_msgs(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_bat
     AGNES_TRY(hipSetDevice(c->device));
     const hipStream_t st = (hipStream_t)stream;
     AGNES_ORDER(c, st);
-    AGNES_TRY(hipMemsetAsync(c->d_err, 0, sizeof(unsigned long long), st));
+    AGNES_TRY(hipMemsetAsync(c->d_err, 0, AGNES_ERR_BYTES, st));
     return status_of(agnes_launch_apply_msgs(b, kinds, pol, c->d_power, c->d_sets, c->n_sets, c->n_vals,
                                              cfg->max_rounds, cfg->flags, states, msgs, codes, c->d_err, st));
 }
@@ -679,7 +681,7 @@ int agnes_tally_events(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_b
         /* the flow kernel counted its batches' records; the walk list's instances here */
         AGNES_TRY(hipMemsetAsync(offsets, 0, sizeof(uint64_t), st));
         AGNES_TRY(agnes_launch_event_count_list(b, codes, c->d_list + (size_t)c->list_cap,
-                                                reinterpret_cast<const uint32_t*>(c->d_err + 1) + AGNES_WALK_COUNT,
+                                                reinterpret_cast<const uint32_t*>(c->d_err + AGNES_ERR_BYTES / 8) + AGNES_WALK_COUNT,
                                                 offsets, c->num_cus, st));
         AgnesKt kt("event_scan", st);
         AGNES_TRY(agnes_launch_offsets_scan(offsets, b->n_instances, c->d_scan, st));

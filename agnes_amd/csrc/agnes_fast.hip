@@ -691,7 +691,7 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
     }
     flush();
     const uint32_t nb = rdl(scan(bad), 63u);
-    if (lane == 0 && nb) atomicAdd(a.n_invalid, (unsigned long long)nb);
+    if (lane == 0 && nb) add_invalid(a.n_invalid, (unsigned long long)nb);
 }
 
 } // namespace fast

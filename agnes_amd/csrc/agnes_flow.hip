@@ -1154,7 +1154,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
     }
     flush();
     const uint32_t nb = rdl(scan(bad), 63u);
-    if (lane == 0 && nb) atomicAdd(a.n_invalid, (unsigned long long)nb);
+    if (lane == 0 && nb) add_invalid(a.n_invalid, (unsigned long long)nb);
 }
 
 } // namespace flow

@@ -193,12 +193,23 @@ hipError_t agnes_launch_dedup_reject(const uint8_t* type_masked, uint64_t n, uin
 /* list_count[0] counts the deferred (i64 LIST) list; list_count[1 .. AGNES_QUEUE_N] are
  * the u32 kernels' work-queue counters; list_count[AGNES_WALK_COUNT] counts the sweep's
  * walk list and list_count[AGNES_WALK_QUEUE] is the walk kernel's queue counter; they
- * follow the u64 invalid-vote count in one device block, zeroed by one memset per call */
+ * follow the invalid-vote count in one device block, zeroed by one memset per call.
+ * The invalid-vote count is AGNES_ERR_STRIPES u64 stripes AGNES_ERR_STRIDE bytes
+ * apart: a wave adds its count to its block's stripe (add_invalid) — a thousand waves
+ * adding to ONE address serialize at the memory side (10 us of C5d's 45-us pass B,
+ * measured) — and agnes_last_error_count sums the stripes. */
 #define AGNES_QUEUE_N 256
 #define AGNES_WALK_COUNT (AGNES_QUEUE_N + 1)
 #define AGNES_WALK_QUEUE (AGNES_QUEUE_N + 2)
 #define AGNES_QUEUE_WORDS (AGNES_QUEUE_N + 4)
-#define AGNES_COUNTER_BYTES (8 + AGNES_QUEUE_WORDS * 4)
+#define AGNES_ERR_STRIPES 32
+#define AGNES_ERR_STRIDE 512
+#define AGNES_ERR_BYTES (AGNES_ERR_STRIPES * AGNES_ERR_STRIDE)
+#define AGNES_COUNTER_BYTES (AGNES_ERR_BYTES + AGNES_QUEUE_WORDS * 4)
+/* one wave's invalid votes into its block's stripe of the count */
+__device__ __forceinline__ void add_invalid(unsigned long long* n_invalid, unsigned long long n) {
+    atomicAdd(n_invalid + (blockIdx.x % AGNES_ERR_STRIPES) * (AGNES_ERR_STRIDE / 8u), n);
+}
 #define AGNES_MAX_LDS_PER_WAVE (36 * 1024)
 
 #endif

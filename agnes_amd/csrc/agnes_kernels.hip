@@ -1027,7 +1027,7 @@ __global__ __launch_bounds__(256) void tally_kernel(agnes_tally_args a, uint32_t
     }
     flush();
     const uint32_t nb = rdl(scan(bad_lane), 63u);
-    if (lane == 0 && nb) atomicAdd(a.n_invalid, (unsigned long long)nb);
+    if (lane == 0 && nb) add_invalid(a.n_invalid, (unsigned long long)nb);
 }
 
 /* ------------------------------------------------------------------ */
@@ -1144,7 +1144,7 @@ __global__ __launch_bounds__(64) void apply_msgs_kernel(MsgArgs a) {
         a.codes[j] = (uint8_t)code;
     }
     sm_store(&a.states[i], s);
-    if (bad) atomicAdd(a.n_invalid, (unsigned long long)bad);
+    if (bad) add_invalid(a.n_invalid, (unsigned long long)bad);
 }
 
 __global__ __launch_bounds__(256) void apply_events_kernel(agnes_state* states, uint32_t n,

@@ -627,7 +627,7 @@ __global__ __launch_bounds__(256) void sweep(agnes_tally_args a, uint32_t lds_pe
     }
     flush();
     const uint32_t nb = rdl(scan(bad), 63u);
-    if (lane == 0 && nb) atomicAdd(a.n_invalid, (unsigned long long)nb);
+    if (lane == 0 && nb) add_invalid(a.n_invalid, (unsigned long long)nb);
 }
 
 } // namespace sweep
