@@ -121,7 +121,7 @@ WORKLOADS = {
                 gen=dict(n_instances=1, n_vals=1_000_000, rounds_min=1, rounds_max=1, nil_permille=200,
                          dup_permille=100, equiv_permille=100),
                 power=(abi.POWER_ZIPF, 1, 1_000_000, 1), mode=abi.MODE_DEDUP, flags=0,
-                max_rounds=1, scaling="strong", one_instance=True, segments=1024),
+                max_rounds=1, scaling="strong", one_instance=True, segments=2048),
     # signed wire records -> verified SoA columns (not a BASELINE config)
     "wire": dict(desc="wire ingest: 104-byte signed vote records (Ed25519, OpenSSL-made fixture records "
                       "replicated to 2^20 per GPU, 48 of every 92 valid) -> verified SoA columns",
