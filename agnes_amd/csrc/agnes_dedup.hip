@@ -50,17 +50,25 @@ __device__ __forceinline__ bool valid_key(const DedupArgs& a, uint64_t j, uint64
     return ok;
 }
 
+/* 0xFF in byte s for bit s of ok (ok < 16) */
+__device__ __forceinline__ uint32_t ok_bytes(uint32_t ok) {
+    const uint32_t b = (ok * 0x00204081u) & 0x01010101u;
+    return (b << 8) - b;
+}
+
 /* V4: four consecutive votes per thread (instance / validator 16-B, round / type 4-B
  * aligned columns): the keys of votes j .. j+3 (j a multiple of 4), bit s of the
- * returned mask = vote j+s is valid */
+ * returned mask = vote j+s is valid; tb: their type bytes */
 template <bool V4>
-__device__ __forceinline__ uint32_t valid_keys4(const DedupArgs& a, uint64_t j, uint64_t (&key)[4]) {
+__device__ __forceinline__ uint32_t valid_keys4(const DedupArgs& a, uint64_t j, uint64_t (&key)[4], uint32_t& tb) {
     uint32_t ok = 0;
+    tb = 0;
     if (V4 && j + 4u <= a.n_votes) {
         const uint4 in = *reinterpret_cast<const uint4*>(a.instance + j);
         const uint4 vx = *reinterpret_cast<const uint4*>(a.validator + j);
         const uint32_t r4 = *reinterpret_cast<const uint32_t*>(a.round + j);
         const uint32_t t4 = *reinterpret_cast<const uint32_t*>(a.type + j);
+        tb = t4;
         const uint32_t ins[4] = {in.x, in.y, in.z, in.w}, xs[4] = {vx.x, vx.y, vx.z, vx.w};
 #pragma unroll
         for (uint32_t s = 0; s < 4u; ++s) {
@@ -72,7 +80,10 @@ __device__ __forceinline__ uint32_t valid_keys4(const DedupArgs& a, uint64_t j, 
 #pragma unroll
         for (uint32_t s = 0; s < 4u; ++s) {
             key[s] = 0;
-            if (j + s < a.n_votes && valid_key(a, j + s, key[s])) ok |= 1u << s;
+            if (j + s < a.n_votes) {
+                if (valid_key(a, j + s, key[s])) ok |= 1u << s;
+                tb |= (uint32_t)a.type[j + s] << (8u * s);
+            }
         }
     }
     return ok;
@@ -92,7 +103,8 @@ __global__ __launch_bounds__(256) void mask_kernel(DedupArgs a, const unsigned l
     if (V4) { /* four votes per thread; the keys' first-index gathers issued together */
         for (uint64_t j = 4u * ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x); j < a.n_votes; j += 4u * stride) {
             uint64_t key[4];
-            const uint32_t ok = valid_keys4<true>(a, j, key);
+            uint32_t tb;
+            const uint32_t ok = valid_keys4<true>(a, j, key, tb);
             unsigned long long f[4];
 #pragma unroll
             for (uint32_t s = 0; s < 4u; ++s) f[s] = ((ok >> s) & 1u) ? first[key[s]] : 0ull;
@@ -144,8 +156,8 @@ __global__ __launch_bounds__(256) void reject_kernel(const uint8_t* type_masked,
  *   prefix   block b: its row of cnt as an exclusive scan (the offset of each
  *            block's votes inside the bucket) and the row's total;
  *   scatter  block g: the bucket starts (an exclusive scan of the row totals in
- *            LDS; block 0 writes them out), then each valid vote to its bucket's
- *            range as {key % KB, j} (8 B), its slots claimed by LDS atomics;
+ *            LDS; block 0 writes them out), the block's valid votes sorted by
+ *            bucket in LDS, then written as {key % KB, j} (8 B) runs per bucket;
  *   min      block b: an LDS table of KB u32 indices, atomicMin per entry, then
  *            first[key] = min(first[key], base + index) for its keys (coalesced).
  * About 10 + 10 + 8 + 8 B per vote plus the table's read and write. */
@@ -194,7 +206,8 @@ __global__ __launch_bounds__(256) void bucket_count(DedupArgs a, uint32_t nb, ui
     const uint64_t j0 = (uint64_t)g * BV, j1 = j0 + BV < a.n_votes ? j0 + BV : a.n_votes;
     for (uint64_t j = j0 + 4u * threadIdx.x; j < j1; j += 1024u) {
         uint64_t key[4];
-        const uint32_t ok = valid_keys4<V4>(a, j, key);
+        uint32_t tb;
+        const uint32_t ok = valid_keys4<V4>(a, j, key, tb);
 #pragma unroll
         for (uint32_t s = 0; s < 4u; ++s)
             if ((ok >> s) & 1u) atomicAdd(&hist[(uint32_t)(key[s] / KB)], 1u);
@@ -227,14 +240,22 @@ __global__ __launch_bounds__(256) void bucket_prefix(uint32_t G, uint32_t* cnt, 
     if (t == 0u) rowtot[blockIdx.x] = carry;
 }
 
-/* MASK (agnes_dedup_first_mask): also the mask's defaults, AGNES_TYPE_MASKED for a
- * valid vote (the min pass writes the firsts' types over it) and 0xFF for an invalid
- * one; the pair then carries the vote's type in bit 13 */
+/* The block's valid votes are first sorted by bucket in LDS (a local counting sort:
+ * the block's per-bucket counts are its column of cnt), then written out in that
+ * order, so each bucket's run of the block (~BV / nb pairs) leaves as consecutive
+ * 8-B stores instead of one random line per vote.  MASK (agnes_dedup_first_mask):
+ * also the mask's defaults, the vote's own type for a valid vote (the min pass
+ * writes AGNES_TYPE_MASKED over the ones that are not their key's first) and 0xFF for
+ * an invalid one. */
 template <bool V4, bool MASK>
 __global__ __launch_bounds__(256) void bucket_scatter(DedupArgs a, uint32_t nb, uint32_t G, const uint32_t* cnt,
                                                       const uint32_t* rowtot, uint32_t* bstart, uint2* pairs,
                                                       uint8_t* type_out) {
-    __shared__ uint32_t cur[MAX_NB + 1u];
+    __shared__ uint32_t cur[MAX_NB + 1u]; /* the block's first global slot per bucket */
+    __shared__ uint32_t lst[MAX_NB + 1u]; /* the block's local start per bucket       */
+    __shared__ uint32_t lcur[MAX_NB];     /* local slot cursors                       */
+    __shared__ uint2 stage[BV];
+    __shared__ uint16_t sbk[BV];
     const uint32_t g = blockIdx.x;
     for (uint32_t b = threadIdx.x; b < nb; b += 256u) cur[b] = rowtot[b];
     __syncthreads();
@@ -242,30 +263,43 @@ __global__ __launch_bounds__(256) void bucket_scatter(DedupArgs a, uint32_t nb, 
     if (g == 0u)
         for (uint32_t b = threadIdx.x; b <= nb; b += 256u) bstart[b] = cur[b];
     __syncthreads();
-    for (uint32_t b = threadIdx.x; b < nb; b += 256u) cur[b] += cnt[(uint64_t)b * G + g];
+    for (uint32_t b = threadIdx.x; b < nb; b += 256u) {
+        const uint32_t o = cnt[(uint64_t)b * G + g]; /* the block's offset inside the bucket */
+        const uint32_t o1 = g + 1u < G ? cnt[(uint64_t)b * G + g + 1u] : rowtot[b];
+        cur[b] += o;
+        lst[b] = o1 - o; /* the block's count, scanned below */
+    }
+    __syncthreads();
+    lds_scan_1024(lst, nb);
+    for (uint32_t b = threadIdx.x; b < nb; b += 256u) lcur[b] = lst[b];
     __syncthreads();
     const uint64_t j0 = (uint64_t)g * BV, j1 = j0 + BV < a.n_votes ? j0 + BV : a.n_votes;
     for (uint64_t j = j0 + 4u * threadIdx.x; j < j1; j += 1024u) {
         uint64_t key[4];
-        const uint32_t ok = valid_keys4<V4>(a, j, key);
+        uint32_t tb;
+        const uint32_t ok = valid_keys4<V4>(a, j, key, tb);
 #pragma unroll
         for (uint32_t s = 0; s < 4u; ++s) {
             if ((ok >> s) & 1u) {
-                const uint32_t p = atomicAdd(&cur[(uint32_t)(key[s] / KB)], 1u);
-                /* key % KB = (r * 2 + t) * n_vals + x mod KB; the type from the key is not
-                 * recoverable here, so MASK reads it (bit 13) */
-                const uint32_t tb = MASK ? ((uint32_t)a.type[j + s] << 13) : 0u;
-                pairs[p] = make_uint2((uint32_t)(key[s] % KB) | tb, (uint32_t)(j + s));
+                const uint32_t bk = (uint32_t)(key[s] / KB);
+                const uint32_t p = atomicAdd(&lcur[bk], 1u);
+                stage[p] = make_uint2((uint32_t)(key[s] % KB), (uint32_t)(j + s));
+                sbk[p] = (uint16_t)bk;
             }
         }
         if (MASK) {
-            uint32_t o = 0;
-#pragma unroll
-            for (uint32_t s = 0; s < 4u; ++s) o |= (((ok >> s) & 1u) ? AGNES_TYPE_MASKED : 0xFFu) << (8u * s);
+            const uint32_t m = ok_bytes(ok);
+            const uint32_t o = (tb & m) | ~m;
             if (V4 && j + 4u <= a.n_votes) *reinterpret_cast<uint32_t*>(type_out + j) = o;
             else
                 for (uint32_t s = 0; s < 4u && j + s < j1; ++s) type_out[j + s] = (uint8_t)(o >> (8u * s));
         }
+    }
+    __syncthreads();
+    const uint32_t tot = lst[nb];
+    for (uint32_t i = threadIdx.x; i < tot; i += 256u) {
+        const uint32_t bk = sbk[i];
+        pairs[cur[bk] + (i - lst[bk])] = stage[i];
     }
 }
 
@@ -280,7 +314,7 @@ __global__ __launch_bounds__(MT) void bucket_min(uint64_t n_keys, const uint32_t
     const uint32_t e0 = bstart[b], e1 = bstart[b + 1u];
     for (uint32_t e = e0 + threadIdx.x; e < e1; e += MT) {
         const uint2 q = pairs[e];
-        atomicMin(&tab[q.x & (KB - 1u)], q.y);
+        atomicMin(&tab[q.x], q.y);
     }
     __syncthreads();
     const uint64_t k0 = (uint64_t)b * KB;
@@ -293,11 +327,11 @@ __global__ __launch_bounds__(MT) void bucket_min(uint64_t n_keys, const uint32_t
             if (v < old) first[k0 + k] = v;
         }
     }
-    if (MASK) { /* the firsts' types over the scatter's AGNES_TYPE_MASKED */
+    if (MASK) { /* AGNES_TYPE_MASKED over the scatter's type for a vote that is not its key's first */
         __syncthreads();
         for (uint32_t e = e0 + threadIdx.x; e < e1; e += MT) {
             const uint2 q = pairs[e];
-            if (tab[q.x & (KB - 1u)] == q.y) type_out[q.y] = (uint8_t)(q.x >> 13);
+            if (tab[q.x & (KB - 1u)] != q.y) type_out[q.y] = (uint8_t)AGNES_TYPE_MASKED;
         }
     }
 }
