@@ -351,7 +351,8 @@ def test_gpu_split_instance_continued_across_calls(eng):
 
 @pytest.mark.gpu
 def test_gpu_tally_carried_rejects(eng):
-    """ONE_INSTANCE needs the carried entry point; the carried path is REFERENCE only"""
+    """ONE_INSTANCE and MASKED_REJECTED need the carried entry point; the carried path is
+    REFERENCE only"""
     from agnes_amd.engine import DeviceBatch
     from agnes_amd.lib import AgnesError
     hb, power, cfg = _instance(seed=3, n_vals=64, R=1)
@@ -360,6 +361,8 @@ def test_gpu_tally_carried_rejects(eng):
     codes = torch.zeros(hb.n_votes, dtype=torch.uint8, device=eng.device)
     with pytest.raises(AgnesError):
         eng.tally(abi.config(abi.MODE_REFERENCE, abi.FLAG_ONE_INSTANCE, 1), db, codes)
+    with pytest.raises(AgnesError):
+        eng.tally(abi.config(abi.MODE_REFERENCE, abi.FLAG_MASKED_REJECTED, 1), db, codes)
     counts = torch.zeros((1, 2, 3), dtype=torch.int64, device=eng.device)
     with pytest.raises(AgnesError):
         eng.tally_carried(abi.config(abi.MODE_DEDUP, 0, 1), db, codes, counts)
