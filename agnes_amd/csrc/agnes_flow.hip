@@ -560,6 +560,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                 };
                 /* ---- K1: votes of the chunk + validation + weight gather ---- */
                 uint32_t value[LV], val[LV], r8[2], t8[2];
+                uint32_t w[LV];
+                uint64_t wq[W64 ? LV : 1u]; /* (W64) the weights from the i64 table */
                 uint32_t nb0 = 0, nb1 = 0; /* 0x10 in the bytes of nil votes */
                 bool all_ok;
                 uint32_t okb0, okb1; /* byte masks of the votes that checked in (exact path) */
@@ -582,6 +584,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                         val[4] = d1.x; val[5] = d1.y; val[6] = d1.z; val[7] = d1.w;
                         r8[0] = rr.x; r8[1] = rr.y;
                         t8[0] = tt.x; t8[1] = tt.y;
+                    }
+                    /* K1: w = power[set][validator] (consensus_executor.rs:62-63 ->
+                     * validators.rs:7), gathered before the checks so their VALU work
+                     * covers the latency: an index outside the set's row reads entry 0
+                     * (a vote that checks out weighs 0, below) */
+                    {
+                        const uint32_t pbA = recA.y, pbB = recB.y;
+#pragma unroll
+                        for (uint32_t s = 0; s < LV; ++s) {
+                            const uint32_t v = val[s], pb = s < 4u ? pbA : pbB, nvs = s < 4u ? recA.z : recB.z;
+                            const uint32_t idx = v < nvs ? pb + v : 0u;
+                            if constexpr (W64)
+                                wq[s] = PC ? reinterpret_cast<const uint64_t*>(agnes_smem)[idx] : (uint64_t)a.power[idx];
+                            else
+                                w[s] = PC ? reinterpret_cast<const uint32_t*>(agnes_smem)[idx] : a.power32[idx];
+                        }
                     }
 #pragma unroll
                     for (uint32_t s = 0; s < 4u; ++s) {
@@ -621,35 +639,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                         bad += (uint32_t)(__builtin_popcount(p0m & ~okb0) + __builtin_popcount(p1m & ~okb1)) >> 3;
                     }
                 }
-                uint32_t w[LV];
-                uint64_t wq[W64 ? LV : 1u]; /* (W64) the weights from the i64 table */
-                if constexpr (W64) {
-                    const uint32_t pbA = recA.y, pbB = recB.y;
+                if (!(all_ok && lo_r == 0u && hi_r == CH)) { /* votes that checked out weigh 0 */
 #pragma unroll
                     for (uint32_t s = 0; s < LV; ++s) {
                         const bool o = (((s < 4u ? okb0 : okb1) >> (8u * (s & 3u))) & 1u) != 0u;
-                        const uint32_t idx = o ? (s < 4u ? pbA : pbB) + val[s] : 0u;
-                        const uint64_t x = PC ? reinterpret_cast<const uint64_t*>(agnes_smem)[idx] : (uint64_t)a.power[idx];
-                        wq[s] = o ? x : 0ull;
-                    }
-                } else {
-                    /* K1: w = power[set][validator] (consensus_executor.rs:62-63 ->
-                     * validators.rs:7); a vote that checked out weighs 0 */
-                    const uint32_t pbA = recA.y, pbB = recB.y;
-                    if (all_ok && lo_r == 0u && hi_r == CH) {
-#pragma unroll
-                        for (uint32_t s = 0; s < LV; ++s) {
-                            const uint32_t idx = (s < 4u ? pbA : pbB) + val[s];
-                            w[s] = PC ? reinterpret_cast<const uint32_t*>(agnes_smem)[idx] : a.power32[idx];
-                        }
-                    } else {
-#pragma unroll
-                        for (uint32_t s = 0; s < LV; ++s) {
-                            const bool o = (((s < 4u ? okb0 : okb1) >> (8u * (s & 3u))) & 1u) != 0u;
-                            const uint32_t idx = o ? (s < 4u ? pbA : pbB) + val[s] : 0u;
-                            const uint32_t x = PC ? reinterpret_cast<const uint32_t*>(agnes_smem)[idx] : a.power32[idx];
-                            w[s] = o ? x : 0u;
-                        }
+                        if constexpr (W64) wq[s] = o ? wq[s] : 0ull;
+                        else w[s] = o ? w[s] : 0u;
                     }
                 }
                 /* a gather from HBM retires before the DMA below is issued: a wait on it
