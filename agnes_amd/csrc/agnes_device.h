@@ -69,7 +69,19 @@ __device__ __forceinline__ uint64_t dpp_step64(uint64_t x) {
     return x + (((uint64_t)hi << 32) | lo);
 }
 
+/* u64 steps as two DPP-sourced adds (carry through VCC): the lane's own value plus
+ * the source lane's, bound_ctrl zero for a source outside the row, rows outside
+ * row_mask unchanged — 2 VALU per step instead of the compiler's moves + adds.
+ * s_nop 1: the DPP read of a VGPR the previous VALU wrote needs 2 wait states. */
+#define AGNES_DPP_ADD64(CTRL, RMASK)                                                                   \
+    asm volatile("s_nop 1\n\t"                                                                         \
+                 "v_add_co_u32_dpp %0, vcc, %0, %0 " CTRL " row_mask:" RMASK " bank_mask:0xf bound_ctrl:1\n\t" \
+                 "v_addc_co_u32_dpp %1, vcc, %1, %1, vcc " CTRL " row_mask:" RMASK " bank_mask:0xf bound_ctrl:1"   \
+                 : "+v"(lo), "+v"(hi)                                                                  \
+                 :                                                                                     \
+                 : "vcc")
 __device__ __forceinline__ uint64_t scan(uint64_t x) {
+#ifdef AGNES_SCAN64_PLAIN
     x = dpp_step64<0x111, 0xf>(x);
     x = dpp_step64<0x112, 0xf>(x);
     x = dpp_step64<0x114, 0xf>(x);
@@ -77,6 +89,16 @@ __device__ __forceinline__ uint64_t scan(uint64_t x) {
     x = dpp_step64<0x142, 0xa>(x);
     x = dpp_step64<0x143, 0xc>(x);
     return x;
+#else
+    uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    AGNES_DPP_ADD64("row_shr:1", "0xf");
+    AGNES_DPP_ADD64("row_shr:2", "0xf");
+    AGNES_DPP_ADD64("row_shr:4", "0xf");
+    AGNES_DPP_ADD64("row_shr:8", "0xf");
+    AGNES_DPP_ADD64("row_bcast:15", "0xa");
+    AGNES_DPP_ADD64("row_bcast:31", "0xc");
+    return ((uint64_t)hi << 32) | lo;
+#endif
 }
 
 __host__ __device__ inline uint64_t align16(uint64_t x) { return (x + 15u) & ~15ull; }
