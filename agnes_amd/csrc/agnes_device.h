@@ -97,6 +97,9 @@ __device__ __forceinline__ uint64_t scan(uint64_t x) {
     AGNES_DPP_ADD64("row_shr:8", "0xf");
     AGNES_DPP_ADD64("row_bcast:15", "0xa");
     AGNES_DPP_ADD64("row_bcast:31", "0xc");
+    /* the compiler's hazard tracking does not look inside the asm: the wait states a
+     * following DPP read of lo / hi would need */
+    asm volatile("s_nop 1" ::: "memory");
     return ((uint64_t)hi << 32) | lo;
 #endif
 }
