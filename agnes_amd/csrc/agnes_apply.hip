@@ -386,19 +386,27 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
     issue(blk);
     for (;;) {
         fast::dma_wait();
-#pragma unroll 1
+        /* the block's four windows out of LDS at once (one wait, not one per window) */
+        uint4 cw[4], rw[4];
+#pragma unroll
         for (uint32_t k = 0; k < 4u; ++k) {
             const uint64_t w = blk + 16u * k;
-            if (w >= hi) break;
             unsigned char* const cs = wbase + k * 1024u + 16u * lane;
             unsigned char* const rs = wbase + (4u + k) * 1024u + 16u * lane;
-            if (w + 16u > lo && w > wmax) { /* past the batch end: the real bytes */
+            if (w < hi && w + 16u > lo && w > wmax) { /* past the batch end: the real bytes */
                 tail_fill(a.codes, w, NV, cs);
                 tail_fill(a.vb.round, w, NV, rs);
             }
+            cw[k] = *reinterpret_cast<const uint4*>(cs);
+            rw[k] = *reinterpret_cast<const uint4*>(rs);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 4u; ++k) {
+            const uint64_t w = blk + 16u * k;
+            if (w >= hi) break;
             if (w + 16u > lo) {
-                if (SKIP) walk(w, *reinterpret_cast<const uint4*>(cs), *reinterpret_cast<const uint4*>(rs));
-                else walk_ns(w, *reinterpret_cast<const uint4*>(cs), *reinterpret_cast<const uint4*>(rs));
+                if (SKIP) walk(w, cw[k], rw[k]);
+                else walk_ns(w, cw[k], rw[k]);
             }
             if (step == AGNES_STEP_COMMIT) break;
         }
