@@ -161,7 +161,10 @@ __global__ __launch_bounds__(256) void reject_kernel(const uint8_t* type_masked,
  *   min      block b: an LDS table of KB u32 indices, atomicMin per entry, then
  *            first[key] = min(first[key], base + index) for its keys (coalesced).
  * About 10 + 10 + 8 + 8 B per vote plus the table's read and write. */
-constexpr uint32_t KB = 8192u;     /* keys per bucket (32 KB of LDS indices) */
+#ifndef AGNES_DEDUP_KB
+#define AGNES_DEDUP_KB 8192
+#endif
+constexpr uint32_t KB = AGNES_DEDUP_KB; /* keys per bucket (32 KB of LDS indices) */
 constexpr uint32_t MAX_NB = 1024u; /* buckets (LDS histograms)               */
 #ifndef AGNES_DEDUP_BV
 #define AGNES_DEDUP_BV 4096
