@@ -145,9 +145,11 @@ VOTE_EVENT_DTYPE = np.dtype([("vote", "<u8"), ("instance", "<u4"), ("value", "<u
 assert VOTE_EVENT_DTYPE.itemsize == 24
 # agnes_multi_exchange modes (include/agnes.h)
 MULTI_EXCHANGE_AUTO, MULTI_EXCHANGE_HOST, MULTI_EXCHANGE_RCCL = 0, 1, 2
+# agnes_multi_stats.exchange bits
+MULTI_X_RCCL, MULTI_X_FALLBACK, MULTI_X_HOST = 1, 2, 4
 VOTE_COUNT_DTYPE = np.dtype([("value_w", "<i8"), ("nil_w", "<i8"), ("value", "<u4"),
                              ("reserved", "<u4")])  # agnes_vote_count
-MULTI_STATS_DTYPE = np.dtype([("device", "<u4"), ("i0", "<u4"), ("i1", "<u4"), ("pad", "<u4"),
+MULTI_STATS_DTYPE = np.dtype([("device", "<u4"), ("i0", "<u4"), ("i1", "<u4"), ("exchange", "<u4"),
                               ("n_votes", "<u8"), ("n_invalid", "<u8"), ("h2d_ms", "<f8"), ("tally_ms", "<f8"),
                               ("d2h_ms", "<f8")])
 assert STATE_DTYPE.itemsize == 64 and EVENT_DTYPE.itemsize == 24 and MESSAGE_DTYPE.itemsize == 24

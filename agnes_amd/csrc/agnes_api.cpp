@@ -346,7 +346,7 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     if (a.states && states_in && states_in != states) {
         /* the sweep route reads the input States itself; the other routes work in place */
         const uint32_t route = (cfg->flags >> AGNES_ROUTE_SHIFT) & AGNES_ROUTE_MASK;
-        const bool sweep = !wide_all && (!w64 || cfg->max_rounds == 1u) && route == AGNES_ROUTE_AUTO &&
+        const bool sweep = !wide_all && route == AGNES_ROUTE_AUTO &&
                            cfg->mode == AGNES_MODE_REFERENCE &&
                            !(cfg->flags & AGNES_FLAG_ROUND_SKIP) && cfg->max_rounds <= 15u;
         if (sweep) {
@@ -752,8 +752,15 @@ int agnes_dedup_mask(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_bat
 
 int agnes_dedup_first_mask(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint64_t base,
                            uint64_t* first, uint8_t* type_out, void* stream) {
-    if (!type_out && b && b->n_votes) return AGNES_E_INVALID;
-    if (b && b->n_votes == 0) return AGNES_OK;
+    if (!c || !cfg_ok(cfg) || !b || !first) return AGNES_E_INVALID;
+    if (!type_out && b->n_votes) return AGNES_E_INVALID;
+    if (b->n_votes == 0) { /* no vote: the table is still written whole (INT64_MAX everywhere) */
+        if (c->n_vals == 0) return AGNES_E_INVALID;
+        AGNES_TRY(hipSetDevice(c->device));
+        AGNES_ORDER(c, (hipStream_t)stream);
+        AGNES_TRY(agnes_launch_dedup_fill(first, 2ull * cfg->max_rounds * c->n_vals, (hipStream_t)stream));
+        return AGNES_OK;
+    }
     return dedup_impl(c, cfg, b, base, first, type_out, stream, true);
 }
 

@@ -170,6 +170,8 @@ constexpr uint32_t MAX_NB = 1024u; /* buckets (LDS histograms)               */
 #define AGNES_DEDUP_BV 4096
 #endif
 constexpr uint32_t BV = AGNES_DEDUP_BV; /* votes per count / scatter block */
+static_assert((KB & (KB - 1u)) == 0u && KB * 4u <= 64u * 1024u, "AGNES_DEDUP_KB: a power of two, its LDS table <= 64 KiB");
+static_assert(BV % 4u == 0u && BV * 8u <= 64u * 1024u, "AGNES_DEDUP_BV: a multiple of 4, its LDS stage <= 64 KiB");
 
 /* exclusive scan of x[0..n) in LDS, n <= 1024, by a 256-thread block; the total into x[n] */
 __device__ void lds_scan_1024(uint32_t* x, uint32_t n) {
@@ -334,7 +336,7 @@ __global__ __launch_bounds__(MT) void bucket_min(uint64_t n_keys, const uint32_t
         __syncthreads();
         for (uint32_t e = e0 + threadIdx.x; e < e1; e += MT) {
             const uint2 q = pairs[e];
-            if (tab[q.x & (KB - 1u)] != q.y) type_out[q.y] = (uint8_t)AGNES_TYPE_MASKED;
+            if (tab[q.x] != q.y) type_out[q.y] = (uint8_t)AGNES_TYPE_MASKED;
         }
     }
 }

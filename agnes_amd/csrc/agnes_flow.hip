@@ -206,7 +206,6 @@ struct Hdr {
 #endif
 template <bool PC, bool SM, bool R1, bool EVC, bool W64>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES_FLOW_W64_WPE : AGNES_FLOW_WPE))) void flow(agnes_tally_args a, uint32_t lds_per_wave) {
-    static_assert(!W64 || (R1 && !EVC), "W64: one round, no record counts");
     constexpr uint32_t RW = W64 ? RECW64 : RECW; /* record words */
 
     const uint32_t lane = lane_id();
@@ -862,67 +861,102 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                     }
                     __builtin_amdgcn_wave_barrier();
                 };
-                if constexpr (W64) {
-                    /* one round, u64 sums: the four buckets as separate lane-serial prefixes
-                     * (prevote / precommit x value / nil), the vote's own type's sums after it
-                     * kept per vote, four u64 DPP scans, thresholds q2 - base in int64 */
-                    /* pass 1: the lane's bucket totals (and through vote 3); the per-vote sums are
-                     * recomputed in pass 2 rather than held (VGPRs) */
+                /* W64: the same pass with u64 sums (the u64 domain, agnes_fast.h defer_si):
+                 * the four buckets as separate lane-serial u64 prefixes (prevote / precommit x
+                 * value / nil), four u64 DPP scans, and the compares on each vote's own running
+                 * sums (the base before the lane plus the lane prefix) against q2 -- no per-vote
+                 * thresholds held.  Pass 1 sums the lane's bucket totals (and through vote 3);
+                 * pass 2 recomputes the running sums rather than holding them (VGPRs).  ONE:
+                 * every round of the chunk in one pass (runs mode, each unit its run's carry). */
+                auto pass64 = [&](auto one_t, uint32_t r) {
+                    constexpr bool ONE = decltype(one_t)::value;
+                    const uint32_t sAx = ONE ? sAr : sA;
+                    const bool splitx = ONE ? splitr : split, multix = ONE ? multir : multi;
+                    /* 0xFF in the bytes of this round's votes */
+                    const uint32_t rm0 = (R > 1u && !ONE) ? mark_bytes(zero_marks(r8[0] ^ (r * 0x01010101u))) : 0xFFFFFFFFu;
+                    const uint32_t rm1 = (R > 1u && !ONE) ? mark_bytes(zero_marks(r8[1] ^ (r * 0x01010101u))) : 0xFFFFFFFFu;
+                    auto wt = [&](uint32_t s) -> uint64_t { /* the vote's weight in this pass */
+                        uint64_t x = wq[s];
+                        if (R > 1u && !ONE) {
+                            const int32_t m = __builtin_amdgcn_sbfe((int32_t)(s < 4u ? rm0 : rm1), 8u * (s & 3u), 8u);
+                            x &= (uint64_t)(int64_t)m;
+                        }
+                        return x;
+                    };
                     uint64_t Svp = 0, Snp = 0, Svc = 0, Snc = 0, P3vp = 0, P3np = 0, P3vc = 0, P3nc = 0;
 #pragma unroll
                     for (uint32_t s = 0; s < LV; ++s) {
                         const uint32_t bs = 8u * (s & 3u);
                         const bool pc = (((s < 4u ? t8[0] : t8[1]) >> bs) & 1u) != 0u;
                         const bool nil = (((s < 4u ? nb0 : nb1) >> bs) & 0x10u) != 0u;
-                        const uint64_t x = wq[s];
+                        const uint64_t x = wt(s);
                         Svp += (!pc && !nil) ? x : 0ull;
                         Snp += (!pc && nil) ? x : 0ull;
                         Svc += (pc && !nil) ? x : 0ull;
                         Snc += (pc && nil) ? x : 0ull;
                         if (s == 3u) { P3vp = Svp; P3np = Snp; P3vc = Svc; P3nc = Snc; }
                     }
-                    const uint64_t Tvp = split ? Svp - P3vp : Svp, Tnp = split ? Snp - P3np : Snp;
-                    const uint64_t Tvc = split ? Svc - P3vc : Svc, Tnc = split ? Snc - P3nc : Snc;
+                    const uint64_t Tvp = splitx ? Svp - P3vp : Svp, Tnp = splitx ? Snp - P3np : Snp;
+                    const uint64_t Tvc = splitx ? Svc - P3vc : Svc, Tnc = splitx ? Snc - P3nc : Snc;
                     const uint64_t Ivp = scan(Tvp), Inp = scan(Tnp), Ivc = scan(Tvc), Inc = scan(Tnc);
                     const uint64_t Evp = Ivp - Tvp, Enp = Inp - Tnp, Evc = Ivc - Tvc, Enc = Inc - Tnc;
-                    const uint64_t* const A64 = reinterpret_cast<const uint64_t*>(A); /* vp vc np nc */
+                    /* carried executors (u64 rows: vw[2R] then vn[2R], keys 2r prevote, 2r + 1
+                     * precommit): uniform reads per pass, or (ONE) each unit's own round's */
+                    const uint64_t* const A64 = reinterpret_cast<const uint64_t*>(A);
+                    const uint32_t K = 2u * r;
                     uint64_t cvp = 0, cnp = 0, cvc = 0, cnc = 0;
-                    if (cont0) {
-                        cvp = A64[0];
-                        cvc = A64[1];
-                        cnp = A64[2];
-                        cnc = A64[3];
+                    if (ONE) {
+                        if (cA) {
+                            cvp = A64[2u * uA];
+                            cvc = A64[2u * uA + 1u];
+                            cnp = A64[2u * R + 2u * uA];
+                            cnc = A64[2u * R + 2u * uA + 1u];
+                        }
+                    } else if (cont0) {
+                        cvp = A64[K];
+                        cvc = A64[K + 1u];
+                        cnp = A64[2u * R + K];
+                        cnc = A64[2u * R + K + 1u];
                     }
                     uint64_t bvp = Evp, bnp = Enp, bvc = Evc, bnc = Enc;
-                    if (multi) {
-                        bvp -= shfl(Evp, sA);
-                        bnp -= shfl(Enp, sA);
-                        bvc -= shfl(Evc, sA);
-                        bnc -= shfl(Enc, sA);
+                    if (multix) {
+                        bvp -= shfl(Evp, sAx);
+                        bnp -= shfl(Enp, sAx);
+                        bvc -= shfl(Evc, sAx);
+                        bnc -= shfl(Enc, sAx);
                     }
-                    if (cA) {
+                    if (ONE || cA) {
                         bvp += cvp;
                         bnp += cnp;
                         bvc += cvc;
                         bnc += cnc;
                     }
-                    /* pass 2: each vote's own running sums as absolute u64 values (the base
-                     * before the lane plus the lane prefix; unit B of a split lane starts its
-                     * instance from zero) against q2 — no per-vote thresholds held */
+                    /* unit B of a split lane starts its segment from its own carry-in (a new
+                     * instance, or a new run: the run's carried row) */
+                    uint64_t dvp = 0, dnp = 0, dvc = 0, dnc = 0;
+                    if (ONE && multix && splitx && cont0 && kB == k0) {
+                        dvp = A64[2u * uB];
+                        dvc = A64[2u * uB + 1u];
+                        dnp = A64[2u * R + 2u * uB];
+                        dnc = A64[2u * R + 2u * uB + 1u];
+                    }
                     const uint64_t qA = u64of(recA.x, itab[RW * kA + R_Q2H]);
-                    const uint64_t qB = (multi && split) ? u64of(recB.x, itab[RW * kB + R_Q2H]) : qA;
+                    const uint64_t qB = (multix && splitx) ? u64of(recB.x, itab[RW * kB + R_Q2H]) : qA;
                     uint32_t l0 = 0, l1 = 0;
                     uint64_t Avp = bvp, Anp = bnp, Avc = bvc, Anc = bnc, q = qA;
 #pragma unroll
                     for (uint32_t s = 0; s < LV; ++s) {
-                        if (s == 4u && multi && split) {
-                            Avp = Anp = Avc = Anc = 0ull;
+                        if (s == 4u && multix && splitx) {
+                            Avp = dvp;
+                            Anp = dnp;
+                            Avc = dvc;
+                            Anc = dnc;
                             q = qB;
                         }
                         const uint32_t bs = 8u * (s & 3u);
                         const bool pc = (((s < 4u ? t8[0] : t8[1]) >> bs) & 1u) != 0u;
                         const bool nil = (((s < 4u ? nb0 : nb1) >> bs) & 0x10u) != 0u;
-                        const uint64_t x = wq[s];
+                        const uint64_t x = wt(s);
                         Avp += (!pc && !nil) ? x : 0ull;
                         Anp += (!pc && nil) ? x : 0ull;
                         Avc += (pc && !nil) ? x : 0ull;
@@ -935,30 +969,71 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                         else l1 |= l << bs;
                     }
                     if (SM) { /* crossed before the unit: the sums before it already past q2 */
-                        cf |= (bvp > qA || bnp > qA) ? 1u : 0u;
+                        const bool eA_ = R1 || (ONE ? uA : r) == recA.w, eB_ = R1 || (ONE ? uB : r) == recB.w;
+                        cf |= (eA_ && (bvp > qA || bnp > qA)) ? 1u : 0u;
                         cf |= bvc > qA ? 2u : 0u;
-                        if (!split) {
-                            cf |= (bvp + P3vp > qA || bnp + P3np > qA) ? 4u : 0u;
+                        if (!splitx) {
+                            cf |= (eB_ && (bvp + P3vp > qA || bnp + P3np > qA)) ? 4u : 0u;
                             cf |= bvc + P3vc > qA ? 8u : 0u;
                         }
                     }
-                    lv0 |= l0;
-                    lv1 |= l1;
-                    if (lastc) { /* the last segment's executors after the chunk (lane 0 writes) */
-                        const uint64_t nvp = rdl(Ivp, 63u) - rdl(Evp, slast) + (cL ? cvp : 0ull);
-                        const uint64_t nnp = rdl(Inp, 63u) - rdl(Enp, slast) + (cL ? cnp : 0ull);
-                        const uint64_t nvc = rdl(Ivc, 63u) - rdl(Evc, slast) + (cL ? cvc : 0ull);
-                        const uint64_t nnc = rdl(Inc, 63u) - rdl(Enc, slast) + (cL ? cnc : 0ull);
-                        if (lane == 0u) {
-                            uint64_t* const B64 = reinterpret_cast<uint64_t*>(B);
-                            B64[0] = nvp;
-                            B64[1] = nvc;
-                            B64[2] = nnp;
-                            B64[3] = nnc;
+                    lv0 |= l0 & rm0;
+                    lv1 |= l1 & rm1;
+                    if (lastc) {
+                        uint64_t* const B64 = reinterpret_cast<uint64_t*>(B);
+                        if (ONE) { /* every run of the last instance: its executors at the run's end */
+                            const bool endA = splitx, endB = lane == 63u || ((SAr >> (lane + 1u)) & 1ull) != 0ull;
+                            if (endA && kA == klast) {
+                                B64[2u * uA] = bvp + P3vp;
+                                B64[2u * uA + 1u] = bvc + P3vc;
+                                B64[2u * R + 2u * uA] = bnp + P3np;
+                                B64[2u * R + 2u * uA + 1u] = bnc + P3nc;
+                            }
+                            if (endB && kB == klast) {
+                                B64[2u * uB] = splitx ? dvp + Tvp : bvp + Svp;
+                                B64[2u * uB + 1u] = splitx ? dvc + Tvc : bvc + Svc;
+                                B64[2u * R + 2u * uB] = splitx ? dnp + Tnp : bnp + Snp;
+                                B64[2u * R + 2u * uB + 1u] = splitx ? dnc + Tnc : bnc + Snc;
+                            }
+                        } else { /* the last segment's executors after the chunk (lane 0 writes) */
+                            const uint64_t nvp = rdl(Ivp, 63u) - rdl(Evp, slast) + (cL ? cvp : 0ull);
+                            const uint64_t nnp = rdl(Inp, 63u) - rdl(Enp, slast) + (cL ? cnp : 0ull);
+                            const uint64_t nvc = rdl(Ivc, 63u) - rdl(Evc, slast) + (cL ? cvc : 0ull);
+                            const uint64_t nnc = rdl(Inc, 63u) - rdl(Enc, slast) + (cL ? cnc : 0ull);
+                            if (lane == 0u) {
+                                B64[K] = nvp;
+                                B64[K + 1u] = nvc;
+                                B64[2u * R + K] = nnp;
+                                B64[2u * R + K + 1u] = nnc;
+                            }
                         }
                     }
                     __builtin_amdgcn_wave_barrier();
-                } else if (R1) {
+                };
+                auto passes = [&](auto pf) {
+                    if (R1) {
+                        pf(std::false_type{}, 0u);
+                    } else if (runs) {
+                        pf(std::true_type{}, 0u);
+                    } else {
+                        /* the rounds present among the votes that checked in, one pass each */
+                        uint32_t rb = 0;
+#pragma unroll
+                        for (uint32_t s = 0; s < LV; ++s) {
+                            const uint32_t ok = ((s < 4u ? okb0 : okb1) >> (8u * (s & 3u))) & 1u;
+                            rb |= ok << ((r8[s >> 2] >> (8u * (s & 3u))) & 15u);
+                        }
+                        uint32_t rset = wave_or(rb);
+                        while (rset) {
+                            const uint32_t r = (uint32_t)__builtin_ctz(rset);
+                            rset &= rset - 1u;
+                            pf(std::false_type{}, r);
+                        }
+                    }
+                };
+                if constexpr (W64) {
+                    passes(pass64);
+                } else if (R1) { /* (the u32 chain spelled out: the same code as before W64 took R > 1) */
                     pass(std::false_type{}, 0u);
                 } else if (runs) {
                     pass(std::true_type{}, 0u);
@@ -1222,10 +1297,12 @@ static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStrea
 
 bool agnes_flow_supported(const agnes_tally_args* a) {
     /* rounds 0..14 in the byte checks; the per-wave LDS fits the waves a CU holds (16
-     * without the State machine, 12 with it: its VGPRs allow 3 waves per SIMD) */
+     * without the State machine, 12 with it: its VGPRs allow 3 waves per SIMD; the u64
+     * kernel's allow 2) */
     const bool sm = (a->flags & AGNES_FLAG_STATE_MACHINE) != 0 && a->states != nullptr;
+    const uint32_t waves = a->w64 ? 8u : (sm ? 12u : 16u);
     return a->max_rounds <= 15u &&
-           agnes::flow::lds_bytes(sm, a->max_rounds, a->ev_counts != nullptr, a->w64 != 0u) * (sm ? 12u : 16u) <= 160u * 1024u;
+           agnes::flow::lds_bytes(sm, a->max_rounds, a->ev_counts != nullptr, a->w64 != 0u) * waves <= 160u * 1024u;
 }
 
 bool agnes_flow_counts_events(uint32_t flags, uint32_t max_rounds) {
@@ -1235,9 +1312,11 @@ bool agnes_flow_counts_events(uint32_t flags, uint32_t max_rounds) {
 
 hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t st) {
     const bool sm = (a->flags & AGNES_FLAG_STATE_MACHINE) != 0 && a->states != nullptr;
-    if (a->w64) { /* the u64 domain: one round, no record counts (agnes_sweep_supported) */
-        if (a->max_rounds != 1u || a->ev_counts) return hipErrorInvalidValue;
-        return sm ? launch_flow_k<true, true, false, true>(a, num_cus, st) : launch_flow_k<false, true, false, true>(a, num_cus, st);
+    if (a->w64) { /* the u64 domain: no record counts (agnes_sweep_supported) */
+        if (a->ev_counts) return hipErrorInvalidValue;
+        if (a->max_rounds == 1u)
+            return sm ? launch_flow_k<true, true, false, true>(a, num_cus, st) : launch_flow_k<false, true, false, true>(a, num_cus, st);
+        return sm ? launch_flow_k<true, false, false, true>(a, num_cus, st) : launch_flow_k<false, false, false, true>(a, num_cus, st);
     }
     if (a->ev_counts) {
         if (a->max_rounds == 1u)

@@ -97,9 +97,11 @@ struct agnes_multi {
     uint32_t n_vals = 0;
     uint32_t xmode = AGNES_MULTI_EXCHANGE_AUTO;
     std::vector<ncclComm_t> comms; /* one rank per device (RCCL exchanges), created on first use */
-    bool comms_dead = false;       /* a collective failed on some rank: aborted, rebuilt on the next call */
-    std::atomic<bool> rccl_checked{false};     /* the first RCCL all-gather was compared with the host exchange */
-    std::atomic<bool> rccl_bad{false};         /* ... and differed: the host exchange from then on */
+    std::atomic<bool> comms_dead{false}; /* a collective failed on some rank: aborted (handles null), rebuilt next call */
+    std::atomic<uint32_t> rccl_checked{0u}; /* bit op: the first RCCL collective of that kind was checked */
+    std::atomic<bool> rccl_bad{false};      /* ... and differed: the host exchange from then on */
+    std::atomic<bool> used_rccl{false};     /* the last call's exchanges went through RCCL */
+    uint32_t test_corrupt = 0;              /* test hook (agnes_multi_test_corrupt): bit op flips a result */
     std::vector<int> xerr;         /* per device: its status entering an RCCL exchange (host agreement) */
     agnes::multi::Barrier bar;
     std::vector<unsigned char*> stage; /* pinned host staging of the host exchange, per device */
@@ -269,36 +271,68 @@ bool agree_ok(agnes_multi* m, uint32_t d, int mine) {
     return ok;
 }
 
-/* The first RCCL all-gather of a handle is checked against the same gather through
- * pinned host memory (the multi-device RCCL path has not run on hardware in this
- * repository's tests, which share one device): every thread compares its received
- * rows with every device's staged send buffer.  A mismatch anywhere makes every
- * thread take the host rows and the handle use the host exchange from then on. */
-int check_gather(agnes_multi* m, uint32_t d, const int64_t* send, int64_t* recv, uint64_t count) {
-    Dev& dv = m->dev[d];
+/* The host exchange's result for op over every device's staged send buffer (8-B
+ * elements; X_GATHER: the D buffers in device order). */
+void host_result(const agnes_multi* m, XOp op, uint64_t count, uint64_t* out) {
     const uint32_t D = (uint32_t)m->dev.size();
-    const uint64_t bytes = 8u * count;
-    int rc = stage_grow(m, d, bytes);
-    std::vector<int64_t> got((size_t)D * count);
-    if (rc == AGNES_OK && hipMemcpyAsync(m->stage[d], send, bytes, hipMemcpyDeviceToHost, dv.st) != hipSuccess)
-        rc = AGNES_E_DEVICE;
-    if (rc == AGNES_OK && hipMemcpyAsync(got.data(), recv, D * bytes, hipMemcpyDeviceToHost, dv.st) != hipSuccess)
+    if (op == X_GATHER) {
+        for (uint32_t k = 0; k < D; ++k) std::memcpy(out + (size_t)k * count, m->stage[k], 8u * count);
+        return;
+    }
+    for (uint64_t e = 0; e < count; ++e) {
+        uint64_t acc = reinterpret_cast<const uint64_t*>(m->stage[0])[e];
+        for (uint32_t k = 1; k < D; ++k) {
+            const uint64_t x = reinterpret_cast<const uint64_t*>(m->stage[k])[e];
+            if (op == X_MIN_U64) acc = x < acc ? x : acc;
+            else if (op == X_MIN_I64) acc = (int64_t)x < (int64_t)acc ? x : acc;
+            else acc = (int64_t)x > (int64_t)acc ? x : acc;
+        }
+        out[e] = acc;
+    }
+}
+
+/* The first RCCL collective of each kind (the all-gather, the MIN all-reduces on u64
+ * and i64, the MAX one) of a handle is checked against the host exchange of the same
+ * data: the multi-device RCCL path has not run on hardware in this repository's tests,
+ * which share one device.  Before the collective every thread stages its send buffer
+ * in pinned memory (the all-reduces run in place); after it every thread compares its
+ * received elements with the host result.  A mismatch anywhere makes every thread take
+ * the host result, and the handle use the host exchange from then on; the fallback is
+ * reported in agnes_multi_stats.exchange (AGNES_MULTI_X_FALLBACK). */
+int stage_send(agnes_multi* m, uint32_t d, const int64_t* send, uint64_t count) {
+    Dev& dv = m->dev[d];
+    int rc = stage_grow(m, d, 8u * count);
+    if (rc == AGNES_OK && hipMemcpyAsync(m->stage[d], send, 8u * count, hipMemcpyDeviceToHost, dv.st) != hipSuccess)
         rc = AGNES_E_DEVICE;
     if (rc == AGNES_OK && hipStreamSynchronize(dv.st) != hipSuccess) rc = AGNES_E_DEVICE;
-    if (!agree_ok(m, d, rc)) return rc != AGNES_OK ? rc : AGNES_E_DEVICE; /* every stage written */
-    bool same = true;
-    for (uint32_t k = 0; k < D; ++k)
-        same = same && std::memcmp(got.data() + (size_t)k * count, m->stage[k], bytes) == 0;
-    const bool all_same = agree_ok(m, d, same ? AGNES_OK : AGNES_E_DEVICE);
-    if (!all_same) {
-        for (uint32_t k = 0; k < D && rc == AGNES_OK; ++k)
-            if (hipMemcpyAsync(recv + k * count, m->stage[k], bytes, hipMemcpyHostToDevice, dv.st) != hipSuccess)
-                rc = AGNES_E_DEVICE;
-        if (rc == AGNES_OK && hipStreamSynchronize(dv.st) != hipSuccess) rc = AGNES_E_DEVICE;
-        if (d == 0u) m->rccl_bad = true;
+    return rc;
+}
+
+int check_collective(agnes_multi* m, uint32_t d, XOp op, int64_t* recv, uint64_t count) {
+    Dev& dv = m->dev[d];
+    const uint32_t D = (uint32_t)m->dev.size();
+    const uint64_t n = op == X_GATHER ? (uint64_t)D * count : count;
+    std::vector<uint64_t> want((size_t)n), got((size_t)n);
+    int rc = AGNES_OK;
+    if (m->test_corrupt & (1u << op)) { /* test hook: one received element flipped */
+        if (hipMemsetAsync(recv, 0x5A, 1, dv.st) != hipSuccess) rc = AGNES_E_DEVICE;
     }
-    m->bar.wait(); /* the stages are free again; every thread has seen rccl_bad */
-    if (d == 0u) m->rccl_checked = true;
+    if (rc == AGNES_OK && hipMemcpyAsync(got.data(), recv, 8u * n, hipMemcpyDeviceToHost, dv.st) != hipSuccess)
+        rc = AGNES_E_DEVICE;
+    if (rc == AGNES_OK && hipStreamSynchronize(dv.st) != hipSuccess) rc = AGNES_E_DEVICE;
+    host_result(m, op, count, want.data());
+    const bool same = rc == AGNES_OK && std::memcmp(want.data(), got.data(), 8u * n) == 0;
+    const bool all_same = agree_ok(m, d, same ? AGNES_OK : AGNES_E_DEVICE);
+    if (!all_same && rc == AGNES_OK) {
+        if (hipMemcpyAsync(recv, want.data(), 8u * n, hipMemcpyHostToDevice, dv.st) != hipSuccess) rc = AGNES_E_DEVICE;
+        if (rc == AGNES_OK && hipStreamSynchronize(dv.st) != hipSuccess) rc = AGNES_E_DEVICE;
+    }
+    m->bar.wait(); /* every thread has compared: the stages are free again */
+    if (d == 0u) {
+        if (!all_same) m->rccl_bad = true;
+        m->rccl_checked |= 1u << op;
+    }
+    m->bar.wait(); /* every thread sees the same flags from here on */
     return rc;
 }
 
@@ -306,6 +340,8 @@ int exchange(agnes_multi* m, uint32_t d, XOp op, const int64_t* send, int64_t* r
     Dev& dv = m->dev[d];
     const uint32_t D = (uint32_t)m->dev.size();
     if (!m->comms.empty()) {
+        const bool check = !(m->rccl_checked & (1u << op));
+        if (check && mine == AGNES_OK) mine = stage_send(m, d, send, count);
         if (!agree_ok(m, d, mine)) return mine != AGNES_OK ? mine : AGNES_E_DEVICE;
         ncclResult_t r;
         if (op == X_GATHER)
@@ -315,11 +351,15 @@ int exchange(agnes_multi* m, uint32_t d, XOp op, const int64_t* send, int64_t* r
                               op == X_MAX_I64 ? ncclMax : ncclMin, m->comms[d], dv.st);
         const int rc = r == ncclSuccess ? AGNES_OK : AGNES_E_DEVICE;
         if (!agree_ok(m, d, rc)) {
+            /* every rank aborts its own communicator; the handles are dropped (the next
+             * call rebuilds them) so that nothing destroys an aborted one again */
             (void)ncclCommAbort(m->comms[d]);
-            m->comms_dead = true;
+            m->comms[d] = nullptr;
+            if (d == 0u) m->comms_dead = true;
             return AGNES_E_DEVICE;
         }
-        if (op == X_GATHER && !m->rccl_checked) return check_gather(m, d, send, recv, count);
+        m->used_rccl = true;
+        if (check) return check_collective(m, d, op, recv, count);
         return AGNES_OK;
     }
     const uint64_t bytes = 8u * count;
@@ -529,6 +569,8 @@ int run_one(agnes_multi* m, uint32_t d, const agnes_config* cfg, const agnes_vot
         out->device = (uint32_t)dv.device;
         out->i0 = 0;
         out->i1 = 1;
+        out->exchange = (m->used_rccl ? AGNES_MULTI_X_RCCL : 0u) | (m->rccl_bad ? AGNES_MULTI_X_FALLBACK : 0u) |
+                        (D > 1u && !m->used_rccl ? AGNES_MULTI_X_HOST : 0u);
         out->n_votes = nv;
         out->n_invalid = bad;
         out->h2d_ms = h2d;
@@ -551,8 +593,10 @@ int ensure_exchange(agnes_multi* m) {
     }
     m->bar.n = D;
     m->xerr.assign(D, AGNES_OK);
+    m->used_rccl = false;
     if (m->comms_dead) { /* a collective failed in an earlier call: its communicators were aborted */
-        for (ncclComm_t c : m->comms) (void)ncclCommDestroy(c);
+        for (ncclComm_t c : m->comms)
+            if (c) (void)ncclCommDestroy(c);
         m->comms.clear();
         m->comms_dead = false;
     }
@@ -563,7 +607,8 @@ int ensure_exchange(agnes_multi* m) {
     const bool want = !m->rccl_bad && (m->xmode == AGNES_MULTI_EXCHANGE_RCCL ||
                                        (m->xmode == AGNES_MULTI_EXCHANGE_AUTO && distinct && D > 1));
     if (!want) {
-        for (ncclComm_t c : m->comms) (void)ncclCommDestroy(c);
+        for (ncclComm_t c : m->comms)
+            if (c) (void)ncclCommDestroy(c);
         m->comms.clear();
         return AGNES_OK;
     }
@@ -630,7 +675,8 @@ void agnes_multi_destroy(agnes_multi* m) {
         }
         if (d.ctx) agnes_ctx_destroy(d.ctx);
     }
-    for (ncclComm_t c : m->comms) (void)ncclCommDestroy(c);
+    for (ncclComm_t c : m->comms)
+        if (c) (void)ncclCommDestroy(c);
     for (unsigned char* p : m->stage)
         if (p) (void)hipHostFree(p);
     delete m;
@@ -690,6 +736,13 @@ int agnes_multi_exchange(agnes_multi* m, uint32_t mode) {
     if (!m || mode > AGNES_MULTI_EXCHANGE_RCCL) return AGNES_E_INVALID;
     m->xmode = mode;
     return ensure_exchange(m);
+}
+
+int agnes_multi_test_corrupt(agnes_multi* m, uint32_t ops) {
+    if (!m || ops > 15u) return AGNES_E_INVALID;
+    m->test_corrupt = ops;
+    m->rccl_checked = 0u; /* the next collective of each kind is checked again */
+    return AGNES_OK;
 }
 
 int agnes_multi_tally_one(agnes_multi* m, const agnes_config* cfg, const agnes_vote_batch* hb, uint8_t* codes,

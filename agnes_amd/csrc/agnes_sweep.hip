@@ -637,9 +637,9 @@ __global__ __launch_bounds__(256) void sweep(agnes_tally_args a, uint32_t lds_pe
 /* launcher                                                            */
 
 bool agnes_sweep_supported(const agnes_tally_args* a) {
-    /* keys round * 2 + type < 31: one bit each in a u32; the u64 domain (flow<W64>) for
-     * one round without record counts only (its walk list goes to the i64 LIST kernel) */
-    return a->max_rounds <= 15u && (!a->w64 || (a->max_rounds == 1u && a->ev_counts == nullptr));
+    /* keys round * 2 + type < 31: one bit each in a u32; the u64 domain (flow<W64>)
+     * without record counts (its walk list goes to the i64 LIST kernel) */
+    return a->max_rounds <= 15u && (!a->w64 || a->ev_counts == nullptr);
 }
 
 template <bool SM>

@@ -78,6 +78,7 @@ def load():
         "agnes_multi_tally_one": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, C.c_uint32, P],
                                   C.c_int),
         "agnes_multi_exchange": ([P, C.c_uint32], C.c_int),
+        "agnes_multi_test_corrupt": ([P, C.c_uint32], C.c_int),
         "agnes_multi_edge_offsets": ([P, C.POINTER(abi.Config), P], C.c_int),
         "agnes_multi_edges": ([P, C.POINTER(abi.Config), P, P], C.c_int),
         "agnes_valset_build": ([P, P, C.c_uint32, P, P, C.c_uint64, C.c_uint32, P, P, P, P, P,

@@ -66,6 +66,12 @@ class MultiEngine:
         """abi.MULTI_EXCHANGE_AUTO / _HOST / _RCCL for tally_one's exchanges."""
         check(self.lib.agnes_multi_exchange(self.h, mode), "agnes_multi_exchange")
 
+    def test_corrupt(self, ops: int):
+        """Test hook: bit k flips the first received byte of the next checked RCCL
+        collective of kind k (0 MIN u64, 1 MIN i64, 2 MAX i64, 3 all-gather), so the
+        self-check's fallback (stats['exchange'] & abi.MULTI_X_FALLBACK) can be tested."""
+        check(self.lib.agnes_multi_test_corrupt(self.h, ops), "agnes_multi_test_corrupt")
+
     def tally_one(self, cfg: abi.Config, hb, state: Optional[np.ndarray] = None, segments: int = 0):
         """C5: hb holds ONE instance (host columns).  Returns (codes u8, state (1
         record) or None, counts abi.VOTE_COUNT_DTYPE [2 * max_rounds], stats)."""

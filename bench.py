@@ -103,6 +103,13 @@ WORKLOADS = {
                          nil_permille=200),
                 power=(abi.POWER_UNIFORM, 1 << 28, 1 << 34, 1), mode=abi.MODE_REFERENCE,
                 flags=abi.FLAG_STATE_MACHINE, max_rounds=1, scaling="weak"),
+    # one C3 rank's shard with i64 stakes: powers U[2^28, 2^34] over 1024 sets (set totals
+    # > 2^32), 1..4 rounds (round_votes.rs:9,16-18,31-33; validators.rs:7): flow<W64> runs mode
+    "c3w": dict(desc="C3 8-GPU shard with i64 stakes: 125k instances x 150 validators x 1..4 rounds, "
+                     "30% nil, powers U[2^28, 2^34] over 1024 sets (set totals > 2^32)",
+                gen=dict(n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300),
+                power=(abi.POWER_UNIFORM, 1 << 28, 1 << 34, 1024), mode=abi.MODE_REFERENCE,
+                flags=abi.FLAG_STATE_MACHINE, max_rounds=4, scaling="weak"),
     "c4": dict(desc="C4: C3 shape per rank (125k instances), Zipf power, 10% dup + 10% "
                     "equivocation + 5% next-round votes, DEDUP + RoundSkip",
                gen=dict(n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4,

@@ -574,7 +574,7 @@ int agnes_wire_ingest(agnes_ctx* ctx, const agnes_wire_vote* records, uint64_t n
 typedef struct agnes_multi agnes_multi;
 typedef struct agnes_multi_stats {
     uint32_t device, i0, i1; /* the range [i0, i1) this device tallied */
-    uint32_t pad;
+    uint32_t exchange;       /* agnes_multi_tally_one: AGNES_MULTI_X_* bits of how it exchanged */
     uint64_t n_votes, n_invalid;
     double h2d_ms, tally_ms, d2h_ms; /* host wall-clock of the three phases */
 } agnes_multi_stats;
@@ -613,6 +613,18 @@ int agnes_multi_tally_one(agnes_multi* m, const agnes_config* cfg, const agnes_v
 #define AGNES_MULTI_EXCHANGE_HOST 1u
 #define AGNES_MULTI_EXCHANGE_RCCL 2u
 int agnes_multi_exchange(agnes_multi* m, uint32_t mode);
+/* agnes_multi_stats.exchange: RCCL carried the call's collectives; FALLBACK: the
+ * handle's RCCL self-check failed (the first collective of each kind -- all-gather,
+ * MIN on u64 / i64, MAX -- is compared with the host exchange of the same data; on a
+ * mismatch the call's results come from the host exchange and the handle uses it from
+ * then on); HOST: pinned host memory carried them. */
+#define AGNES_MULTI_X_RCCL 1u
+#define AGNES_MULTI_X_FALLBACK 2u
+#define AGNES_MULTI_X_HOST 4u
+/* Test hook (not for production): bit k of ops flips the first received byte of the
+ * next checked RCCL collective of kind k (0 MIN u64, 1 MIN i64, 2 MAX i64, 3 all-gather)
+ * before the self-check, so tests can drive the fallback path. */
+int agnes_multi_test_corrupt(agnes_multi* m, uint32_t ops);
 
 /* ---------------------------------------------------------------------------
  * Edge-triggered summary of a coded batch.

@@ -7,6 +7,7 @@ between host and device.
   C2  1M instances x 100 validators x 1 round (the bench's c2 batch), State machine
   C2w the same with i64 stakes U[2^28, 2^34] (the bench's c2w batch, u64 sums)
   C3  a 125k-instance shard of 1M x 150 validators x 1..4 rounds, 1024 power sets
+  C3w the same with i64 stakes U[2^28, 2^34] (the bench's c3w batch, flow<W64> runs mode)
   C4  125k instances, Zipf power, 10 % duplicates + 10 % equivocations + 5 %
       next-round votes, DEDUP + RoundSkip + State machine
   C5  one instance x 1M validators (Zipf), REFERENCE and DEDUP (10 % + 10 %),
@@ -87,6 +88,17 @@ def test_full_c3_shard(eng):
     p = abi.gen_params(seed=0xA6E5, n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4,
                        nil_permille=300)
     power = ol.gen_power(0xA6E5, 1024, 150, abi.POWER_UNIFORM, 1, 1000)
+    _, st = _compare(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 4), p, power, 1024)
+    assert st["decided"].sum() > 0
+
+
+def test_full_c3w_shard(eng):
+    """The bench's c3w batch: a 125k-instance C3 shard with i64 stakes U[2^28, 2^34] over
+    1024 sets (set totals > 2^32), 1..4 rounds: flow<W64> in runs mode (round 5)."""
+    p = abi.gen_params(seed=0xA6E5, n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4,
+                       nil_permille=300)
+    power = ol.gen_power(0xA6E5, 1024, 150, abi.POWER_UNIFORM, 1 << 28, 1 << 34)
+    assert power.sum(axis=1).min() > (1 << 32)
     _, st = _compare(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 4), p, power, 1024)
     assert st["decided"].sum() > 0
 

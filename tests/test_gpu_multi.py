@@ -129,6 +129,39 @@ def test_multi_tally_one_rccl_one_rank():
         m.close()
 
 
+@pytest.mark.parametrize("ops", [1, 2, 4, 8, 15])
+def test_multi_rccl_selfcheck_fallback(ops):
+    """The RCCL self-check: the first collective of each kind (MIN u64 = the DEDUP
+    first-vote table, MIN i64 = P1 / C, MAX i64 = valid / decision round, all-gather =
+    the slice totals) is compared with the host exchange of the same data.  A test
+    hook flips a received byte of the chosen kinds: the call must still be exact (the
+    host result replaces RCCL's), report AGNES_MULTI_X_FALLBACK, and the handle's next
+    call must run on the host exchange."""
+    hb = _c5_batch(7, 4096, True)
+    power = ol.gen_power(7, 1, 4096, abi.POWER_ZIPF, 1, 1_000_000)
+    cfg = abi.config(abi.MODE_DEDUP, abi.FLAG_STATE_MACHINE, 1)
+    st0 = abi.new_states(1, 1, abi.STEP_PREVOTE)
+    want, want_st, _ = ol.tally(cfg, hb, power, None, st0)
+    m = MultiEngine([0])
+    try:
+        m.exchange(abi.MULTI_EXCHANGE_RCCL)
+        m.upload_power(power)
+        codes, st, _, stats = m.tally_one(cfg, hb, st0, segments=33)  # clean: RCCL, checked, no fallback
+        assert np.array_equal(codes, want) and st.tobytes() == want_st.tobytes()
+        assert int(stats["exchange"][0]) == abi.MULTI_X_RCCL
+        m.test_corrupt(ops)
+        codes, st, _, stats = m.tally_one(cfg, hb, st0, segments=33)
+        assert np.array_equal(codes, want) and st.tobytes() == want_st.tobytes()
+        assert int(stats["exchange"][0]) & abi.MULTI_X_FALLBACK
+        m.test_corrupt(0)
+        codes, st, _, stats = m.tally_one(cfg, hb, st0, segments=33)  # the handle left RCCL
+        assert np.array_equal(codes, want) and st.tobytes() == want_st.tobytes()
+        assert not int(stats["exchange"][0]) & abi.MULTI_X_RCCL
+        assert int(stats["exchange"][0]) & abi.MULTI_X_FALLBACK
+    finally:
+        m.close()
+
+
 @pytest.mark.parametrize("n_dev", [1, 3])
 def test_multi_edges_gathered(n_dev):
     """The edge summary of the last agnes_multi_tally, gathered from every range in

@@ -225,6 +225,16 @@ CONFIGS = {
                   (abi.POWER_ZIPF, 1 << 31, 1 << 36, 3), (abi.MODE_REFERENCE, 0, 1)),
     "w64_deferred": (dict(n_instances=600, n_vals=300, rounds_min=1, rounds_max=2, nil_permille=250),
                      (abi.POWER_UNIFORM, 1 << 50, 1 << 52, 2), (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 2)),
+    # flow<W64> over several rounds (round 5): runs mode (c3w_small), the per-round passes
+    # when an instance revisits a round inside a chunk (w64_revisit: next-round votes), and
+    # the plain tally without the State machine
+    "c3w_small": (dict(n_instances=3000, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300),
+                  (abi.POWER_UNIFORM, 1 << 28, 1 << 34, 1024), (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 4)),
+    "c3w_plain": (dict(n_instances=2500, n_vals=120, rounds_min=2, rounds_max=4, nil_permille=350),
+                  (abi.POWER_ZIPF, 1 << 31, 1 << 36, 3), (abi.MODE_REFERENCE, 0, 4)),
+    "w64_revisit": (dict(n_instances=2000, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300,
+                         dup_permille=100, equiv_permille=100, higher_permille=50),
+                    (abi.POWER_UNIFORM, 1 << 28, 1 << 34, 5), (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 5)),
     "many_rounds": (dict(n_instances=200, n_vals=20, rounds_min=30, rounds_max=60,
                          nil_permille=300, higher_permille=100),
                     (abi.POWER_UNIFORM, 1, 100, 5),
@@ -521,7 +531,8 @@ def test_c3_shard_parity(eng):
 
 
 @pytest.mark.parametrize("route", list(ROUTES))
-@pytest.mark.parametrize("name", ["c2_sm", "c3_small", "c4_small", "c2w_small", "w64_dedup_skip"])
+@pytest.mark.parametrize("name", ["c2_sm", "c3_small", "c4_small", "c2w_small", "w64_dedup_skip", "c3w_small",
+                                  "w64_revisit"])
 def test_routes_generated(eng, route, name):
     p, hb, power, cfg = _make(name)
     cfg = abi.config(cfg.mode, cfg.flags | ROUTES[route], cfg.max_rounds)

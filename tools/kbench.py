@@ -42,6 +42,26 @@ VARIANTS = {
     "c4_dedup_only": (dict(n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4,
                            nil_permille=300, dup_permille=100, equiv_permille=100),
                       (abi.POWER_ZIPF, 1, 1_000_000, 1024), abi.MODE_DEDUP, 0, 5),
+    # round-5 C4 ceiling: the C4 stream (dup/equiv/next-round votes) tallied in REFERENCE mode
+    # without RoundSkip, powers inside flow's domain (maxpow < 4096)
+    "c4_ref_u": (dict(n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4,
+                      nil_permille=300, dup_permille=100, equiv_permille=100, higher_permille=50),
+                 (abi.POWER_UNIFORM, 1, 1000, 1024), abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 5),
+    "c4_ref_u_noh": (dict(n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4,
+                          nil_permille=300, dup_permille=100, equiv_permille=100),
+                     (abi.POWER_UNIFORM, 1, 1000, 1024), abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 5),
+    "c4_ref_z": (dict(n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4,
+                      nil_permille=300, dup_permille=100, equiv_permille=100, higher_permille=50),
+                 (abi.POWER_ZIPF, 1, 1_000_000, 1024), abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 5),
+    "c4_dedup_sm": (dict(n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4,
+                         nil_permille=300, dup_permille=100, equiv_permille=100, higher_permille=50),
+                    (abi.POWER_ZIPF, 1, 1_000_000, 1024), abi.MODE_DEDUP, abi.FLAG_STATE_MACHINE, 5),
+    "c4_skip_sm": (dict(n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4,
+                        nil_permille=300, dup_permille=100, equiv_permille=100, higher_permille=50),
+                   (abi.POWER_ZIPF, 1, 1_000_000, 1024), abi.MODE_REFERENCE,
+                   abi.FLAG_STATE_MACHINE | abi.FLAG_ROUND_SKIP, 5),
+    "c3shard": (dict(n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300),
+                (abi.POWER_UNIFORM, 1, 1000, 1024), abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 4),
 }
 
 
