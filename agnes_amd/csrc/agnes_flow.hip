@@ -47,6 +47,16 @@ namespace flow {
 using namespace agnes::fast;
 
 constexpr uint32_t LV = 8u, CH = 64u * LV; /* votes per lane, per chunk */
+
+/* Diagnostics build only (AGNES_FLOW_DIAG, tools/flowdiag.py): per wave, 64 u64 words --
+ * [0] s_memrealtime at the start (100 MHz), [1] at the end, [2] batches, [3] chunks, then
+ * per batch k < 30: [4 + 2k] its start time, [5 + 2k] instances | chunks << 16 | votes << 32. */
+#ifdef AGNES_FLOW_DIAG
+__device__ unsigned long long* flow_diag_buf;
+#define FDIAG(...) __VA_ARGS__
+#else
+#define FDIAG(...)
+#endif
 /* DMA slot: each column of the chunk as a contiguous image */
 constexpr uint32_t F_INST = 0, F_VALUE = 2048, F_VAL = 4096, F_ROUND = 6144, F_TYPE = 6656, F_BYTES = 7168;
 /* instances per batch: header offsets in lanes 0..FB, per-instance data in lane k.  A
@@ -57,6 +67,12 @@ constexpr uint32_t F_INST = 0, F_VALUE = 2048, F_VAL = 4096, F_ROUND = 6144, F_T
 #endif
 #ifndef AGNES_FLOW_BATCHES_PER_WAVE
 #define AGNES_FLOW_BATCHES_PER_WAVE 4 /* batches per wave the batch size leaves (0: always FB); c3shard A/B 4 vs FB: flow 0.362 vs 0.444 ms */
+#endif
+#ifndef AGNES_FLOW_TAIL_VOTES
+#define AGNES_FLOW_TAIL_VOTES 1024 /* votes per batch of the queue's tail (0: the SMALLB tail) */
+#endif
+#ifndef AGNES_FLOW_TAIL_PER_WAVE
+#define AGNES_FLOW_TAIL_PER_WAVE 2
 #endif
 #ifndef AGNES_FLOW_SMALLB
 #define AGNES_FLOW_SMALLB 4
@@ -252,8 +268,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
     /* batch size: FB, or (launcher) fewer for a batch too small to give every wave
      * several batches -- the makespan is a wave's last batch */
     const uint32_t fb = a.batch && a.batch < FB ? a.batch : FB;
-    const uint32_t sb_ = SMALLB < fb ? SMALLB : fb;
-    const uint64_t NB = (uint64_t)(n / fb) * (AGNES_FLOW_TAIL_DIV - 1u) / AGNES_FLOW_TAIL_DIV;
+    /* the queue's tail: the last a.tail_n instances in batches of a.tail_batch (the
+     * launcher sizes them to about AGNES_FLOW_TAIL_VOTES votes, a couple per wave, so
+     * the waves of a counter finish within a small batch of each other), or (0) the
+     * last 1/AGNES_FLOW_TAIL_DIV in SMALLB batches */
+    const uint32_t sb_ = a.tail_batch ? (a.tail_batch < fb ? a.tail_batch : fb) : (SMALLB < fb ? SMALLB : fb);
+    const uint64_t NB = a.tail_batch ? (uint64_t)(n - (a.tail_n < n ? a.tail_n : n)) / fb
+                                     : (uint64_t)(n / fb) * (AGNES_FLOW_TAIL_DIV - 1u) / AGNES_FLOW_TAIL_DIV;
     auto range_of = [&](uint32_t t, uint32_t& s0, uint32_t& e0) {
         const uint64_t b = (uint64_t)t * qn + qk;
         const uint64_t s = b < NB ? b * fb : NB * fb + (b - NB) * sb_;
@@ -414,7 +435,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
         range_of(t + 1u, N.s0, N.e0);
         if (lane == 0) tq = atomicAdd(ctr, 1u);
     }
-    if (H.s0 >= H.e0) return;
+    FDIAG(unsigned long long* const dg = flow_diag_buf + 64ull * (blockIdx.x * AGNES_WAVES_PER_BLOCK + wave);
+          uint32_t dg_b = 0, dg_c = 0;
+          if (lane == 0) dg[0] = __builtin_amdgcn_s_memrealtime();)
+    if (H.s0 >= H.e0) {
+        FDIAG(if (lane == 0) { dg[1] = __builtin_amdgcn_s_memrealtime(); dg[2] = 0; dg[3] = 0; })
+        return;
+    }
     hdr1(H);
     hdr2(H);
     hdr3(H);
@@ -423,6 +450,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
 
     for (;;) { /* batches: H current, N next */
         const uint32_t m = H.e0 - H.s0;
+        FDIAG(const uint32_t dg_c0 = dg_c; const unsigned long long dg_t = __builtin_amdgcn_s_memrealtime();)
         unsigned char* const sbh = sb + spar * (FB * 64u);
         bool smf = SM; /* the State views are not yet set up from the staged States */
         if (!H.stream) { /* not one flow stream: the walk list (agnes_sweep.hip) */
@@ -450,6 +478,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
             const uint64_t mm64 = (1ull << m) - 1ull;
 
             for (uint32_t rc = 0; rc < Lend; rc += CH) {
+                FDIAG(++dg_c;)
                 const uint64_t c = Sa + rc;
                 const uint32_t lo_r = rc == 0u ? lead : 0u; /* the chunk's active votes: lo_r .. hi_r */
                 if (pf_at != c) dma_chunk(c, lo_r, Lend - rc); /* not prefetched: a wave's first chunk */
@@ -1210,6 +1239,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                 finalize(m, H.s0, sbh);
             }
         }
+        FDIAG(if (lane == 0) {
+                  if (dg_b < 30u) {
+                      const uint64_t nvb = u64of(rdl(H.olo, m), rdl(H.ohi, m)) - u64of(rdl(H.olo, 0u), rdl(H.ohi, 0u));
+                      dg[4u + 2u * dg_b] = dg_t;
+                      dg[5u + 2u * dg_b] = (unsigned long long)m | ((unsigned long long)(dg_c - dg_c0) << 16) | (nvb << 32);
+                  }
+              }
+              ++dg_b;)
         if (N.s0 >= N.e0) break;
         if (N.stage < 3u) { /* a short batch: the rest of the header now */
             if (N.stage == 1u) hdr2(N);
@@ -1225,6 +1262,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
     flush();
     const uint32_t nb = rdl(scan(bad), 63u);
     if (lane == 0 && nb) add_invalid(a.n_invalid, (unsigned long long)nb);
+    FDIAG(if (lane == 0) {
+        dg[1] = __builtin_amdgcn_s_memrealtime();
+        dg[2] = dg_b;
+        dg[3] = dg_c;
+    })
 }
 
 } // namespace flow
@@ -1280,6 +1322,19 @@ static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStrea
         uint64_t fbx = AGNES_FLOW_BATCHES_PER_WAVE ? (uint64_t)n / (waves * AGNES_FLOW_BATCHES_PER_WAVE) : agnes::flow::FB;
         fbx = fbx < 4u ? 4u : (fbx > agnes::flow::FB ? agnes::flow::FB : fbx);
         b.batch = (uint32_t)fbx;
+        /* the tail: batches of about AGNES_FLOW_TAIL_VOTES votes, AGNES_FLOW_TAIL_PER_WAVE
+         * per wave, at most a quarter of the instances */
+        b.tail_batch = 0u;
+        b.tail_n = 0u;
+        if (AGNES_FLOW_TAIL_VOTES && a->vb.n_votes) {
+            const uint64_t avg = (a->vb.n_votes + n - 1u) / n;
+            uint64_t tb = ((uint64_t)AGNES_FLOW_TAIL_VOTES + avg - 1u) / avg;
+            tb = tb < 1u ? 1u : (tb > fbx ? fbx : tb);
+            uint64_t tn = (uint64_t)AGNES_FLOW_TAIL_PER_WAVE * waves * tb;
+            if (tn > n / 4u) tn = n / 4u;
+            b.tail_batch = (uint32_t)tb;
+            b.tail_n = (uint32_t)tn;
+        }
     }
     if (lds > 48u * 1024u) {
         hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1294,6 +1349,14 @@ static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStrea
     else hipLaunchKernelGGL((flow<false, SM, R1, EVC, W64>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
     return hipGetLastError();
 }
+
+#ifdef AGNES_FLOW_DIAG
+/* diagnostics build only: arm the per-wave record buffer (device memory, 64 u64 per wave
+ * of the grid; nullptr disarms) */
+extern "C" int agnes_flow_diag_arm(unsigned long long* dev_buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(agnes::flow::flow_diag_buf), &dev_buf, sizeof(dev_buf)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 bool agnes_flow_supported(const agnes_tally_args* a) {
     /* rounds 0..14 in the byte checks; the per-wave LDS fits the waves a CU holds (16

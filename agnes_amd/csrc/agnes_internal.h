@@ -63,6 +63,8 @@ typedef struct agnes_tally_args {
     uint32_t one_inst;    /* AGNES_FLAG_ONE_INSTANCE: every segment is a slice of instance one_id */
     uint32_t one_id;
     uint32_t batch;       /* flow: instances per work-queue batch (0: the kernel's FB) */
+    uint32_t tail_batch;  /* flow: instances per batch of the queue's tail (0: the SMALLB tail) */
+    uint32_t tail_n;      /* flow: instances in the tail (the last ones)                        */
     uint32_t w64;         /* the u64 fast domain (agnes_set_info.w64 sets outside the u32 one):
                              tally_fast with u64 sums, the apply pass tests the same deferral */
     uint64_t* ev_counts;  /* optional [n_instances]: the flow kernel writes each instance's event

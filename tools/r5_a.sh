@@ -9,3 +9,5 @@ for c in c2w c3w; do
   timeout -k 10 200 python3 bench.py --config $c --no-cpu-baseline > gpurun_out/r5/b_$c.json 2> gpurun_out/r5/b_$c.err || { tail -20 gpurun_out/r5/b_$c.err; exit 1; }
   python3 -c "import json; d=json.loads(open('gpurun_out/r5/b_$c.json').read().strip().splitlines()[-1]); print('$c', d['ms_per_step'], d['roofline'].get('frac'), d['roofline'].get('path_frac'), {k:round(v['avg_ms'],4) for k,v in d['kernels'].items()})"
 done
+timeout -k 10 300 python3 tools/flowdiag.py agnes_amd/_exp/lib_diag.so c3shard c3 c2 > gpurun_out/r5/flowdiag.jsonl 2> gpurun_out/r5/flowdiag.err || { tail -20 gpurun_out/r5/flowdiag.err; exit 1; }
+cut -c1-600 gpurun_out/r5/flowdiag.jsonl
