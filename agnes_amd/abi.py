@@ -143,6 +143,9 @@ FOLD_RESET, FOLD_APPLY, FOLD_CARRY_ZERO_NONE, FOLD_ZERO_LABELS, FOLD_TOTAL_ZERO_
 VOTE_EVENT_DTYPE = np.dtype([("vote", "<u8"), ("instance", "<u4"), ("value", "<u4"), ("round", "u1"),
                              ("kind", "u1"), ("message", "u1"), ("pad", "u1", (5,))])  # agnes_vote_event
 assert VOTE_EVENT_DTYPE.itemsize == 24
+SEG_EVENT_DTYPE = np.dtype([("vote", "<u8"), ("value", "<u4"), ("round", "u1"), ("kind", "u1"),
+                            ("message", "u1"), ("pad", "u1")])  # agnes_seg_event
+assert SEG_EVENT_DTYPE.itemsize == 16
 # agnes_multi_exchange modes (include/agnes.h)
 MULTI_EXCHANGE_AUTO, MULTI_EXCHANGE_HOST, MULTI_EXCHANGE_RCCL = 0, 1, 2
 # agnes_multi_stats.exchange bits

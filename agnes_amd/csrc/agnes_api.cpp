@@ -297,7 +297,8 @@ int64_t agnes_lds_bytes_per_wave(const agnes_config* cfg, uint32_t n_vals) {
 static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b,
                       uint8_t* codes, const agnes_state* states_in, agnes_state* states,
                       agnes_carry_rec* carry, const agnes_set_info* sets, uint32_t n_sets, uint32_t sets_dom,
-                      hipStream_t st, uint64_t* ev_counts = nullptr, bool* counted = nullptr) {
+                      hipStream_t st, uint64_t* ev_counts = nullptr, bool* counted = nullptr,
+                      void* rec_out = nullptr) {
     if (!c || !cfg_ok(cfg) || !b || !b->offsets) return AGNES_E_INVALID;
     if (b->n_votes && (!codes || !b->instance || !b->round || !b->type || !b->value ||
                        !b->validator))
@@ -381,9 +382,10 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
                           !(cfg->flags & AGNES_FLAG_ROUND_SKIP) && agnes_flow_counts_events(cfg->flags, cfg->max_rounds);
         /* DEDUP / RoundSkip on the stream kernel: it counts too (the LIST kernel's
          * instances go on the walk list, counted after their codes) */
-        const bool dfl = !wide_all && (cfg->mode == AGNES_MODE_DEDUP || (cfg->flags & AGNES_FLAG_ROUND_SKIP)) &&
+        const bool dfl = !rec_out && !wide_all && (cfg->mode == AGNES_MODE_DEDUP || (cfg->flags & AGNES_FLAG_ROUND_SKIP)) &&
                          agnes_dflow_route(&a);
         if (flow || dfl) a.ev_counts = ev_counts;
+        if (flow && rec_out) a.rec_out = rec_out; /* agnes_tally_records: the flow kernel writes them too */
         if (counted) *counted = flow || dfl;
     }
     return status_of(agnes_launch_tally(&a, cfg->mode, c->num_cus, wide_all, st));
@@ -689,6 +691,59 @@ int agnes_tally_events(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_b
         AGNES_TRY(agnes_launch_events(b, codes, cfg->max_rounds, offsets, nullptr, c->d_scan, st));
     }
     return status_of(agnes_launch_events(b, codes, cfg->max_rounds, offsets, out, nullptr, st));
+}
+
+static_assert(sizeof(agnes_seg_event) == 16, "agnes_seg_event is one 16-B record");
+
+int agnes_tally_records(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint8_t* codes,
+                        const agnes_state* states_in, agnes_state* states_out, uint64_t* counts, agnes_seg_event* out,
+                        void* stream) {
+    if (!c || !cfg || !b || (cfg->flags & (AGNES_FLAG_ONE_INSTANCE | AGNES_FLAG_WEIGHTS_CACHED | AGNES_FLAG_MASKED_REJECTED)))
+        return AGNES_E_INVALID;
+    if ((b->n_instances && !counts) || (b->n_votes && !out) || ((uintptr_t)out & 15u)) return AGNES_E_INVALID;
+    if (b->n_votes && (!b->value || ((uintptr_t)b->value & 3u))) return AGNES_E_INVALID;
+    if (cfg_ok(cfg) && cfg->max_rounds > 64u) return AGNES_E_UNSUPPORTED; /* the walk's value slots in LDS */
+    const hipStream_t st = (hipStream_t)stream;
+    bool counted = false;
+    const int rc = tally_impl(c, cfg, b, codes, states_in, states_out, nullptr, c->d_sets, c->n_sets, c->sets_dom, st,
+                              counts, &counted, out);
+    if (rc != AGNES_OK) return rc;
+    const uint32_t mult = (cfg->flags & AGNES_FLAG_ROUND_SKIP) ? 2u : 1u;
+    if (counted) /* the flow kernel wrote its batches' records; the walk list's instances here */
+        return status_of(agnes_launch_seg_walk(b, codes, cfg->max_rounds, mult, c->d_list + (size_t)c->list_cap,
+                                               reinterpret_cast<const uint32_t*>(c->d_err + AGNES_ERR_BYTES / 8) +
+                                                   AGNES_WALK_COUNT,
+                                               counts, out, st));
+    return status_of(agnes_launch_seg_walk(b, codes, cfg->max_rounds, mult, nullptr, nullptr, counts, out, st));
+}
+
+int agnes_records_compact(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, const uint64_t* counts,
+                          const agnes_seg_event* seg, uint64_t* offsets, agnes_vote_event* out, void* stream) {
+    if (!c || !cfg_ok(cfg) || !b || !b->offsets || !offsets || (b->n_instances && (!counts || !seg)) ||
+        ((uintptr_t)out & 7u) || ((uintptr_t)seg & 15u))
+        return AGNES_E_INVALID;
+    AGNES_TRY(hipSetDevice(c->device));
+    const hipStream_t st = (hipStream_t)stream;
+    AGNES_ORDER(c, st);
+    AGNES_TRY(hipMemsetAsync(offsets, 0, sizeof(uint64_t), st));
+    if (b->n_instances == 0) return AGNES_OK;
+    const uint64_t words = agnes_edges_scratch_words(b->n_instances);
+    if (words > c->scan_cap) {
+        AGNES_TRY(hipStreamSynchronize(st));
+        if (c->d_scan) AGNES_TRY(hipFree(c->d_scan));
+        c->d_scan = nullptr;
+        c->scan_cap = 0;
+        AGNES_TRY(hipMalloc(&c->d_scan, words * sizeof(uint64_t)));
+        c->scan_cap = words;
+    }
+    AGNES_TRY(hipMemcpyAsync(offsets + 1, counts, sizeof(uint64_t) * b->n_instances, hipMemcpyDeviceToDevice, st));
+    {
+        AgnesKt kt("event_scan", st);
+        AGNES_TRY(agnes_launch_offsets_scan(offsets, b->n_instances, c->d_scan, st));
+    }
+    if (!out) return AGNES_OK; /* the offsets only (the caller sizes out from offsets[n]) */
+    const uint32_t mult = (cfg->flags & AGNES_FLAG_ROUND_SKIP) ? 2u : 1u;
+    return status_of(agnes_launch_seg_compact(b, mult, seg, offsets, out, st));
 }
 
 int agnes_events(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, const uint8_t* codes,

@@ -184,6 +184,74 @@ __global__ __launch_bounds__(64) void event_walk(EvArgs a) {
     }
 }
 
+/* ---- the segmented records (agnes_tally_records) ------------------------------------
+ * Instance i's records go to seg[mult * offsets[i] + k] (mult 2 with RoundSkip: a vote
+ * gives up to two records), k < counts[i], as 16-B agnes_seg_event.  The flow route
+ * writes them from the tally kernel itself; these are the other routes' (one lane per
+ * instance, the event_walk order) and the flow route's walk-list instances (LIST). */
+__device__ __forceinline__ void put_seg(uint4* o, uint64_t j, uint32_t value, uint32_t round, uint32_t kind,
+                                        uint32_t msg) {
+    *o = make_uint4((uint32_t)j, (uint32_t)(j >> 32), value, round | (kind << 8) | (msg << 16));
+}
+
+template <bool LIST>
+__global__ __launch_bounds__(64) void seg_walk(EvArgs a, const uint32_t* list, const uint32_t* list_n, uint32_t mult,
+                                               uint4* seg, uint64_t* counts) {
+    uint32_t* const lab = reinterpret_cast<uint32_t*>(agnes_smem);
+    const uint32_t lane = threadIdx.x;
+    uint32_t i;
+    if (LIST) {
+        const uint32_t k = blockIdx.x * 64u + lane;
+        if (k >= *(volatile const uint32_t*)list_n) return;
+        i = list[k];
+    } else {
+        i = blockIdx.x * 64u + lane;
+        if (i >= a.vb.n_instances) return;
+    }
+    for (uint32_t k = 0; k < a.keys; ++k) lab[k * 64u + lane] = 0u; /* VoteCount::new: Value{} */
+    const uint64_t NV = a.vb.n_votes;
+    uint64_t lo = a.vb.offsets[i], hi = a.vb.offsets[i + 1u];
+    lo = lo < NV ? lo : NV;
+    hi = hi < NV ? hi : NV;
+    uint4* const out = seg + (uint64_t)mult * a.vb.offsets[i];
+    uint64_t cnt = 0;
+    for (uint64_t j = lo; j < hi; ++j) {
+        const uint32_t cb = a.codes[j], ev = cb & AGNES_CODE_EVENT_MASK;
+        if (ev == AGNES_CODE_INVALID || ev == AGNES_CODE_REJECTED) continue; /* not added by the tally */
+        const uint32_t rb = a.vb.round[j], tb = a.vb.type[j], key = rb * 2u + tb;
+        if (tb > 1u || key >= a.keys) continue; /* (never for a code the tally wrote) */
+        uint32_t* const p = lab + key * 64u + lane;
+        const uint32_t v = a.vb.value[j];
+        if (v != AGNES_NIL) *p = v; /* the value slot, last writer wins (round_votes.rs:50-54) */
+        const uint32_t msg = cb >> AGNES_CODE_MSG_SHIFT;
+        if ((cb >> 3) & 1u) put_seg(out + cnt++, j, AGNES_NIL, rb, AGNES_EV_ROUND_SKIP, msg);
+        if (ev != AGNES_CODE_NONE) {
+            const bool val = ev == AGNES_CODE_POLKA_VALUE || ev == AGNES_CODE_PRECOMMIT_VALUE;
+            put_seg(out + cnt++, j, val ? *p : AGNES_NIL, rb, kind_of(ev), msg);
+        }
+    }
+    counts[i] = cnt;
+}
+
+/* the dense stream from the segmented one: wave w copies instances 32w .. 32w + 31,
+ * each instance's records by the 64 lanes, adding the instance id (agnes_vote_event) */
+__global__ __launch_bounds__(256) void seg_compact(agnes_vote_batch vb, uint32_t mult, const uint4* seg,
+                                                   const uint64_t* offs, agnes_vote_event* out) {
+    const uint32_t lane = threadIdx.x & 63u, w = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t n = vb.n_instances;
+    for (uint32_t i = 32u * w; i < n && i < 32u * w + 32u; ++i) {
+        const uint64_t o = offs[i], cnt = offs[i + 1u] - o;
+        const uint4* const src = seg + (uint64_t)mult * vb.offsets[i];
+        for (uint64_t k = lane; k < cnt; k += 64u) {
+            const uint4 r = src[k];
+            uint2* const q = reinterpret_cast<uint2*>(out + o + k);
+            q[0] = make_uint2(r.x, r.y);
+            q[1] = make_uint2(i, r.z);
+            q[2] = make_uint2(r.w, 0u);
+        }
+    }
+}
+
 /* The emit pass, one WAVE per instance (columns aligned: codes / round / type 4 B,
  * value 16 B): the instance in 256-vote passes, lane l holding votes w + 4l ..
  * w + 4l + 3 (coalesced 4-B / 16-B loads).  Per pass: each vote's record count
@@ -807,5 +875,34 @@ hipError_t agnes_launch_events(const agnes_vote_batch* vb, const uint8_t* codes,
         hipLaunchKernelGGL(event_emit_wave, dim3(blocks), dim3(256), lds_w, st, a);
     } else
         hipLaunchKernelGGL((event_walk<true, 4u, false>), grid, blk, lds, st, a);
+    return hipGetLastError();
+}
+
+hipError_t agnes_launch_seg_walk(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds, uint32_t mult,
+                                 const uint32_t* list, const uint32_t* list_n, uint64_t* counts, void* seg,
+                                 hipStream_t st) {
+    using namespace agnes::events;
+    const uint32_t n = vb->n_instances;
+    if (n == 0) return hipSuccess;
+    EvArgs a{*vb, codes, nullptr, nullptr, 2u * max_rounds};
+    const size_t lds = (size_t)a.keys * 64u * sizeof(uint32_t);
+    AgnesKt kt("seg_walk", st);
+    if (list)
+        hipLaunchKernelGGL((seg_walk<true>), dim3((n + 63u) / 64u), dim3(64), lds, st, a, list, list_n, mult,
+                           reinterpret_cast<uint4*>(seg), counts);
+    else
+        hipLaunchKernelGGL((seg_walk<false>), dim3((n + 63u) / 64u), dim3(64), lds, st, a, list, list_n, mult,
+                           reinterpret_cast<uint4*>(seg), counts);
+    return hipGetLastError();
+}
+
+hipError_t agnes_launch_seg_compact(const agnes_vote_batch* vb, uint32_t mult, const void* seg, const uint64_t* offs,
+                                    agnes_vote_event* out, hipStream_t st) {
+    const uint32_t n = vb->n_instances;
+    if (n == 0) return hipSuccess;
+    const uint32_t waves = (n + 31u) / 32u, blocks = (waves + 3u) / 4u;
+    AgnesKt kt("seg_compact", st);
+    hipLaunchKernelGGL(agnes::events::seg_compact, dim3(blocks), dim3(256), 0, st, *vb, mult,
+                       reinterpret_cast<const uint4*>(seg), offs, out);
     return hipGetLastError();
 }

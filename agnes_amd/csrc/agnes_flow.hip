@@ -209,6 +209,27 @@ struct Hdr {
     uint32_t stream;    /* stage 2: the offsets pass; stage 3: walked by this kernel */
 };
 
+/* The value slot of executor (inst, r, t) after the votes before j (round_votes.rs:
+ * 50-54, one value slot, last writer wins): the last non-nil value the tally added,
+ * walking back to the instance start lo; Value{} (0) when none.  The rare path of the
+ * fused records: a nil vote whose PolkaValue / PrecommitValue executor took no non-nil
+ * vote earlier in its part of the chunk.  A vote counts when it is valid (REFERENCE:
+ * every valid vote is added): its instance id, type <= 1, validator in the set (its
+ * round is r < max_rounds). */
+__device__ __attribute__((noinline)) uint32_t label_back(const uint32_t* inst_col, const uint8_t* round_col,
+                                                        const uint8_t* type_col, const uint32_t* value_col,
+                                                        const uint32_t* val_col, uint64_t lo, uint64_t j, uint32_t inst,
+                                                        uint32_t r, uint32_t t, uint32_t nvs) {
+    for (uint64_t q = j; q > lo;) {
+        --q;
+        if (round_col[q] != r || type_col[q] != t) continue;
+        const uint32_t v = value_col[q];
+        if (v == AGNES_NIL || inst_col[q] != inst || val_col[q] >= nvs) continue;
+        return v;
+    }
+    return 0u;
+}
+
 /* EVC: also the number of event records of each instance of a flow batch (votes whose
  * code is Some(Event), 1..5: this route never sets the RoundSkip bit) into
  * a.ev_counts[instance] -- the count pass of the event stream (agnes_events.hip) */
@@ -220,8 +241,9 @@ struct Hdr {
 #ifndef AGNES_FLOW_WPE
 #define AGNES_FLOW_WPE 3
 #endif
-template <bool PC, bool SM, bool R1, bool EVC, bool W64>
+template <bool PC, bool SM, bool R1, bool EVC, bool W64, bool REC = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES_FLOW_W64_WPE : AGNES_FLOW_WPE))) void flow(agnes_tally_args a, uint32_t lds_per_wave) {
+    static_assert(!REC || (EVC && !W64), "records: with the record counts, u32 sums");
     constexpr uint32_t RW = W64 ? RECW64 : RECW; /* record words */
 
     const uint32_t lane = lane_id();
@@ -1203,6 +1225,96 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                     }
                 }
 
+                if constexpr (REC) {
+                    /* ---- the records themselves (agnes_tally_records): every vote whose event is
+                     * Some (codes 1..5) as a 16-B agnes_seg_event in its instance's segment,
+                     * out[offsets[i] + k] with k the instance's records before it, written while
+                     * the votes are in registers (vote_executor.rs:20-36) ---- */
+                    auto recm = [](uint32_t cw4) -> uint32_t { /* 0x80 in the bytes of votes with a record */
+                        const uint32_t e = cw4 & 0x07070707u;
+                        return (e + 0x7F7F7F7Fu) & ~(e + 0x7A7A7A7Au) & 0x80808080u;
+                    };
+                    const uint32_t hA = actA ? recm(c0) : 0u, hB = actB ? recm(c1) : 0u;
+                    if (ballot((hA | hB) != 0u)) {
+                        const uint32_t nA = (uint32_t)__builtin_popcount(hA), nB = (uint32_t)__builtin_popcount(hB);
+                        /* ranks inside the chunk: an exclusive scan of the lanes' last-instance counts,
+                         * less the scan at the instance's first lane; plus the instance's records of
+                         * earlier chunks (etab, before this chunk's counts are added below) */
+                        const uint32_t Tn = split ? nB : nA + nB;
+                        const uint32_t En = scan(Tn) - Tn;
+                        const uint32_t rA = etab[kA] + En - (multi ? shfl(En, sA) : 0u);
+                        const uint32_t rB = split ? etab[kB] : rA + nA;
+                        const uint64_t gA = Sa + shfl(rl, kA), gB = Sa + shfl(rl, kB); /* instance starts */
+                        /* the Value a PolkaValue / PrecommitValue carries (round_votes.rs:50-54): the
+                         * vote's own when non-nil; for a nil vote the last non-nil value its executor
+                         * took before it -- in the lane, else (one round, or runs: the segment is the
+                         * executor's run up to its type) the last earlier lane of the segment holding
+                         * one, else the stream before the chunk part (label_back) */
+                        const uint32_t vok0 = okb0 & ~mark_bytes(nb0 << 3), vok1 = okb1 & ~mark_bytes(nb1 << 3); /* valid non-nil */
+                        uint32_t vv[LV];
+                        uint32_t pend = 0u; /* bit s: a nil Value vote not resolved in the lane */
+                        bool hv0 = false, hv1 = false;
+                        uint32_t lv0x = 0u, lv1x = 0u;
+                        const bool spl = R1 ? split : splitr;
+#pragma unroll
+                        for (uint32_t q = 0; q < LV; ++q) {
+                            if (q == 4u && spl) { hv0 = false; hv1 = false; }
+                            const uint32_t bs = 8u * (q & 3u);
+                            const uint32_t cq = ((q < 4u ? c0 : c1) >> bs) & 7u;
+                            const bool tq = (((q < 4u ? t8[0] : t8[1]) >> bs) & 1u) != 0u;
+                            const bool nn = (((q < 4u ? vok0 : vok1) >> bs) & 1u) != 0u;
+                            const bool isv = cq == AGNES_CODE_POLKA_VALUE || cq == AGNES_CODE_PRECOMMIT_VALUE;
+                            const bool hasT = tq ? hv1 : hv0;
+                            const uint32_t lT = tq ? lv1x : lv0x;
+                            vv[q] = nn ? value[q] : (isv && hasT ? lT : AGNES_NIL);
+                            pend |= (isv && !nn && !hasT) ? 1u << q : 0u;
+                            if (nn) {
+                                if (tq) { hv1 = true; lv1x = value[q]; } else { hv0 = true; lv0x = value[q]; }
+                            }
+                        }
+                        if (ballot(pend != 0u)) {
+                            const bool fast = R1 || runs;
+                            const uint32_t sx = !fast ? 0u : (R1 ? (multi ? sA : 0u) : (multir ? sAr : 0u));
+                            const uint64_t seg = (((1ull << lane) - 1ull) >> sx) << sx; /* lanes [sx, lane) */
+                            const uint64_t B0 = ballot(hv0), B1 = ballot(hv1);
+                            const uint64_t m0 = B0 & seg, m1 = B1 & seg;
+                            const uint32_t j0 = m0 ? 63u - (uint32_t)__builtin_clzll(m0) : 0u;
+                            const uint32_t j1 = m1 ? 63u - (uint32_t)__builtin_clzll(m1) : 0u;
+                            const uint32_t f0 = shfl(lv0x, j0), f1 = shfl(lv1x, j1);
+                            for (uint32_t q = 0; q < LV; ++q) {
+                                if (!((pend >> q) & 1u)) continue;
+                                const uint32_t bs = 8u * (q & 3u);
+                                const bool tq = (((q < 4u ? t8[0] : t8[1]) >> bs) & 1u) != 0u;
+                                if (fast && (q < 4u || !spl) && (tq ? m1 : m0)) {
+                                    vv[q] = tq ? f1 : f0;
+                                } else {
+                                    const uint32_t rq = ((q < 4u ? r8[0] : r8[1]) >> bs) & 0xFFu;
+                                    const uint64_t gq = q < 4u ? gA : gB;
+                                    vv[q] = label_back(a.vb.instance, a.vb.round, a.vb.type, a.vb.value, a.vb.validator, gq,
+                                                       c + o8 + q, H.s0 + (q < 4u ? kA : kB), rq, tq ? 1u : 0u,
+                                                       q < 4u ? recA.z : recB.z);
+                                }
+                            }
+                        }
+                        /* the stores: one 16-B record per vote with an event */
+#pragma unroll
+                        for (uint32_t q = 0; q < LV; ++q) {
+                            const uint32_t bs = 8u * (q & 3u);
+                            const uint32_t hm = q < 4u ? hA : hB;
+                            if ((hm >> (bs + 7u)) & 1u) {
+                                const uint32_t k = (q < 4u ? rA : rB) + (uint32_t)__builtin_popcount(hm & ((1u << bs) - 1u));
+                                const uint32_t cb = ((q < 4u ? c0 : c1) >> bs) & 0xFFu;
+                                const uint32_t rq = ((q < 4u ? r8[0] : r8[1]) >> bs) & 0xFFu;
+                                const uint64_t j = c + o8 + q;
+                                const bool isv = (cb & 7u) == AGNES_CODE_POLKA_VALUE || (cb & 7u) == AGNES_CODE_PRECOMMIT_VALUE;
+                                const uint4 rec = make_uint4((uint32_t)j, (uint32_t)(j >> 32), isv ? vv[q] : AGNES_NIL,
+                                                             rq | (((cb & 7u) + 3u) << 8) | ((cb >> 4) << 16));
+                                reinterpret_cast<uint4*>(a.rec_out)[(q < 4u ? gA : gB) + k] = rec;
+                            }
+                        }
+                    }
+                }
+
                 if (EVC) { /* records per unit: the votes whose event is Some (codes 1..5) */
                     auto recs = [](uint32_t cw4) -> uint32_t {
                         const uint32_t e = cw4 & 0x07070707u;
@@ -1275,13 +1387,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
 /* ------------------------------------------------------------------ */
 /* launcher                                                            */
 
-template <bool SM, bool R1, bool EVC, bool W64>
+template <bool SM, bool R1, bool EVC, bool W64, bool REC = false>
 static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStream_t st) {
     const uint32_t n = a->vb.n_instances;
     if (n == 0) return hipSuccess;
     using agnes::flow::flow;
-    const void* fns[2] = {reinterpret_cast<const void*>(&flow<false, SM, R1, EVC, W64>),
-                          reinterpret_cast<const void*>(&flow<true, SM, R1, EVC, W64>)};
+    const void* fns[2] = {reinterpret_cast<const void*>(&flow<false, SM, R1, EVC, W64, REC>),
+                          reinterpret_cast<const void*>(&flow<true, SM, R1, EVC, W64, REC>)};
     const uint32_t lpw = agnes::flow::lds_bytes(SM, a->max_rounds, EVC, W64);
     const uint64_t wave_lds = (uint64_t)lpw * AGNES_WAVES_PER_BLOCK;
     const uint64_t pcb = agnes::align16((W64 ? 8ull : 4ull) * a->n_sets * a->n_vals);
@@ -1345,8 +1457,8 @@ static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStrea
     const uint64_t cap = ncu * (uint64_t)o->per_cu;
     if (blocks > cap) blocks = cap;
     if (blocks == 0) blocks = 1;
-    if (o->pc) hipLaunchKernelGGL((flow<true, SM, R1, EVC, W64>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
-    else hipLaunchKernelGGL((flow<false, SM, R1, EVC, W64>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
+    if (o->pc) hipLaunchKernelGGL((flow<true, SM, R1, EVC, W64, REC>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
+    else hipLaunchKernelGGL((flow<false, SM, R1, EVC, W64, REC>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
     return hipGetLastError();
 }
 
@@ -1380,6 +1492,14 @@ hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t
         if (a->max_rounds == 1u)
             return sm ? launch_flow_k<true, true, false, true>(a, num_cus, st) : launch_flow_k<false, true, false, true>(a, num_cus, st);
         return sm ? launch_flow_k<true, false, false, true>(a, num_cus, st) : launch_flow_k<false, false, false, true>(a, num_cus, st);
+    }
+    if (a->rec_out) { /* agnes_tally_records: counts and the records themselves */
+        if (!a->ev_counts) return hipErrorInvalidValue;
+        if (a->max_rounds == 1u)
+            return sm ? launch_flow_k<true, true, true, false, true>(a, num_cus, st)
+                      : launch_flow_k<false, true, true, false, true>(a, num_cus, st);
+        return sm ? launch_flow_k<true, false, true, false, true>(a, num_cus, st)
+                  : launch_flow_k<false, false, true, false, true>(a, num_cus, st);
     }
     if (a->ev_counts) {
         if (a->max_rounds == 1u)

@@ -67,6 +67,9 @@ typedef struct agnes_tally_args {
     uint32_t tail_n;      /* flow: instances in the tail (the last ones)                        */
     uint32_t w64;         /* the u64 fast domain (agnes_set_info.w64 sets outside the u32 one):
                              tally_fast with u64 sums, the apply pass tests the same deferral */
+    void* rec_out;        /* optional (agnes_tally_records): agnes_seg_event [n_votes], instance i's
+                             records at [offsets[i], offsets[i] + ev_counts[i]) -- the flow
+                             kernel writes them (REC); every other route's emit pass does */
     uint64_t* ev_counts;  /* optional [n_instances]: the flow kernel writes each instance's event
                              record count (agnes_tally_events); instances it hands to the walk
                              list are left to agnes_launch_event_count_list */
@@ -106,6 +109,14 @@ hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t
 bool agnes_dflow_supported(const agnes_tally_args* a);
 bool agnes_dflow_route(const agnes_tally_args* a);
 hipError_t agnes_launch_dflow(const agnes_tally_args* a, uint32_t mode, int num_cus, hipStream_t stream);
+/* the segmented records (agnes_tally_records) of every instance, or of the ones on a
+ * list (the flow route's walk list; list_n on the device), one lane per instance; and
+ * the dense stream from them (offs: the exclusive scan of the counts) */
+hipError_t agnes_launch_seg_walk(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds, uint32_t mult,
+                                 const uint32_t* list, const uint32_t* list_n, uint64_t* counts, void* seg,
+                                 hipStream_t stream);
+hipError_t agnes_launch_seg_compact(const agnes_vote_batch* vb, uint32_t mult, const void* seg, const uint64_t* offs,
+                                    agnes_vote_event* out, hipStream_t stream);
 /* the flow kernel can count event records (agnes_tally_events) in this configuration */
 bool agnes_flow_counts_events(uint32_t flags, uint32_t max_rounds);
 /* the batched State::apply pass over the codes a tally kernel left (agnes_apply.hip):

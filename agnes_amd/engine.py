@@ -168,6 +168,45 @@ class Engine:
               "agnes_tally_events")
         return offsets, out
 
+    def tally_records(self, cfg: abi.Config, batch: DeviceBatch, codes: torch.Tensor,
+                      states_in: Optional[torch.Tensor] = None, states_out: Optional[torch.Tensor] = None,
+                      counts: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, stream=None):
+        """agnes_tally_records: the tally (as tally_states) and its records segmented by
+        instance: counts int64 [n_instances], out uint8 [events_capacity, 16] (instance i's
+        records at rows seg(i) .. seg(i) + counts[i], seg(i) = offsets[i], x2 with
+        RoundSkip; view a host copy as abi.SEG_EVENT_DTYPE).  Allocated when None; no sync."""
+        if codes.dtype != torch.uint8 or codes.numel() < batch.n_votes:
+            raise ValueError("codes must be a uint8 tensor of n_votes")
+        for t in (states_in, states_out):
+            if t is not None and t.numel() < 64 * batch.n_instances:
+                raise ValueError("states must hold n_instances 64-byte records")
+        cap = self.events_capacity(cfg, batch)
+        if counts is None:
+            counts = torch.empty(max(batch.n_instances, 1), dtype=torch.int64, device=self.device)
+        if out is None:
+            out = torch.empty((max(cap, 1), 16), dtype=torch.uint8, device=self.device)
+        if counts.numel() < batch.n_instances or out.numel() < 16 * cap:
+            raise ValueError("counts must hold n_instances, out events_capacity records")
+        b = batch.c()
+        check(self.lib.agnes_tally_records(self.ctx, C.byref(cfg), C.byref(b), _ptr(codes), _ptr(states_in),
+                                           _ptr(states_out), _ptr(counts), _ptr(out), _stream_handle(stream)),
+              "agnes_tally_records")
+        return counts, out
+
+    def records_compact(self, cfg: abi.Config, batch: DeviceBatch, counts: torch.Tensor, seg: torch.Tensor,
+                        offsets: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, stream=None):
+        """agnes_records_compact: offsets int64 [n_instances + 1] (the scan of counts) and the
+        dense agnes_vote_event records (uint8 [events_capacity, 24]); allocated when None."""
+        if offsets is None:
+            offsets = torch.empty(batch.n_instances + 1, dtype=torch.int64, device=self.device)
+        if out is None:
+            out = torch.empty((max(self.events_capacity(cfg, batch), 1), 24), dtype=torch.uint8, device=self.device)
+        b = batch.c()
+        check(self.lib.agnes_records_compact(self.ctx, C.byref(cfg), C.byref(b), _ptr(counts), _ptr(seg),
+                                             _ptr(offsets), _ptr(out), _stream_handle(stream)),
+              "agnes_records_compact")
+        return offsets, out
+
     def events_capacity(self, cfg: abi.Config, batch: DeviceBatch) -> int:
         b = batch.c()
         return int(self.lib.agnes_events_capacity(C.byref(cfg), C.byref(b)))

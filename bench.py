@@ -331,6 +331,58 @@ def tally_events_timed(eng, cfg, batch, codes, st0, states, steps, ref_offs, ref
             "kernels": {name: {"launches": k, "avg_ms": t / max(k, 1)} for name, (k, t) in kt.items()}}
 
 
+def tally_records_timed(eng, cfg, batch, codes, st0, states, steps, ref_offs, ref_recs):
+    """agnes_tally_records (round 5): the step and its records SEGMENTED by instance, the
+    flow kernel writing them while the votes are in registers (no pass over the votes
+    after the tally), graph-captured and timed like the step, outside the timed region
+    of `value`; then agnes_records_compact (one pass over the records) to the dense
+    stream, which must equal the two-call stream's (ref_offs / ref_recs) byte for byte."""
+    cap = eng.events_capacity(cfg, batch)
+    counts = torch.empty(max(batch.n_instances, 1), dtype=torch.int64, device=eng.device)
+    seg = torch.empty((max(cap, 1), 16), dtype=torch.uint8, device=eng.device)
+
+    def call():
+        eng.tally_records(cfg, batch, codes, st0, states, counts, seg)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            fn()
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=side):
+            fn()
+        g.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            g.replay()
+        torch.cuda.synchronize()
+        del g
+        return (time.perf_counter() - t0) * 1e3 / steps
+
+    call()
+    torch.cuda.synchronize()
+    eng.kernel_timing(True)
+    for _ in range(3):
+        call()
+    torch.cuda.synchronize()
+    kt = eng.kernel_times()
+    eng.kernel_timing(False)
+    ms = timed(call)
+    offs = torch.empty(batch.n_instances + 1, dtype=torch.int64, device=eng.device)
+    dense = torch.empty((max(cap, 1), 24), dtype=torch.uint8, device=eng.device)
+    ms_c = timed(lambda: eng.records_compact(cfg, batch, counts, seg, offs, dense))
+    n = int(offs[-1].item())
+    equal = bool(torch.equal(offs, ref_offs) and torch.equal(dense[:n], ref_recs))
+    del seg, dense
+    return {"ms_per_call": ms, "compact_ms": ms_c, "records": n, "compacted_equal_to_two_call_stream": equal,
+            "kernels": {name: {"launches": k, "avg_ms": t / max(k, 1)} for name, (k, t) in kt.items()}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -438,6 +490,9 @@ def main():
     te = tally_events_timed(eng, cfg, batch, codes, st0, states, args.steps, ev_offs, ev_recs)
     te["records_ms"] = te["ms_per_call"] - elapsed * 1e3 / args.steps  # over the tally step alone
     events["tally_events"] = te
+    tr = tally_records_timed(eng, cfg, batch, codes, st0, states, args.steps, ev_offs, ev_recs)
+    tr["records_ms"] = tr["ms_per_call"] - elapsed * 1e3 / args.steps
+    events["tally_records"] = tr
     ed_offs = edges.pop("_offsets")
     if world > 1:  # every rank's edge records to every rank (RCCL), outside the timed region
         edges["all_gather"] = adist.gather_edges_timed(edges.pop("_records"))

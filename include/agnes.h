@@ -714,6 +714,36 @@ int agnes_tally_events(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote
                        agnes_vote_event* out, void* stream);
 uint64_t agnes_events_capacity(const agnes_config* cfg, const agnes_vote_batch* batch);
 
+/* The same records SEGMENTED by instance (round 5): no scan between the tally and the
+ * records, so on the flow route (REFERENCE without RoundSkip, max_rounds <= 15, every
+ * offset a multiple of 4 -- the C2 / C3 streams) the tally kernel writes them itself
+ * while the votes are in registers: the records cost no second pass over the votes.
+ * Instance i's records are out[seg(i) + k], k < counts[i], in vote order, with
+ * seg(i) = batch->offsets[i] (2 * offsets[i] with AGNES_FLAG_ROUND_SKIP); the slots
+ * between an instance's last record and the next segment are left as they were.  Every
+ * other route (and the flow route's walk-list instances) writes them with an emit walk.
+ * counts (DEVICE, n_instances u64); out (DEVICE, 16-B aligned) must hold
+ * agnes_events_capacity(cfg, batch) records.  The record is agnes_vote_event without
+ * the instance (the segment names it) and the padding. */
+typedef struct agnes_seg_event {
+    uint64_t vote;    /* index of the vote in the batch                             */
+    uint32_t value;   /* PolkaValue / PrecommitValue: the Value; else AGNES_NIL      */
+    uint8_t round;    /* Vote.round                                                 */
+    uint8_t kind;     /* AGNES_EV_POLKA_ANY .. AGNES_EV_PRECOMMIT_VALUE, _ROUND_SKIP */
+    uint8_t message;  /* the vote's State machine message nibble (code >> 4)        */
+    uint8_t pad;
+} agnes_seg_event;
+int agnes_tally_records(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch, uint8_t* codes,
+                        const agnes_state* states_in, agnes_state* states_out, uint64_t* counts, agnes_seg_event* out,
+                        void* stream);
+/* The dense layout from the segmented one (one pass over the records, none over the
+ * votes): offsets (DEVICE, n_instances + 1) := the exclusive scan of counts
+ * (offsets[n_instances] = the total), then (out not null, 8-B aligned) the
+ * agnes_vote_event records in instance then vote order -- exactly agnes_tally_events'. */
+int agnes_records_compact(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
+                          const uint64_t* counts, const agnes_seg_event* seg, uint64_t* offsets, agnes_vote_event* out,
+                          void* stream);
+
 /* ---------------------------------------------------------------------------
  * Synthetic workload generator (counter-based splitmix64; identical on host
  * and device, see agnes_amd/csrc/agnes_gen.h).  Not part of the hot path.

@@ -1,6 +1,8 @@
 """agnes_tally_events (the tally and its event stream in one C-ABI call, SURVEY.md
 §8(b) agnes_tally's d_out / d_n_out) against the checker (orc_tally_labels +
-orc_events): codes, States, offsets and every 24-B record bit for bit.
+orc_events): codes, States, offsets and every 24-B record bit for bit; and (round 5)
+agnes_tally_records, the same records segmented by instance and written by the flow
+kernel itself, plus agnes_records_compact's dense stream, on every case.
 
 The fused route (REFERENCE without RoundSkip) counts each instance's records inside
 the flow kernel; the instances it hands to its walk list (unaligned offsets, sets
@@ -61,7 +63,45 @@ def _check(eng, cfg, hb, power, states=None, in_place=True):
     e_offs, e_recs = eng.events(cfg, db, codes)
     assert np.array_equal(e_offs.cpu().numpy().view(np.uint64), g_offs)
     assert e_recs.cpu().numpy().tobytes() == out[:n].cpu().numpy().tobytes()
+    _check_records(eng, cfg, hb, db, states, in_place, o_codes, o_states, o_offs, o_ev)
     return o_ev
+
+
+def _check_records(eng, cfg, hb, db, states, in_place, o_codes, o_states, o_offs, o_ev):
+    """agnes_tally_records (round 5): the same tally, the records segmented by instance
+    (instance i's at rows mult * offsets[i] ..), then agnes_records_compact -> the dense
+    stream; every record bit for bit against the checker's."""
+    codes = torch.full((max(hb.n_votes, 1),), 0xEE, dtype=torch.uint8, device=eng.device)
+    s_in = s_out = None
+    if states is not None:
+        s_in = states_to_device(states, eng.device)
+        s_out = s_in if in_place else torch.zeros_like(s_in)
+    cap = eng.events_capacity(cfg, db)
+    seg = torch.full((max(cap, 1), 16), 0xCD, dtype=torch.uint8, device=eng.device)
+    counts, seg = eng.tally_records(cfg, db, codes, s_in, s_out, out=seg)
+    torch.cuda.synchronize()
+    assert np.array_equal(codes[:hb.n_votes].cpu().numpy(), o_codes), "codes differ (tally_records)"
+    if states is not None:
+        assert states_to_host(s_out).tobytes() == o_states.tobytes(), "States differ (tally_records)"
+    g_cnt = counts[:hb.n_instances].cpu().numpy().view(np.uint64)
+    o_cnt = np.diff(o_offs.astype(np.uint64))
+    assert np.array_equal(g_cnt, o_cnt), f"record counts differ (first at {np.nonzero(g_cnt != o_cnt)[0][:1]})"
+    mult = 2 if cfg.flags & abi.FLAG_ROUND_SKIP else 1
+    g_seg = seg.cpu().numpy().reshape(-1).view(abi.SEG_EVENT_DTYPE)
+    off = hb.offsets.astype(np.int64)
+    idx = np.concatenate([np.arange(mult * off[i], mult * off[i] + int(o_cnt[i])) for i in range(hb.n_instances)]
+                         + [np.zeros(0, np.int64)]).astype(np.int64)
+    got = g_seg[idx]
+    for f in ["vote", "value", "round", "kind", "message"]:
+        if not np.array_equal(got[f], o_ev[f]):
+            bad = np.nonzero(got[f] != o_ev[f])[0]
+            raise AssertionError(f"segmented records: field {f} differs in {len(bad)} of {len(o_ev)}; first {bad[0]}: "
+                                 f"gpu {got[bad[0]]} checker {o_ev[bad[0]]}")
+    d_offs, dense = eng.records_compact(cfg, db, counts, seg)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_offs.cpu().numpy().view(np.uint64), o_offs)
+    n = int(o_offs[-1])
+    assert dense[:n].cpu().numpy().tobytes() == o_ev.tobytes(), "compacted records differ"
 
 
 @pytest.mark.parametrize("flags", [abi.FLAG_STATE_MACHINE, 0, abi.FLAG_STATE_MACHINE | abi.FLAG_DISTINCT_VALUES])
@@ -150,6 +190,22 @@ def test_tally_events_mixed_batches(eng):
                       ol.gen_power(57, 1, 64, abi.POWER_UNIFORM, 1 << 40, 1 << 41)[0]])  # i64 domain
     _check(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 1), hb, power,
            abi.new_states(4096, 1, abi.STEP_PREVOTE))
+
+
+@pytest.mark.parametrize("nil", [300, 600])
+def test_tally_records_revisited_rounds(eng, nil):
+    """flow with rounds revisited inside a chunk (5 % next-round votes, 300-vote rounds
+    so every offset stays a multiple of 4): the per-round passes, and nil PolkaValue /
+    PrecommitValue votes whose executor's value slot comes from before the chunk
+    (the fused records' label walk back, round_votes.rs:50-54)"""
+    p = abi.gen_params(seed=62, n_instances=3000, n_vals=120, rounds_min=1, rounds_max=4, nil_permille=nil,
+                       dup_permille=100, equiv_permille=100, higher_permille=50)
+    hb = ol.gen_batch(p)
+    assert (hb.offsets % 4 == 0).all()
+    power = ol.gen_power(62, 7, 120, abi.POWER_UNIFORM, 1, 1000)
+    _check(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 5), hb, power,
+           abi.new_states(3000, 1, abi.STEP_PREVOTE))
+    _check(eng, abi.config(abi.MODE_REFERENCE, 0, 5), hb, power)
 
 
 def test_tally_events_fifteen_rounds(eng):
