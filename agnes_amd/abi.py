@@ -47,8 +47,6 @@ def FLAG_ROUTE(r: int) -> int:
     return (r & 3) << ROUTE_SHIFT
 
 
-# with ROUTE_AUTO: DEDUP / RoundSkip batches on the one-pass stream kernel (agnes_dflow.hip)
-FLAG_ROUTE_STREAM = 0x400
 
 
 def FLAG_EPOCH_BITS(b: int) -> int:

@@ -12,7 +12,7 @@ from concurrent.futures import ThreadPoolExecutor
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 OBJ = os.path.join(PKG_DIR, "_obj")
-SOURCES = ["agnes_kernels.hip", "agnes_fast.hip", "agnes_sweep.hip", "agnes_flow.hip", "agnes_dflow.hip", "agnes_apply.hip",
+SOURCES = ["agnes_kernels.hip", "agnes_fast.hip", "agnes_sweep.hip", "agnes_flow.hip", "agnes_apply.hip",
            "agnes_edges.hip", "agnes_events.hip", "agnes_partials.hip", "agnes_fold.hip", "agnes_onesm.hip", "agnes_dedup.hip",
            "agnes_multi.hip", "agnes_valset.hip", "agnes_wire.hip", "agnes_api.cpp"]
 HEADERS = ["agnes_device.h", "agnes_ed25519.h", "agnes_fast.h", "agnes_gen.h", "agnes_gen_host.h",

@@ -122,7 +122,7 @@ bool cfg_ok(const agnes_config* cfg) {
     return cfg && cfg->max_rounds >= 1 && cfg->max_rounds <= 256 && cfg->mode <= AGNES_MODE_DEDUP &&
            (cfg->flags & ~(AGNES_FLAG_ROUND_SKIP | AGNES_FLAG_STATE_MACHINE | AGNES_FLAG_DISTINCT_VALUES |
                            AGNES_FLAG_ONE_INSTANCE | AGNES_FLAG_WEIGHTS_CACHED | AGNES_FLAG_MASKED_REJECTED |
-                           (AGNES_ROUTE_MASK << AGNES_ROUTE_SHIFT) | AGNES_FLAG_ROUTE_STREAM |
+                           (AGNES_ROUTE_MASK << AGNES_ROUTE_SHIFT) |
                            AGNES_FLAG_EPOCH_BITS(0x1F))) == 0;
 }
 
@@ -380,13 +380,9 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
         const uint32_t route = (cfg->flags >> AGNES_ROUTE_SHIFT) & AGNES_ROUTE_MASK;
         const bool flow = !wide_all && !w64 && route == AGNES_ROUTE_AUTO && cfg->mode == AGNES_MODE_REFERENCE &&
                           !(cfg->flags & AGNES_FLAG_ROUND_SKIP) && agnes_flow_counts_events(cfg->flags, cfg->max_rounds);
-        /* DEDUP / RoundSkip on the stream kernel: it counts too (the LIST kernel's
-         * instances go on the walk list, counted after their codes) */
-        const bool dfl = !rec_out && !wide_all && (cfg->mode == AGNES_MODE_DEDUP || (cfg->flags & AGNES_FLAG_ROUND_SKIP)) &&
-                         agnes_dflow_route(&a);
-        if (flow || dfl) a.ev_counts = ev_counts;
+        if (flow) a.ev_counts = ev_counts;
         if (flow && rec_out) a.rec_out = rec_out; /* agnes_tally_records: the flow kernel writes them too */
-        if (counted) *counted = flow || dfl;
+        if (counted) *counted = flow;
     }
     return status_of(agnes_launch_tally(&a, cfg->mode, c->num_cus, wide_all, st));
 }

@@ -1256,6 +1256,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                         bool hv0 = false, hv1 = false;
                         uint32_t lv0x = 0u, lv1x = 0u;
                         const bool spl = R1 ? split : splitr;
+                        /* one round, or runs: a lane part of one segment is one executor per type;
+                         * otherwise (rounds revisited in the chunk) every nil Value vote walks back */
+                        const bool fast = R1 || runs;
 #pragma unroll
                         for (uint32_t q = 0; q < LV; ++q) {
                             if (q == 4u && spl) { hv0 = false; hv1 = false; }
@@ -1264,7 +1267,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                             const bool tq = (((q < 4u ? t8[0] : t8[1]) >> bs) & 1u) != 0u;
                             const bool nn = (((q < 4u ? vok0 : vok1) >> bs) & 1u) != 0u;
                             const bool isv = cq == AGNES_CODE_POLKA_VALUE || cq == AGNES_CODE_PRECOMMIT_VALUE;
-                            const bool hasT = tq ? hv1 : hv0;
+                            const bool hasT = fast && (tq ? hv1 : hv0);
                             const uint32_t lT = tq ? lv1x : lv0x;
                             vv[q] = nn ? value[q] : (isv && hasT ? lT : AGNES_NIL);
                             pend |= (isv && !nn && !hasT) ? 1u << q : 0u;
@@ -1273,7 +1276,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                             }
                         }
                         if (ballot(pend != 0u)) {
-                            const bool fast = R1 || runs;
                             const uint32_t sx = !fast ? 0u : (R1 ? (multi ? sA : 0u) : (multir ? sAr : 0u));
                             const uint64_t seg = (((1ull << lane) - 1ull) >> sx) << sx; /* lanes [sx, lane) */
                             const uint64_t B0 = ballot(hv0), B1 = ballot(hv1);

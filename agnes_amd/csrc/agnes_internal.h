@@ -104,11 +104,6 @@ hipError_t agnes_launch_sweep(const agnes_tally_args* a, int num_cus, hipStream_
 /* the 8-votes-per-lane flow kernel (agnes_flow.hip) for the sweep route's streams */
 bool agnes_flow_supported(const agnes_tally_args* a);
 hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t stream);
-/* the stream kernel for DEDUP / RoundSkip batches (agnes_dflow.hip): codes only, the
- * State machine left to the apply pass; agnes_dflow_route: the AUTO route takes it */
-bool agnes_dflow_supported(const agnes_tally_args* a);
-bool agnes_dflow_route(const agnes_tally_args* a);
-hipError_t agnes_launch_dflow(const agnes_tally_args* a, uint32_t mode, int num_cus, hipStream_t stream);
 /* the segmented records (agnes_tally_records) of every instance, or of the ones on a
  * list (the flow route's walk list; list_n on the device), one lane per instance; and
  * the dense stream from them (offs: the exclusive scan of the counts) */

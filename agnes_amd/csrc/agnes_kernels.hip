@@ -1305,10 +1305,6 @@ static hipError_t launch_mode(const agnes_tally_args* a, uint32_t lpw, int num_c
                            agnes_sweep_supported(a);
         if (sweep) {
             e = agnes_launch_sweep(a, num_cus, st); /* the stream and walk kernels */
-        } else if (route == AGNES_ROUTE_AUTO && agnes_dflow_route(a)) {
-            /* DEDUP / RoundSkip: the stream kernel (tally, RoundSkip, State machine) */
-            AgnesKt kt("dflow", st);
-            e = agnes_launch_dflow(a, MODE, num_cus, st);
         } else {
             /* per-instance route: split (C4 1.04 vs 1.11 ms fused) unless forced fused */
             const bool split = SM && route != AGNES_ROUTE_INSTANCE && agnes_apply_codes_supported(a);

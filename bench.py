@@ -38,7 +38,6 @@ BYTES_PER_VOTE = 15            # 14 B canonical SoA in + 1 B code out (BASELINE.
 KERNEL_BYTES_PER_VOTE = {
     "flow": 15,          # instance, value, validator u32 + round, type u8 in; code u8 out
     "tally_fast": 15,
-    "dflow": 15,         # DEDUP / RoundSkip stream kernel: the same columns in, code out
     "tally_wide": 15,
     "tally_list": 15,    # the i64 kernel over the instances the u32 kernels hand over (c2w: all)
     "sweep_walk": 15,
@@ -55,14 +54,13 @@ C5_PASS_B_BYTES_PER_VOTE = 23
 # read and written once per step (64-B agnes_state in, 64 B out) by the kernel that
 # applies the events (flow on the fused route, apply_codes on the split one)
 STATE_BYTES_PER_INSTANCE = 128
-KERNEL_STATE_IO = {"flow", "dflow", "apply_codes", "tally_list", "sweep_walk"}
+KERNEL_STATE_IO = {"flow", "apply_codes", "tally_list", "sweep_walk"}
 KERNEL_SYMBOLS = {
     # template parameters: PC (power table in LDS), SM (State machine), R1 (one round);
     # c2 runs flow<true, true, true>, c3 flow<false, true, false> (rocprofv3 names them)
     "flow": "agnes::flow::flow<PC, SM, R1>",
     "sweep_walk": "agnes::sweep::sweep<PC, SM>",
     "tally_fast": "agnes::fast::tally_fast<...>",
-    "dflow": "agnes::dflow::dflow<DEDUP, SKIP, PC, EVC, SM>",
     "tally_wide": "agnes::tally_kernel<true, ...>",
     "tally_list": "agnes::tally_kernel<true, MODE, SKIP, SM, LIST=true>",
     "apply_codes": "agnes::apply::apply_codes<RoundSkip>",

@@ -214,11 +214,6 @@ typedef struct agnes_state {
 #define AGNES_ROUTE_SPLIT 2u
 #define AGNES_ROUTE_WIDE 3u
 #define AGNES_FLAG_ROUTE(r) ((uint32_t)(r) << AGNES_ROUTE_SHIFT)
-/* With AGNES_ROUTE_AUTO: a DEDUP / RoundSkip batch on the one-pass stream kernel
- * (agnes_dflow.hip: tally, RoundSkip and the State machine in one pass over the
- * votes) instead of the per-instance kernel + apply pass.  Identical results;
- * measured slower on C4 (1.70 vs 0.98 ms), so not the engine's own choice. */
-#define AGNES_FLAG_ROUTE_STREAM 0x400u
 /* Bits 16..20 of agnes_config.flags: minimum bits the DEDUP / RoundSkip first-vote
  * tables spend on a vote's index inside its instance (0 = just enough for the
  * batch).  More index bits leave fewer epochs per table fill, so the tables are

@@ -26,14 +26,12 @@ EV_BY_NAME = {n: i for i, n in enumerate(abi.EVENT_NAMES)}
 # every route the launcher can take (agnes_kernels.hip launch_mode), forced by the
 # cfg route field: the engine's choice (the fused sweep for REFERENCE without
 # RoundSkip), the per-instance kernel with the State machine fused, the same
-# followed by the apply pass, the i64 kernel for every instance, and the one-pass
-# stream kernel for DEDUP / RoundSkip (AGNES_FLAG_ROUTE_STREAM)
+# followed by the apply pass, and the i64 kernel for every instance
 ROUTES = {
     "auto": abi.FLAG_ROUTE(abi.ROUTE_AUTO),
     "fused": abi.FLAG_ROUTE(abi.ROUTE_INSTANCE),
     "split": abi.FLAG_ROUTE(abi.ROUTE_SPLIT),
     "wide": abi.FLAG_ROUTE(abi.ROUTE_WIDE),
-    "stream": abi.FLAG_ROUTE(abi.ROUTE_AUTO) | abi.FLAG_ROUTE_STREAM,  # DEDUP / RoundSkip: agnes_dflow.hip
 }
 
 

@@ -126,17 +126,14 @@ def test_tally_events_rounds(eng, in_place):
            abi.new_states(4000, 1, abi.STEP_PREVOTE), in_place=in_place)
 
 
-@pytest.mark.parametrize("stream", [False, True])
-def test_tally_events_dedup_skip(eng, stream):
-    """C4's shape: the per-instance route, records counted by the count pass; or
-    (stream) the one-pass stream kernel, which counts them itself"""
+def test_tally_events_dedup_skip(eng):
+    """C4's shape: the per-instance route, records counted by the count pass"""
     p = abi.gen_params(seed=53, n_instances=2000, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300,
                        dup_permille=100, equiv_permille=100, higher_permille=50)
     hb = ol.gen_batch(p)
     hb.instance_set = (np.arange(2000) % 64).astype(np.uint32)
     power = ol.gen_power(53, 64, 150, abi.POWER_ZIPF, 1, 1_000_000)
-    cfg = abi.config(abi.MODE_DEDUP, abi.FLAG_STATE_MACHINE | abi.FLAG_ROUND_SKIP | abi.FLAG_DISTINCT_VALUES |
-                     (abi.FLAG_ROUTE_STREAM if stream else 0), 5)
+    cfg = abi.config(abi.MODE_DEDUP, abi.FLAG_STATE_MACHINE | abi.FLAG_ROUND_SKIP | abi.FLAG_DISTINCT_VALUES, 5)
     ev = _check(eng, cfg, hb, power, abi.new_states(2000, 1, abi.STEP_PREVOTE))
     assert (ev["kind"] == abi.EV_ROUND_SKIP).any()
 

@@ -21,7 +21,6 @@ KERNELS = {
     "flow": r"agnes::flow::flow<",
     "sweep_walk": r"agnes::sweep::sweep<",
     "tally_fast": r"agnes::fast::tally_fast<",
-    "dflow": r"agnes::dflow::dflow<",
     "apply_codes": r"agnes::apply::apply_codes<",
     "tally_list": r"agnes::tally_kernel<true, \w+, \w+, \w+, true,",
     "tally_wide": r"agnes::tally_kernel<true, \w+, \w+, \w+, false,",
