@@ -74,6 +74,9 @@ constexpr uint32_t F_INST = 0, F_VALUE = 2048, F_VAL = 4096, F_ROUND = 6144, F_T
 #ifndef AGNES_FLOW_TAIL_PER_WAVE
 #define AGNES_FLOW_TAIL_PER_WAVE 2
 #endif
+#ifndef AGNES_FLOW_FAST_START
+#define AGNES_FLOW_FAST_START 1 /* static first batches, the first chunk's DMA before the set constants */
+#endif
 #ifndef AGNES_FLOW_SMALLB
 #define AGNES_FLOW_SMALLB 4
 #endif
@@ -449,6 +452,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
 
     Hdr H, N;
     uint32_t tq = 0; /* lane 0: slot of the batch after N (atomic in flight) */
+#if AGNES_FLOW_FAST_START
+    /* the first two batches of a wave need no atomic: the waves of counter qk (blocks
+     * qk, qk + qn, ...) take static slots rank and S + rank; the counter hands out slots
+     * from 2 S on */
+    const uint32_t qS = ((gridDim.x - 1u - qk) / qn + 1u) * AGNES_WAVES_PER_BLOCK;
+    {
+        const uint32_t rank = (blockIdx.x / qn) * AGNES_WAVES_PER_BLOCK + wave;
+        range_of(rank, H.s0, H.e0);
+        range_of(qS + rank, N.s0, N.e0);
+        if (lane == 0) tq = atomicAdd(ctr, 1u) + 2u * qS;
+    }
+#else
+    const uint32_t qS = 0u;
     {
         uint32_t t = 0;
         if (lane == 0) t = atomicAdd(ctr, 2u);
@@ -457,6 +473,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
         range_of(t + 1u, N.s0, N.e0);
         if (lane == 0) tq = atomicAdd(ctr, 1u);
     }
+#endif
     FDIAG(unsigned long long* const dg = flow_diag_buf + 64ull * (blockIdx.x * AGNES_WAVES_PER_BLOCK + wave);
           uint32_t dg_b = 0, dg_c = 0;
           if (lane == 0) dg[0] = __builtin_amdgcn_s_memrealtime();)
@@ -465,6 +482,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
         return;
     }
     hdr1(H);
+#if AGNES_FLOW_FAST_START
+    { /* the first chunk's DMA as soon as the offsets are in, ahead of the set constants
+       * (only for offsets that bound a stream inside the columns; hdr2 decides the rest) */
+        const uint32_t m = H.e0 - H.s0;
+        const uint64_t O0 = u64of(rdl(H.olo, 0u), rdl(H.ohi, 0u)), Om = u64of(rdl(H.olo, m), rdl(H.ohi, m));
+        if (Om > O0 && Om - O0 < (1ull << 30)) {
+            const uint64_t Sa0 = O0 & ~127ull;
+            dma_chunk(Sa0, (uint32_t)(O0 - Sa0), (uint32_t)(Om - Sa0));
+            pf_at = Sa0;
+        }
+    }
+#endif
     hdr2(H);
     hdr3(H);
     dma_states(H, spar);
@@ -476,6 +505,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
         unsigned char* const sbh = sb + spar * (FB * 64u);
         bool smf = SM; /* the State views are not yet set up from the staged States */
         if (!H.stream) { /* not one flow stream: the walk list (agnes_sweep.hip) */
+            if (pf_at != ~0ull) { /* an early first-chunk DMA of this batch: drained, dropped */
+                dma_wait();
+                pf_at = ~0ull;
+            }
             uint32_t w0 = 0;
             if (lane == 0) w0 = atomicAdd(a.list_count + AGNES_WALK_COUNT, m);
             w0 = rdl(w0, 0u);
@@ -1370,7 +1403,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
         H = N;
         spar ^= 1u;
         range_of(rdl(tq, 0u), N.s0, N.e0); /* the batch after, grabbed one batch ago */
-        if (lane == 0) tq = atomicAdd(ctr, 1u);
+        if (lane == 0) tq = atomicAdd(ctr, 1u) + 2u * qS;
         hdr1(N);
     }
     flush();
