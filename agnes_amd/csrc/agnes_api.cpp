@@ -298,7 +298,7 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
                       uint8_t* codes, const agnes_state* states_in, agnes_state* states,
                       agnes_carry_rec* carry, const agnes_set_info* sets, uint32_t n_sets, uint32_t sets_dom,
                       hipStream_t st, uint64_t* ev_counts = nullptr, bool* counted = nullptr,
-                      void* rec_out = nullptr) {
+                      void* rec_out = nullptr, bool edges = false) {
     if (!c || !cfg_ok(cfg) || !b || !b->offsets) return AGNES_E_INVALID;
     if (b->n_votes && (!codes || !b->instance || !b->round || !b->type || !b->value ||
                        !b->validator))
@@ -379,9 +379,10 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     if (ev_counts) {
         const uint32_t route = (cfg->flags >> AGNES_ROUTE_SHIFT) & AGNES_ROUTE_MASK;
         const bool flow = !wide_all && !w64 && route == AGNES_ROUTE_AUTO && cfg->mode == AGNES_MODE_REFERENCE &&
-                          !(cfg->flags & AGNES_FLAG_ROUND_SKIP) && agnes_flow_counts_events(cfg->flags, cfg->max_rounds);
+                          !(cfg->flags & AGNES_FLAG_ROUND_SKIP) && agnes_flow_counts_events(cfg->flags, cfg->max_rounds, edges);
         if (flow) a.ev_counts = ev_counts;
-        if (flow && rec_out) a.rec_out = rec_out; /* agnes_tally_records: the flow kernel writes them too */
+        if (flow && rec_out) a.rec_out = rec_out; /* agnes_tally_records / _edges: the flow kernel writes them too */
+        if (flow && edges) a.edges = 1u;
         if (counted) *counted = flow;
     }
     return status_of(agnes_launch_tally(&a, cfg->mode, c->num_cus, wide_all, st));
@@ -711,6 +712,54 @@ int agnes_tally_records(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_
                                                    AGNES_WALK_COUNT,
                                                counts, out, st));
     return status_of(agnes_launch_seg_walk(b, codes, cfg->max_rounds, mult, nullptr, nullptr, counts, out, st));
+}
+
+int agnes_tally_edges(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, uint8_t* codes,
+                      const agnes_state* states_in, agnes_state* states_out, uint64_t* counts, agnes_edge* out,
+                      void* stream) {
+    if (!c || !cfg || !b || (cfg->flags & (AGNES_FLAG_ONE_INSTANCE | AGNES_FLAG_WEIGHTS_CACHED | AGNES_FLAG_MASKED_REJECTED)))
+        return AGNES_E_INVALID;
+    if ((b->n_instances && !counts) || (b->n_votes && !out) || ((uintptr_t)out & 15u)) return AGNES_E_INVALID;
+    if (cfg_ok(cfg) && cfg->max_rounds > 128u) return AGNES_E_UNSUPPORTED; /* the walk's executor bytes in LDS */
+    const hipStream_t st = (hipStream_t)stream;
+    bool counted = false;
+    const int rc = tally_impl(c, cfg, b, codes, states_in, states_out, nullptr, c->d_sets, c->n_sets, c->sets_dom, st,
+                              counts, &counted, out, true);
+    if (rc != AGNES_OK) return rc;
+    if (counted) /* the flow kernel wrote its batches' edges; the walk list's instances here */
+        return status_of(agnes_launch_edge_seg_walk(b, codes, cfg->max_rounds, c->d_list + (size_t)c->list_cap,
+                                                    reinterpret_cast<const uint32_t*>(c->d_err + AGNES_ERR_BYTES / 8) +
+                                                        AGNES_WALK_COUNT,
+                                                    counts, out, st));
+    return status_of(agnes_launch_edge_seg_walk(b, codes, cfg->max_rounds, nullptr, nullptr, counts, out, st));
+}
+
+int agnes_edges_compact(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, const uint64_t* counts,
+                        const agnes_edge* seg, uint64_t* offsets, agnes_edge* out, void* stream) {
+    if (!c || !cfg_ok(cfg) || !b || !b->offsets || !offsets || (b->n_instances && (!counts || !seg)) ||
+        ((uintptr_t)out & 15u) || ((uintptr_t)seg & 15u))
+        return AGNES_E_INVALID;
+    AGNES_TRY(hipSetDevice(c->device));
+    const hipStream_t st = (hipStream_t)stream;
+    AGNES_ORDER(c, st);
+    AGNES_TRY(hipMemsetAsync(offsets, 0, sizeof(uint64_t), st));
+    if (b->n_instances == 0) return AGNES_OK;
+    const uint64_t words = agnes_edges_scratch_words(b->n_instances);
+    if (words > c->scan_cap) {
+        AGNES_TRY(hipStreamSynchronize(st));
+        if (c->d_scan) AGNES_TRY(hipFree(c->d_scan));
+        c->d_scan = nullptr;
+        c->scan_cap = 0;
+        AGNES_TRY(hipMalloc(&c->d_scan, words * sizeof(uint64_t)));
+        c->scan_cap = words;
+    }
+    AGNES_TRY(hipMemcpyAsync(offsets + 1, counts, sizeof(uint64_t) * b->n_instances, hipMemcpyDeviceToDevice, st));
+    {
+        AgnesKt kt("edge_scan", st);
+        AGNES_TRY(agnes_launch_offsets_scan(offsets, b->n_instances, c->d_scan, st));
+    }
+    if (!out) return AGNES_OK;
+    return status_of(agnes_launch_edge_compact(b, seg, offsets, out, st));
 }
 
 int agnes_records_compact(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, const uint64_t* counts,

@@ -117,6 +117,60 @@ __global__ __launch_bounds__(64) void edge_walk(EdgeArgs a) {
     if (!EMIT) a.offs[i + 1u] = cnt;
 }
 
+/* the segmented edges (agnes_tally_edges) of every instance, or of the ones on a list
+ * (the flow route's walk list): instance i's at out[offsets[i] + k], k < counts[i]
+ * (a vote is at most one edge), one lane per instance, the same walk */
+template <bool LIST>
+__global__ __launch_bounds__(64) void edge_seg_walk(EdgeArgs a, const uint32_t* list, const uint32_t* list_n,
+                                                    uint64_t* counts) {
+    uint32_t* const tab = reinterpret_cast<uint32_t*>(agnes_smem);
+    const uint32_t lane = threadIdx.x;
+    uint32_t i;
+    if (LIST) {
+        const uint32_t k = blockIdx.x * 64u + lane;
+        if (k >= *(volatile const uint32_t*)list_n) return;
+        i = list[k];
+    } else {
+        i = blockIdx.x * 64u + lane;
+        if (i >= a.vb.n_instances) return;
+    }
+    for (uint32_t s = 0; s < a.nslots; ++s) tab[s * 64u + lane] = 0u; /* VoteCount::new: level 0 */
+    const uint64_t NV = a.vb.n_votes;
+    uint64_t lo = a.vb.offsets[i], hi = a.vb.offsets[i + 1u];
+    lo = lo < NV ? lo : NV;
+    hi = hi < NV ? hi : NV;
+    agnes_edge* const out = a.out + a.vb.offsets[i];
+    uint64_t cnt = 0;
+    for (uint64_t j = lo; j < hi; ++j) {
+        const uint32_t cb = a.codes[j], rb = a.vb.round[j], tb = a.vb.type[j];
+        const uint32_t ev = cb & AGNES_CODE_EVENT_MASK, key = rb * 2u + tb;
+        if (ev == AGNES_CODE_INVALID || ev == AGNES_CODE_REJECTED || tb > 1u || key >= a.keys) continue;
+        uint32_t* const p = tab + (key >> 2) * 64u + lane;
+        const uint32_t x = *p, sh = 8u * (key & 3u), old = (x >> sh) & 0xFFu;
+        const uint32_t msg = cb >> AGNES_CODE_MSG_SHIFT;
+        const uint32_t nb = (cb & 0xFu) | (msg ? msg << AGNES_CODE_MSG_SHIFT : old & 0xF0u);
+        if (nb != old) {
+            *reinterpret_cast<uint4*>(out + cnt) = make_uint4((uint32_t)j, (uint32_t)(j >> 32), i,
+                                                              rb | (tb << 8) | (cb << 16) | (old << 24));
+            ++cnt;
+            *p = x ^ ((old ^ nb) << sh);
+        }
+    }
+    counts[i] = cnt;
+}
+
+/* the dense summary from the segmented one: wave w copies instances 32w .. 32w + 31 */
+__global__ __launch_bounds__(256) void edge_compact(agnes_vote_batch vb, const agnes_edge* seg, const uint64_t* offs,
+                                                    agnes_edge* out) {
+    const uint32_t lane = threadIdx.x & 63u, w = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t n = vb.n_instances;
+    for (uint32_t i = 32u * w; i < n && i < 32u * w + 32u; ++i) {
+        const uint64_t o = offs[i], cnt = offs[i + 1u] - o;
+        const uint4* const src = reinterpret_cast<const uint4*>(seg + vb.offsets[i]);
+        for (uint64_t k = lane; k < cnt; k += 64u) reinterpret_cast<uint4*>(out + o)[k] = src[k];
+    }
+}
+
 /* window of the aligned path: 64 B per column (four 16-B loads of one 128-B line
  * issued together, so the line is fetched once although the wave's 64 lanes read
  * 64 different lines) */
@@ -242,5 +296,31 @@ hipError_t agnes_launch_edges(const agnes_vote_batch* vb, const uint8_t* codes, 
         if (w16) hipLaunchKernelGGL((edge_walk<true, EW, false>), grid, blk, lds, st, a);
         else hipLaunchKernelGGL((edge_walk<true, 4u, false>), grid, blk, lds, st, a);
     }
+    return hipGetLastError();
+}
+
+hipError_t agnes_launch_edge_seg_walk(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds,
+                                      const uint32_t* list, const uint32_t* list_n, uint64_t* counts, agnes_edge* seg,
+                                      hipStream_t st) {
+    using namespace agnes::edges;
+    const uint32_t n = vb->n_instances;
+    if (n == 0) return hipSuccess;
+    EdgeArgs a{*vb, codes, nullptr, seg, 2u * max_rounds, (2u * max_rounds + 3u) / 4u};
+    const size_t lds = (size_t)a.nslots * 64u * sizeof(uint32_t);
+    AgnesKt kt("edge_seg_walk", st);
+    if (list)
+        hipLaunchKernelGGL((edge_seg_walk<true>), dim3((n + 63u) / 64u), dim3(64), lds, st, a, list, list_n, counts);
+    else
+        hipLaunchKernelGGL((edge_seg_walk<false>), dim3((n + 63u) / 64u), dim3(64), lds, st, a, list, list_n, counts);
+    return hipGetLastError();
+}
+
+hipError_t agnes_launch_edge_compact(const agnes_vote_batch* vb, const agnes_edge* seg, const uint64_t* offs,
+                                     agnes_edge* out, hipStream_t st) {
+    const uint32_t n = vb->n_instances;
+    if (n == 0) return hipSuccess;
+    const uint32_t waves = (n + 31u) / 32u, blocks = (waves + 3u) / 4u;
+    AgnesKt kt("edge_compact", st);
+    hipLaunchKernelGGL(agnes::edges::edge_compact, dim3(blocks), dim3(256), 0, st, *vb, seg, offs, out);
     return hipGetLastError();
 }

@@ -116,9 +116,9 @@ __host__ __device__ inline uint32_t carry_bytes(uint32_t R, bool w64 = false) {
 }
 /* per-wave LDS: DMA slot | carried executors (2 copies x (vw[2R], vn[2R]) u32, or u64
  * for W64) | instance records | (State machine) valid candidates, two batches' staged States */
-__host__ __device__ inline uint32_t lds_bytes(bool sm, uint32_t R, bool evc = false, bool w64 = false) {
+__host__ __device__ inline uint32_t lds_bytes(bool sm, uint32_t R, bool evc = false, bool w64 = false, bool edg = false) {
     return F_BYTES + carry_bytes(R, w64) + FB * (w64 ? RECW64 : RECW) * 4u + (sm ? FB * 8u + 2u * FB * 64u : 0u) +
-           (evc ? FB * 4u : 0u);
+           (evc ? FB * 4u : 0u) + (edg ? (uint32_t)align16(FB * 2ull * R) : 0u);
 }
 
 /* a State out (plain stores: non-temporal ones measured slower on C2) */
@@ -244,9 +244,15 @@ __device__ __attribute__((noinline)) uint32_t label_back(const uint32_t* inst_co
 #ifndef AGNES_FLOW_WPE
 #define AGNES_FLOW_WPE 3
 #endif
-template <bool PC, bool SM, bool R1, bool EVC, bool W64, bool REC = false>
+/* REC (agnes_tally_records): the event records themselves, segmented by instance.
+ * EDG (agnes_tally_edges): the edge summary instead -- etab counts each instance's
+ * edges and the 16-B agnes_edge records go to the instance's segment (agnes_edges.hip's
+ * definition, orc_edges: a valid vote is an edge when its executor's state, level |
+ * last message << 4, changes). */
+template <bool PC, bool SM, bool R1, bool EVC, bool W64, bool REC = false, bool EDG = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES_FLOW_W64_WPE : AGNES_FLOW_WPE))) void flow(agnes_tally_args a, uint32_t lds_per_wave) {
     static_assert(!REC || (EVC && !W64), "records: with the record counts, u32 sums");
+    static_assert(!EDG || (EVC && !W64 && !REC), "edges: the counts are the edges', u32 sums");
     constexpr uint32_t RW = W64 ? RECW64 : RECW; /* record words */
 
     const uint32_t lane = lane_id();
@@ -279,6 +285,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
     unsigned char* const sb = base + F_BYTES + CB + FB * RW * 4u + FB * 8u;
     uint32_t* const etab = reinterpret_cast<uint32_t*>(base + F_BYTES + CB + FB * RW * 4u +
                                                        (SM ? FB * 8u + 2u * FB * 64u : 0u)); /* (EVC) records */
+    /* (EDG) each executor's edge state after the votes so far, [instance][round * 2 + type] bytes */
+    unsigned char* const elab = reinterpret_cast<unsigned char*>(etab + FB);
     const agnes_state* const st_in = a.states_in ? a.states_in : a.states;
     uint32_t cpar = 0;
     uint64_t pf_at = ~0ull;
@@ -555,6 +563,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                     rk[R_DR] = 0u;
                     if (SM) vtab[lane] = 0ull;
                     if (EVC) etab[lane] = 0u;
+                    if (EDG) {
+                        for (uint32_t q = 0; q < 2u * R; ++q) elab[lane * 2u * R + q] = 0u; /* VoteCount::new, no message */
+                    }
                 }
                 if (SM && smf) { /* the State machine's view of each instance (state_machine.rs:184) */
                     if (lane < m) {
@@ -1350,7 +1361,206 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                     }
                 }
 
-                if (EVC) { /* records per unit: the votes whose event is Some (codes 1..5) */
+                if constexpr (EDG) {
+                    /* ---- the edge summary (agnes_tally_edges): a valid vote is an edge when its
+                     * executor's state -- code bits 0..3 | the last non-zero message << 4 --
+                     * changes (orc_edges; the HeightVotes stub, consensus_executor.rs:5).  Its
+                     * state before it: the previous valid vote of its executor for the low nibble,
+                     * the last one with a message for the high one -- in the lane, else (one
+                     * round, or runs: one executor per type per segment) the last earlier lane of
+                     * the segment holding one, else the executor's state carried in LDS (elab);
+                     * rounds revisited in the chunk: the same per (instance, round, type) key. ---- */
+                    const uint32_t vl0 = actA ? okb0 : 0u, vl1 = actB ? okb1 : 0u; /* 0xFF: valid votes */
+                    const bool fast = R1 || runs;
+                    const bool spl = R1 ? split : splitr;
+                    const uint32_t K2 = 2u * R;
+                    uint32_t prv[LV], nw[LV];
+                    uint32_t pendL = 0u, pendH = 0u;
+                    /* per class (fast: a vote type within the segment; slow: one key), in stream order */
+                    auto cls = [&](uint32_t q) -> uint32_t { /* the vote's key: instance k, round, type */
+                        const uint32_t bs = 8u * (q & 3u);
+                        const uint32_t r = ((q < 4u ? r8[0] : r8[1]) >> bs) & 0xFFu, t = ((q < 4u ? t8[0] : t8[1]) >> bs) & 1u;
+                        return (q < 4u ? kA : kB) * K2 + 2u * r + t;
+                    };
+                    {
+                        bool hl0 = false, hl1 = false, hm0 = false, hm1 = false;
+                        uint32_t ll0 = 0u, ll1 = 0u, lm0 = 0u, lm1 = 0u;
+#pragma unroll
+                        for (uint32_t q = 0; q < LV; ++q) {
+                            if (q == 4u && spl) { hl0 = hl1 = hm0 = hm1 = false; }
+                            const uint32_t bs = 8u * (q & 3u);
+                            const bool v = (((q < 4u ? vl0 : vl1) >> bs) & 1u) != 0u;
+                            const bool tq = (((q < 4u ? t8[0] : t8[1]) >> bs) & 1u) != 0u;
+                            const uint32_t cb = ((q < 4u ? c0 : c1) >> bs) & 0xFFu;
+                            const bool hl = fast && (tq ? hl1 : hl0), hm = fast && (tq ? hm1 : hm0);
+                            prv[q] = (hl ? (tq ? ll1 : ll0) : 0u) | (hm ? ((tq ? lm1 : lm0) << 4) : 0u);
+                            pendL |= (v && !hl) ? 1u << q : 0u;
+                            pendH |= (v && !hm) ? 1u << q : 0u;
+                            if (v) {
+                                if (tq) { hl1 = true; ll1 = cb & 0xFu; } else { hl0 = true; ll0 = cb & 0xFu; }
+                                if (cb >> 4) {
+                                    if (tq) { hm1 = true; lm1 = cb >> 4; } else { hm0 = true; lm0 = cb >> 4; }
+                                }
+                            }
+                        }
+                        if (fast && ballot((pendL | pendH) != 0u)) {
+                            /* the last earlier lane of the segment with a valid vote / a message of the type */
+                            const uint32_t sx = R1 ? (multi ? sA : 0u) : (multir ? sAr : 0u);
+                            const uint64_t segm = (((1ull << lane) - 1ull) >> sx) << sx;
+                            const uint64_t L0 = ballot(hl0) & segm, L1 = ballot(hl1) & segm;
+                            const uint64_t M0 = ballot(hm0) & segm, M1 = ballot(hm1) & segm;
+                            const uint32_t fl0 = shfl(ll0, L0 ? 63u - (uint32_t)__builtin_clzll(L0) : 0u);
+                            const uint32_t fl1 = shfl(ll1, L1 ? 63u - (uint32_t)__builtin_clzll(L1) : 0u);
+                            const uint32_t fm0 = shfl(lm0, M0 ? 63u - (uint32_t)__builtin_clzll(M0) : 0u);
+                            const uint32_t fm1 = shfl(lm1, M1 ? 63u - (uint32_t)__builtin_clzll(M1) : 0u);
+#pragma unroll
+                            for (uint32_t q = 0; q < LV; ++q) {
+                                const bool pl = (pendL >> q) & 1u, ph = (pendH >> q) & 1u;
+                                if (!pl && !ph) continue;
+                                const bool tq = (((q < 4u ? t8[0] : t8[1]) >> (8u * (q & 3u))) & 1u) != 0u;
+                                const bool cross = q < 4u || !spl;
+                                const bool gl = cross && (tq ? L1 : L0) != 0ull, gm = cross && (tq ? M1 : M0) != 0ull;
+                                const uint32_t car = (pl && !gl) || (ph && !gm) ? elab[cls(q)] : 0u;
+                                if (pl) prv[q] |= gl ? (tq ? fl1 : fl0) : (car & 0xFu);
+                                if (ph) prv[q] |= gm ? ((tq ? fm1 : fm0) << 4) : (car & 0xF0u);
+                            }
+                            pendL = pendH = 0u;
+                        }
+                    }
+                    if (!fast) {
+                        /* rounds revisited in the chunk: one key at a time (its valid votes) */
+                        pendL = pendH = 0u;
+                        uint32_t todo = 0u;
+#pragma unroll
+                        for (uint32_t q = 0; q < LV; ++q) todo |= (((q < 4u ? vl0 : vl1) >> (8u * (q & 3u))) & 1u) << q;
+                        for (;;) {
+                            const uint64_t lm = ballot(todo != 0u);
+                            if (!lm) break;
+                            const uint32_t kl = (uint32_t)__builtin_ctzll(lm);
+                            const uint32_t ks = (uint32_t)__builtin_ctz(rdl(todo, kl));
+                            uint32_t mykey = cls(0u);
+#pragma unroll
+                            for (uint32_t q = 1; q < LV; ++q) mykey = ks == q ? cls(q) : mykey;
+                            const uint32_t KY = rdl(mykey, kl);
+                            bool hl = false, hm = false;
+                            uint32_t ll = 0u, lmx = 0u, inb = 0u;
+#pragma unroll
+                            for (uint32_t q = 0; q < LV; ++q) {
+                                if (!((todo >> q) & 1u) || cls(q) != KY) continue;
+                                inb |= 1u << q;
+                                const uint32_t cb = ((q < 4u ? c0 : c1) >> (8u * (q & 3u))) & 0xFFu;
+                                prv[q] = (hl ? ll : 0u) | (hm ? lmx << 4 : 0u);
+                                pendL |= hl ? 0u : 1u << q;
+                                pendH |= hm ? 0u : 1u << q;
+                                hl = true;
+                                ll = cb & 0xFu;
+                                if (cb >> 4) { hm = true; lmx = cb >> 4; }
+                            }
+                            todo &= ~inb;
+                            const uint64_t below = (1ull << lane) - 1ull;
+                            const uint64_t L = ballot(hl) & below, M = ballot(hm) & below;
+                            const uint32_t fl = shfl(ll, L ? 63u - (uint32_t)__builtin_clzll(L) : 0u);
+                            const uint32_t fm = shfl(lmx, M ? 63u - (uint32_t)__builtin_clzll(M) : 0u);
+                            const uint32_t car = elab[KY];
+#pragma unroll
+                            for (uint32_t q = 0; q < LV; ++q) {
+                                if (!((inb >> q) & 1u)) continue;
+                                if ((pendL >> q) & 1u) prv[q] |= L ? fl : (car & 0xFu);
+                                if ((pendH >> q) & 1u) prv[q] |= M ? (fm << 4) : (car & 0xF0u);
+                            }
+                            pendL &= ~inb;
+                            pendH &= ~inb;
+                            /* the key's state after the chunk: its last vote's (the highest lane with one) */
+                            uint32_t fin = 0u;
+#pragma unroll
+                            for (uint32_t q = 0; q < LV; ++q) {
+                                if (!((inb >> q) & 1u)) continue;
+                                const uint32_t cb = ((q < 4u ? c0 : c1) >> (8u * (q & 3u))) & 0xFFu;
+                                fin = (cb & 0xFu) | ((cb >> 4) ? (cb & 0xF0u) : (prv[q] & 0xF0u));
+                            }
+                            const uint64_t H2 = ballot(inb != 0u);
+                            const uint32_t hl2 = 63u - (uint32_t)__builtin_clzll(H2);
+                            const uint32_t fv = rdl(fin, hl2);
+                            __builtin_amdgcn_wave_barrier();
+                            if (lane == 0u) elab[KY] = (unsigned char)fv;
+                            __builtin_amdgcn_wave_barrier();
+                        }
+                    }
+                    /* the new states and the edges */
+                    uint32_t em0 = 0u, em1 = 0u; /* 0x80 in the bytes of the edges */
+#pragma unroll
+                    for (uint32_t q = 0; q < LV; ++q) {
+                        const uint32_t bs = 8u * (q & 3u);
+                        const uint32_t cb = ((q < 4u ? c0 : c1) >> bs) & 0xFFu;
+                        nw[q] = (cb & 0xFu) | ((cb >> 4) ? (cb & 0xF0u) : (prv[q] & 0xF0u));
+                        const bool v = (((q < 4u ? vl0 : vl1) >> bs) & 1u) != 0u;
+                        const uint32_t e = (v && nw[q] != prv[q]) ? 0x80u << bs : 0u;
+                        if (q < 4u) em0 |= e;
+                        else em1 |= e;
+                    }
+                    if (fast) {
+                        /* each (segment, type)'s last vote in the chunk carries the executor's state
+                         * out (elab): a vote is its last unless a later one of the lane, or the first of
+                         * that type in the next lane holding one, is in the same segment */
+                        const uint32_t segA = R1 ? kA : (kA * 16u + uA), segB = R1 ? kB : (kB * 16u + uB);
+                        uint32_t has0 = 0u, has1 = 0u, f0 = 0xFFFFFFFFu, f1 = 0xFFFFFFFFu;
+#pragma unroll
+                        for (uint32_t q = 0; q < LV; ++q) {
+                            const uint32_t bs = 8u * (q & 3u);
+                            const bool v = (((q < 4u ? vl0 : vl1) >> bs) & 1u) != 0u;
+                            const bool tq = (((q < 4u ? t8[0] : t8[1]) >> bs) & 1u) != 0u;
+                            const uint32_t sg = q < 4u ? segA : segB;
+                            if (v && tq) { f1 = has1 ? f1 : sg; has1 = 1u; }
+                            if (v && !tq) { f0 = has0 ? f0 : sg; has0 = 1u; }
+                        }
+                        const uint64_t above = ~((2ull << lane) - 1ull);
+                        const uint64_t N0 = ballot(has0 != 0u) & above, N1 = ballot(has1 != 0u) & above;
+                        uint32_t nx0 = shfl(f0, N0 ? (uint32_t)__builtin_ctzll(N0) : lane);
+                        uint32_t nx1 = shfl(f1, N1 ? (uint32_t)__builtin_ctzll(N1) : lane);
+                        nx0 = N0 ? nx0 : 0xFFFFFFFFu;
+                        nx1 = N1 ? nx1 : 0xFFFFFFFFu;
+#pragma unroll
+                        for (int q = (int)LV - 1; q >= 0; --q) {
+                            const uint32_t bs = 8u * ((uint32_t)q & 3u);
+                            const bool v = ((((uint32_t)q < 4u ? vl0 : vl1) >> bs) & 1u) != 0u;
+                            if (!v) continue;
+                            const bool tq = ((((uint32_t)q < 4u ? t8[0] : t8[1]) >> bs) & 1u) != 0u;
+                            const uint32_t sg = (uint32_t)q < 4u ? segA : segB;
+                            if ((tq ? nx1 : nx0) != sg) elab[cls((uint32_t)q)] = (unsigned char)nw[q];
+                            if (tq) nx1 = sg; else nx0 = sg;
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                    }
+                    /* counts (etab) and the records at the instance's segment */
+                    const uint32_t nA = (uint32_t)__builtin_popcount(em0), nB = (uint32_t)__builtin_popcount(em1);
+                    if (ballot((nA | nB) != 0u)) {
+                        const uint32_t Tn = split ? nB : nA + nB;
+                        const uint32_t En = scan(Tn) - Tn;
+                        const uint32_t rA = etab[kA] + En - (multi ? shfl(En, sA) : 0u);
+                        const uint32_t rB = split ? etab[kB] : rA + nA;
+                        const uint64_t gA = Sa + shfl(rl, kA), gB = Sa + shfl(rl, kB);
+#pragma unroll
+                        for (uint32_t q = 0; q < LV; ++q) {
+                            const uint32_t bs = 8u * (q & 3u);
+                            const uint32_t em = q < 4u ? em0 : em1;
+                            if ((em >> (bs + 7u)) & 1u) {
+                                const uint32_t k = (q < 4u ? rA : rB) + (uint32_t)__builtin_popcount(em & ((1u << bs) - 1u));
+                                const uint32_t cb = ((q < 4u ? c0 : c1) >> bs) & 0xFFu;
+                                const uint32_t rq = ((q < 4u ? r8[0] : r8[1]) >> bs) & 0xFFu;
+                                const uint32_t tq = ((q < 4u ? t8[0] : t8[1]) >> bs) & 1u;
+                                const uint64_t j = c + o8 + q;
+                                const uint4 rec = make_uint4((uint32_t)j, (uint32_t)(j >> 32), H.s0 + (q < 4u ? kA : kB),
+                                                             rq | (tq << 8) | (cb << 16) | (prv[q] << 24));
+                                reinterpret_cast<uint4*>(a.rec_out)[(q < 4u ? gA : gB) + k] = rec;
+                            }
+                        }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    atomicAdd(etab + kA, kA == kB ? nA + nB : nA);
+                    atomicAdd(etab + kB, kA == kB ? 0u : nB);
+                }
+
+                if (EVC && !EDG) { /* records per unit: the votes whose event is Some (codes 1..5) */
                     auto recs = [](uint32_t cw4) -> uint32_t {
                         const uint32_t e = cw4 & 0x07070707u;
                         const uint32_t nz = (e + 0x7F7F7F7Fu) & 0x80808080u; /* event != None        */
@@ -1422,14 +1632,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
 /* ------------------------------------------------------------------ */
 /* launcher                                                            */
 
-template <bool SM, bool R1, bool EVC, bool W64, bool REC = false>
+template <bool SM, bool R1, bool EVC, bool W64, bool REC = false, bool EDG = false>
 static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStream_t st) {
     const uint32_t n = a->vb.n_instances;
     if (n == 0) return hipSuccess;
     using agnes::flow::flow;
-    const void* fns[2] = {reinterpret_cast<const void*>(&flow<false, SM, R1, EVC, W64, REC>),
-                          reinterpret_cast<const void*>(&flow<true, SM, R1, EVC, W64, REC>)};
-    const uint32_t lpw = agnes::flow::lds_bytes(SM, a->max_rounds, EVC, W64);
+    const void* fns[2] = {reinterpret_cast<const void*>(&flow<false, SM, R1, EVC, W64, REC, EDG>),
+                          reinterpret_cast<const void*>(&flow<true, SM, R1, EVC, W64, REC, EDG>)};
+    const uint32_t lpw = agnes::flow::lds_bytes(SM, a->max_rounds, EVC, W64, EDG);
     const uint64_t wave_lds = (uint64_t)lpw * AGNES_WAVES_PER_BLOCK;
     const uint64_t pcb = agnes::align16((W64 ? 8ull : 4ull) * a->n_sets * a->n_vals);
     /* blocks per CU from the occupancy query; the LDS power table only where it
@@ -1492,8 +1702,8 @@ static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStrea
     const uint64_t cap = ncu * (uint64_t)o->per_cu;
     if (blocks > cap) blocks = cap;
     if (blocks == 0) blocks = 1;
-    if (o->pc) hipLaunchKernelGGL((flow<true, SM, R1, EVC, W64, REC>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
-    else hipLaunchKernelGGL((flow<false, SM, R1, EVC, W64, REC>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
+    if (o->pc) hipLaunchKernelGGL((flow<true, SM, R1, EVC, W64, REC, EDG>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
+    else hipLaunchKernelGGL((flow<false, SM, R1, EVC, W64, REC, EDG>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
     return hipGetLastError();
 }
 
@@ -1511,13 +1721,13 @@ bool agnes_flow_supported(const agnes_tally_args* a) {
      * kernel's allow 2) */
     const bool sm = (a->flags & AGNES_FLAG_STATE_MACHINE) != 0 && a->states != nullptr;
     const uint32_t waves = a->w64 ? 8u : (sm ? 12u : 16u);
-    return a->max_rounds <= 15u &&
-           agnes::flow::lds_bytes(sm, a->max_rounds, a->ev_counts != nullptr, a->w64 != 0u) * waves <= 160u * 1024u;
+    return a->max_rounds <= 15u && agnes::flow::lds_bytes(sm, a->max_rounds, a->ev_counts != nullptr, a->w64 != 0u,
+                                                          a->edges != 0u) * waves <= 160u * 1024u;
 }
 
-bool agnes_flow_counts_events(uint32_t flags, uint32_t max_rounds) {
+bool agnes_flow_counts_events(uint32_t flags, uint32_t max_rounds, bool edges) {
     const bool sm = (flags & AGNES_FLAG_STATE_MACHINE) != 0;
-    return max_rounds <= 15u && agnes::flow::lds_bytes(sm, max_rounds, true) * (sm ? 12u : 16u) <= 160u * 1024u;
+    return max_rounds <= 15u && agnes::flow::lds_bytes(sm, max_rounds, true, false, edges) * (sm ? 12u : 16u) <= 160u * 1024u;
 }
 
 hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t st) {
@@ -1527,6 +1737,14 @@ hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t
         if (a->max_rounds == 1u)
             return sm ? launch_flow_k<true, true, false, true>(a, num_cus, st) : launch_flow_k<false, true, false, true>(a, num_cus, st);
         return sm ? launch_flow_k<true, false, false, true>(a, num_cus, st) : launch_flow_k<false, false, false, true>(a, num_cus, st);
+    }
+    if (a->rec_out && a->edges) { /* agnes_tally_edges: the edge counts and records */
+        if (!a->ev_counts) return hipErrorInvalidValue;
+        if (a->max_rounds == 1u)
+            return sm ? launch_flow_k<true, true, true, false, false, true>(a, num_cus, st)
+                      : launch_flow_k<false, true, true, false, false, true>(a, num_cus, st);
+        return sm ? launch_flow_k<true, false, true, false, false, true>(a, num_cus, st)
+                  : launch_flow_k<false, false, true, false, false, true>(a, num_cus, st);
     }
     if (a->rec_out) { /* agnes_tally_records: counts and the records themselves */
         if (!a->ev_counts) return hipErrorInvalidValue;

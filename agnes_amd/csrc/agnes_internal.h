@@ -67,6 +67,7 @@ typedef struct agnes_tally_args {
     uint32_t tail_n;      /* flow: instances in the tail (the last ones)                        */
     uint32_t w64;         /* the u64 fast domain (agnes_set_info.w64 sets outside the u32 one):
                              tally_fast with u64 sums, the apply pass tests the same deferral */
+    uint32_t edges;       /* agnes_tally_edges: ev_counts / rec_out are the edge summary's (EDG) */
     void* rec_out;        /* optional (agnes_tally_records): agnes_seg_event [n_votes], instance i's
                              records at [offsets[i], offsets[i] + ev_counts[i]) -- the flow
                              kernel writes them (REC); every other route's emit pass does */
@@ -112,8 +113,14 @@ hipError_t agnes_launch_seg_walk(const agnes_vote_batch* vb, const uint8_t* code
                                  hipStream_t stream);
 hipError_t agnes_launch_seg_compact(const agnes_vote_batch* vb, uint32_t mult, const void* seg, const uint64_t* offs,
                                     agnes_vote_event* out, hipStream_t stream);
+/* the same for the edge summary (agnes_tally_edges / agnes_edges_compact) */
+hipError_t agnes_launch_edge_seg_walk(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds,
+                                      const uint32_t* list, const uint32_t* list_n, uint64_t* counts, agnes_edge* seg,
+                                      hipStream_t stream);
+hipError_t agnes_launch_edge_compact(const agnes_vote_batch* vb, const agnes_edge* seg, const uint64_t* offs,
+                                     agnes_edge* out, hipStream_t stream);
 /* the flow kernel can count event records (agnes_tally_events) in this configuration */
-bool agnes_flow_counts_events(uint32_t flags, uint32_t max_rounds);
+bool agnes_flow_counts_events(uint32_t flags, uint32_t max_rounds, bool edges = false);
 /* the batched State::apply pass over the codes a tally kernel left (agnes_apply.hip):
  * one instance per lane, skipping the instances deferred to the LIST kernel */
 bool agnes_apply_codes_supported(const agnes_tally_args* a);

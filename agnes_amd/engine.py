@@ -207,6 +207,43 @@ class Engine:
               "agnes_records_compact")
         return offsets, out
 
+    def tally_edges(self, cfg: abi.Config, batch: DeviceBatch, codes: torch.Tensor,
+                    states_in: Optional[torch.Tensor] = None, states_out: Optional[torch.Tensor] = None,
+                    counts: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, stream=None):
+        """agnes_tally_edges: the tally (as tally_states) and its edge summary segmented by
+        instance: counts int64 [n_instances], out uint8 [n_votes, 16] (instance i's edges
+        at rows offsets[i] .. offsets[i] + counts[i]; view a host copy as abi.EDGE_DTYPE).
+        Allocated when None; no sync."""
+        if codes.dtype != torch.uint8 or codes.numel() < batch.n_votes:
+            raise ValueError("codes must be a uint8 tensor of n_votes")
+        for t in (states_in, states_out):
+            if t is not None and t.numel() < 64 * batch.n_instances:
+                raise ValueError("states must hold n_instances 64-byte records")
+        if counts is None:
+            counts = torch.empty(max(batch.n_instances, 1), dtype=torch.int64, device=self.device)
+        if out is None:
+            out = torch.empty((max(batch.n_votes, 1), 16), dtype=torch.uint8, device=self.device)
+        if counts.numel() < batch.n_instances or out.numel() < 16 * batch.n_votes:
+            raise ValueError("counts must hold n_instances, out n_votes records")
+        b = batch.c()
+        check(self.lib.agnes_tally_edges(self.ctx, C.byref(cfg), C.byref(b), _ptr(codes), _ptr(states_in),
+                                         _ptr(states_out), _ptr(counts), _ptr(out), _stream_handle(stream)),
+              "agnes_tally_edges")
+        return counts, out
+
+    def edges_compact(self, cfg: abi.Config, batch: DeviceBatch, counts: torch.Tensor, seg: torch.Tensor,
+                      offsets: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, stream=None):
+        """agnes_edges_compact: offsets int64 [n_instances + 1] and the dense agnes_edge
+        records (uint8 [n_votes, 16]); allocated when None."""
+        if offsets is None:
+            offsets = torch.empty(batch.n_instances + 1, dtype=torch.int64, device=self.device)
+        if out is None:
+            out = torch.empty((max(batch.n_votes, 1), 16), dtype=torch.uint8, device=self.device)
+        b = batch.c()
+        check(self.lib.agnes_edges_compact(self.ctx, C.byref(cfg), C.byref(b), _ptr(counts), _ptr(seg),
+                                           _ptr(offsets), _ptr(out), _stream_handle(stream)), "agnes_edges_compact")
+        return offsets, out
+
     def events_capacity(self, cfg: abi.Config, batch: DeviceBatch) -> int:
         b = batch.c()
         return int(self.lib.agnes_events_capacity(C.byref(cfg), C.byref(b)))

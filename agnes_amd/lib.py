@@ -96,6 +96,8 @@ def load():
         "agnes_events_capacity": ([C.POINTER(abi.Config), C.POINTER(abi.VoteBatch)], C.c_uint64),
         "agnes_tally_records": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P, P, P], C.c_int),
         "agnes_records_compact": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P, P], C.c_int),
+        "agnes_tally_edges": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P, P, P], C.c_int),
+        "agnes_edges_compact": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P, P], C.c_int),
         "agnes_dedup_first": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), C.c_uint64, P, P], C.c_int),
         "agnes_dedup_mask": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), C.c_uint64, P, P, P],
                              C.c_int),

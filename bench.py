@@ -329,6 +329,58 @@ def tally_events_timed(eng, cfg, batch, codes, st0, states, steps, ref_offs, ref
             "kernels": {name: {"launches": k, "avg_ms": t / max(k, 1)} for name, (k, t) in kt.items()}}
 
 
+def tally_edges_timed(eng, cfg, batch, codes, st0, states, steps, ref_offs, ref_recs):
+    """agnes_tally_edges (round 5): the step and its edge summary segmented by instance,
+    found and written by the flow kernel (no pass over the codes), graph-captured and
+    timed like the step outside the timed region of `value`; agnes_edges_compact's dense
+    layout must equal the two-call summary's (ref_offs / ref_recs) byte for byte."""
+    counts = torch.empty(max(batch.n_instances, 1), dtype=torch.int64, device=eng.device)
+    seg = torch.empty((max(batch.n_votes, 1), 16), dtype=torch.uint8, device=eng.device)
+
+    def call():
+        eng.tally_edges(cfg, batch, codes, st0, states, counts, seg)
+
+    call()
+    torch.cuda.synchronize()
+    eng.kernel_timing(True)
+    for _ in range(3):
+        call()
+    torch.cuda.synchronize()
+    kt = eng.kernel_times()
+    eng.kernel_timing(False)
+    ms = graph_timed(call, steps)
+    offs = torch.empty(batch.n_instances + 1, dtype=torch.int64, device=eng.device)
+    dense = torch.empty((max(batch.n_votes, 1), 16), dtype=torch.uint8, device=eng.device)
+    ms_c = graph_timed(lambda: eng.edges_compact(cfg, batch, counts, seg, offs, dense), steps)
+    n = int(offs[-1].item())
+    equal = bool(torch.equal(offs, ref_offs) and torch.equal(dense[:n], ref_recs))
+    del seg, dense
+    return {"ms_per_call": ms, "compact_ms": ms_c, "edges": n, "compacted_equal_to_two_call_summary": equal,
+            "kernels": {name: {"launches": k, "avg_ms": t / max(k, 1)} for name, (k, t) in kt.items()}}
+
+
+def graph_timed(fn, steps):
+    """ms per call of fn captured in a HIP graph and replayed steps times"""
+    fn()
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        fn()
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        fn()
+    g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.replay()
+    torch.cuda.synchronize()
+    del g
+    return (time.perf_counter() - t0) * 1e3 / steps
+
+
 def tally_records_timed(eng, cfg, batch, codes, st0, states, steps, ref_offs, ref_recs):
     """agnes_tally_records (round 5): the step and its records SEGMENTED by instance, the
     flow kernel writing them while the votes are in registers (no pass over the votes
@@ -342,26 +394,6 @@ def tally_records_timed(eng, cfg, batch, codes, st0, states, steps, ref_offs, re
     def call():
         eng.tally_records(cfg, batch, codes, st0, states, counts, seg)
 
-    def timed(fn):
-        fn()
-        torch.cuda.synchronize()
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            fn()
-        torch.cuda.current_stream().wait_stream(side)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=side):
-            fn()
-        g.replay()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            g.replay()
-        torch.cuda.synchronize()
-        del g
-        return (time.perf_counter() - t0) * 1e3 / steps
-
     call()
     torch.cuda.synchronize()
     eng.kernel_timing(True)
@@ -370,10 +402,10 @@ def tally_records_timed(eng, cfg, batch, codes, st0, states, steps, ref_offs, re
     torch.cuda.synchronize()
     kt = eng.kernel_times()
     eng.kernel_timing(False)
-    ms = timed(call)
+    ms = graph_timed(call, steps)
     offs = torch.empty(batch.n_instances + 1, dtype=torch.int64, device=eng.device)
     dense = torch.empty((max(cap, 1), 24), dtype=torch.uint8, device=eng.device)
-    ms_c = timed(lambda: eng.records_compact(cfg, batch, counts, seg, offs, dense))
+    ms_c = graph_timed(lambda: eng.records_compact(cfg, batch, counts, seg, offs, dense), steps)
     n = int(offs[-1].item())
     equal = bool(torch.equal(offs, ref_offs) and torch.equal(dense[:n], ref_recs))
     del seg, dense
@@ -492,6 +524,9 @@ def main():
     tr["records_ms"] = tr["ms_per_call"] - elapsed * 1e3 / args.steps
     events["tally_records"] = tr
     ed_offs = edges.pop("_offsets")
+    tg = tally_edges_timed(eng, cfg, batch, codes, st0, states, args.steps, ed_offs, edges["_records"])
+    tg["edges_ms"] = tg["ms_per_call"] - elapsed * 1e3 / args.steps  # over the tally step alone
+    edges["tally_edges"] = tg
     if world > 1:  # every rank's edge records to every rank (RCCL), outside the timed region
         edges["all_gather"] = adist.gather_edges_timed(edges.pop("_records"))
         ed_recs = None

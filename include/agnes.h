@@ -646,6 +646,20 @@ typedef struct agnes_edge {
     uint8_t prev;      /* the executor before this vote: level | last message << 4 */
 } agnes_edge;
 
+/* The tally and its edge summary in ONE call (round 5), SEGMENTED by instance: instance
+ * i's edges at out[offsets[i] + k], k < counts[i] (a vote is at most one edge), in vote
+ * order -- the records agnes_edges gives, at segment offsets.  On the flow route
+ * (REFERENCE without RoundSkip, max_rounds <= 15, offsets multiples of 4) the tally
+ * kernel finds and writes them while the votes are in registers, each executor's state
+ * carried in LDS: no pass over the codes.  counts (DEVICE, n_instances u64); out
+ * (DEVICE, 16-B aligned, n_votes records; offsets must not go back); max_rounds <= 128.  agnes_edges_compact
+ * gives the dense layout (offsets[n_instances + 1] from the counts; out, when not
+ * null, exactly agnes_edges'). */
+int agnes_tally_edges(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch, uint8_t* codes,
+                      const agnes_state* states_in, agnes_state* states_out, uint64_t* counts, agnes_edge* out,
+                      void* stream);
+int agnes_edges_compact(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch, const uint64_t* counts,
+                        const agnes_edge* seg, uint64_t* offsets, agnes_edge* out, void* stream);
 /* Pass 1: offsets (DEVICE, n_instances + 1): exclusive offsets of each instance's
  * edges, offsets[n_instances] = the total.  codes as agnes_tally left them
  * (DEVICE); votes with round >= cfg->max_rounds or type > 1 are never edges.
@@ -718,8 +732,10 @@ uint64_t agnes_events_capacity(const agnes_config* cfg, const agnes_vote_batch* 
  * between an instance's last record and the next segment are left as they were.  Every
  * other route (and the flow route's walk-list instances) writes them with an emit walk.
  * counts (DEVICE, n_instances u64); out (DEVICE, 16-B aligned) must hold
- * agnes_events_capacity(cfg, batch) records.  The record is agnes_vote_event without
- * the instance (the segment names it) and the padding. */
+ * agnes_events_capacity(cfg, batch) records; the segments are the instances' vote
+ * ranges, so offsets must not go back (overlapping ranges overlap their segments).
+ * The record is agnes_vote_event without the instance (the segment names it) and the
+ * padding. */
 typedef struct agnes_seg_event {
     uint64_t vote;    /* index of the vote in the batch                             */
     uint32_t value;   /* PolkaValue / PrecommitValue: the Value; else AGNES_NIL      */

@@ -186,3 +186,91 @@ def test_edges_offsets_going_back(eng, R):
     offs, recs = eng.edges(cfg, db, dc)
     torch.cuda.synchronize()
     _check(cfg, hb, codes, offs.cpu().numpy().view(np.uint64), recs.cpu().numpy().reshape(-1).view(abi.EDGE_DTYPE))
+
+
+# ------------------------------------------------ round 5: agnes_tally_edges (fused)
+
+def _tally_edges_check(eng, cfg, hb, power, states=None):
+    """agnes_tally_edges: the tally and its edge summary in one call, segmented by
+    instance (the flow kernel finds and writes them on the C2 / C3 route), against the
+    checker's codes, States and orc_edges over them; then agnes_edges_compact's dense
+    layout against orc_edges' offsets and records, byte for byte."""
+    eng.upload_power(power)
+    db = DeviceBatch.from_host(hb, eng.device)
+    n = max(hb.n_votes, 1)
+    codes = torch.full((n,), 0xEE, dtype=torch.uint8, device=eng.device)
+    dst = None if states is None else states_to_device(states, eng.device)
+    seg = torch.full((n, 16), 0xCD, dtype=torch.uint8, device=eng.device)
+    counts, seg = eng.tally_edges(cfg, db, codes, dst, dst, out=seg)
+    torch.cuda.synchronize()
+    o_codes, o_states, _ = ol.tally(cfg, hb, power, None, states, threads=8)
+    g_codes = codes[:hb.n_votes].cpu().numpy()
+    assert np.array_equal(g_codes, o_codes), "codes differ"
+    if states is not None:
+        from agnes_amd.engine import states_to_host
+        assert states_to_host(dst).tobytes() == o_states.tobytes(), "States differ"
+    o_offs, o_recs = ol.edges(cfg, hb, o_codes)
+    g_cnt = counts[:hb.n_instances].cpu().numpy().view(np.uint64)
+    o_cnt = np.diff(o_offs.astype(np.int64)).astype(np.uint64)
+    assert np.array_equal(g_cnt, o_cnt), f"edge counts differ (first at {np.nonzero(g_cnt != o_cnt)[0][:1]})"
+    g_seg = seg.cpu().numpy().reshape(-1).view(abi.EDGE_DTYPE)
+    off = hb.offsets.astype(np.int64)
+    idx = np.concatenate([np.arange(off[i], off[i] + int(o_cnt[i])) for i in range(hb.n_instances)]
+                         + [np.zeros(0, np.int64)]).astype(np.int64)
+    got = g_seg[idx]
+    if got.tobytes() != o_recs.tobytes():
+        k = int(np.nonzero(got != o_recs)[0][0])
+        raise AssertionError(f"segmented edge {k} of {len(o_recs)}: gpu {got[k]} checker {o_recs[k]}")
+    d_offs, dense = eng.edges_compact(cfg, db, counts, seg)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_offs.cpu().numpy().view(np.uint64), o_offs)
+    assert dense[:len(o_recs)].cpu().numpy().tobytes() == o_recs.tobytes()
+    return o_recs
+
+
+@pytest.mark.parametrize("name", ["c2_small", "c2_sm", "c3_small", "c4_small", "c4_ref_skip", "sorted_tiny_sets",
+                                  "many_rounds", "c2w_small"])
+def test_tally_edges_generated(eng, name):
+    p, hb, power, cfg = _make(name)
+    states = _start_states(p.n_instances) if cfg.flags & abi.FLAG_STATE_MACHINE else None
+    recs = _tally_edges_check(eng, cfg, hb, power, states)
+    assert len(recs) > 0
+
+
+@pytest.mark.parametrize("nil", [300, 700])
+def test_tally_edges_revisited_rounds(eng, nil):
+    """flow chunks that revisit rounds (5 % next-round votes, 300-vote rounds: offsets
+    stay multiples of 4): the per-key path of the fused edges"""
+    p = abi.gen_params(seed=63, n_instances=3000, n_vals=120, rounds_min=1, rounds_max=4, nil_permille=nil,
+                       dup_permille=100, equiv_permille=100, higher_permille=50)
+    hb = ol.gen_batch(p)
+    assert (hb.offsets % 4 == 0).all()
+    power = ol.gen_power(63, 7, 120, abi.POWER_UNIFORM, 1, 1000)
+    _tally_edges_check(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 5), hb, power,
+                       _start_states(3000))
+    _tally_edges_check(eng, abi.config(abi.MODE_REFERENCE, 0, 5), hb, power)
+
+
+def test_tally_edges_walk_list_and_empty(eng):
+    """ragged lengths (the flow kernel's walk list: the edge walk over the list), empty
+    instances, invalid votes, one instance, an empty batch"""
+    rng = np.random.default_rng(64)
+    lens = rng.integers(0, 90, 3000)
+    lens[::7] = 0
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    n = int(off[-1])
+    inst = np.repeat(np.arange(3000, dtype=np.uint32), lens)
+    rnd = np.sort(rng.integers(0, 3, n)).astype(np.uint8)
+    val = rng.integers(0, 5, n).astype(np.uint32)
+    val[rng.random(n) < 0.3] = abi.NIL
+    vdr = rng.integers(0, 10, n).astype(np.uint32)
+    inst[rng.random(n) < 0.02] += 1
+    hb = ol.batch_from_lists(inst, rnd, rng.integers(0, 2, n).astype(np.uint8), val, vdr, off)
+    power = ol.gen_power(64, 1, 10, abi.POWER_UNIFORM, 1, 10)
+    _tally_edges_check(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 3), hb, power,
+                       abi.new_states(3000, 1, abi.STEP_PREVOTE))
+    p1 = abi.gen_params(seed=65, n_instances=1, n_vals=100, rounds_min=1, rounds_max=1, nil_permille=200)
+    _tally_edges_check(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 1), ol.gen_batch(p1),
+                       ol.gen_power(65, 1, 100, abi.POWER_UNIFORM, 1, 1000), abi.new_states(1, 1, abi.STEP_PREVOTE))
+    empty = ol.batch_from_lists([], [], [], [], [], np.zeros(5, dtype=np.uint64))
+    _tally_edges_check(eng, abi.config(abi.MODE_REFERENCE, 0, 1), empty, ol.gen_power(66, 1, 4, abi.POWER_UNIFORM, 1, 10))
