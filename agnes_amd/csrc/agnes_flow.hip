@@ -69,10 +69,13 @@ constexpr uint32_t F_INST = 0, F_VALUE = 2048, F_VAL = 4096, F_ROUND = 6144, F_T
 #define AGNES_FLOW_BATCHES_PER_WAVE 4 /* batches per wave the batch size leaves (0: always FB); c3shard A/B 4 vs FB: flow 0.362 vs 0.444 ms */
 #endif
 #ifndef AGNES_FLOW_TAIL_VOTES
-#define AGNES_FLOW_TAIL_VOTES 1024 /* votes per batch of the queue's tail (0: the SMALLB tail) */
+#define AGNES_FLOW_TAIL_VOTES 0 /* votes per batch of the queue's tail (0: the SMALLB tail; 1024 measured 2 % slower on C3 / c3shard) */
 #endif
 #ifndef AGNES_FLOW_TAIL_PER_WAVE
 #define AGNES_FLOW_TAIL_PER_WAVE 2
+#endif
+#ifndef AGNES_FLOW_AHEAD
+#define AGNES_FLOW_AHEAD 1 /* batches a wave holds claimed beyond the current one (1 or 2) */
 #endif
 #ifndef AGNES_FLOW_FAST_START
 #define AGNES_FLOW_FAST_START 1 /* static first batches, the first chunk's DMA before the set constants */
@@ -244,13 +247,16 @@ __device__ __attribute__((noinline)) uint32_t label_back(const uint32_t* inst_co
 #ifndef AGNES_FLOW_WPE
 #define AGNES_FLOW_WPE 3
 #endif
+#ifndef AGNES_FLOW_XWPE
+#define AGNES_FLOW_XWPE 3 /* the records / edges variants */
+#endif
 /* REC (agnes_tally_records): the event records themselves, segmented by instance.
  * EDG (agnes_tally_edges): the edge summary instead -- etab counts each instance's
  * edges and the 16-B agnes_edge records go to the instance's segment (agnes_edges.hip's
  * definition, orc_edges: a valid vote is an edge when its executor's state, level |
  * last message << 4, changes). */
 template <bool PC, bool SM, bool R1, bool EVC, bool W64, bool REC = false, bool EDG = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES_FLOW_W64_WPE : AGNES_FLOW_WPE))) void flow(agnes_tally_args a, uint32_t lds_per_wave) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES_FLOW_W64_WPE : ((REC || EDG) ? AGNES_FLOW_XWPE : AGNES_FLOW_WPE)))) void flow(agnes_tally_args a, uint32_t lds_per_wave) {
     static_assert(!REC || (EVC && !W64), "records: with the record counts, u32 sums");
     static_assert(!EDG || (EVC && !W64 && !REC), "edges: the counts are the edges', u32 sums");
     constexpr uint32_t RW = W64 ? RECW64 : RECW; /* record words */
@@ -469,7 +475,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
         const uint32_t rank = (blockIdx.x / qn) * AGNES_WAVES_PER_BLOCK + wave;
         range_of(rank, H.s0, H.e0);
         range_of(qS + rank, N.s0, N.e0);
-        if (lane == 0) tq = atomicAdd(ctr, 1u) + 2u * qS;
+        if (AGNES_FLOW_AHEAD > 1 && lane == 0) tq = atomicAdd(ctr, 1u) + 2u * qS;
     }
 #else
     const uint32_t qS = 0u;
@@ -479,7 +485,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
         t = rdl(t, 0u);
         range_of(t, H.s0, H.e0);
         range_of(t + 1u, N.s0, N.e0);
-        if (lane == 0) tq = atomicAdd(ctr, 1u);
+        if (AGNES_FLOW_AHEAD > 1 && lane == 0) tq = atomicAdd(ctr, 1u);
     }
 #endif
     FDIAG(unsigned long long* const dg = flow_diag_buf + 64ull * (blockIdx.x * AGNES_WAVES_PER_BLOCK + wave);
@@ -584,7 +590,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                     smf = false;
                 }
                 /* the next batch's header, one stage per chunk; its States behind it */
-                if (N.s0 < N.e0) {
+                if (AGNES_FLOW_AHEAD == 1 && N.stage == 0u) { /* N's slot, claimed at this batch's start */
+                    range_of(rdl(tq, 0u), N.s0, N.e0);
+                    hdr1(N);
+                } else if (N.s0 < N.e0) {
                     if (N.stage == 1u) {
                         hdr2(N);
                     } else if (N.stage == 2u) {
@@ -800,6 +809,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                 const bool cA = cont0 && kA == k0;   /* unit A continues the previous chunk's instance */
                 const bool cL = cont0 && klast == k0; /* so does the last segment */
                 uint32_t lv0 = 0, lv1 = 0; /* levels 0..3, byte s & 3 of unit s >> 2 */
+                uint32_t lvb0 = 0, lvb1 = 0; /* (EDG) the levels BEFORE each vote (its executor's sums without it) */
                 /* (State machine) quorums crossed before each unit: bit 0 / 2 the prevote nil or
                  * value one at State.round (P1 is then behind the unit A / B), bit 1 / 3 a precommit
                  * value one (C behind it) -- the sums only grow, so a unit's first candidate is
@@ -820,11 +830,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                      * Dw: the vote's own type's half after it */
                     uint64_t P = 0, P3 = 0;
                     uint32_t Dw[LV];
+                    uint32_t Dwb[EDG ? LV : 1u]; /* (EDG) the same before the vote */
 #pragma unroll
                     for (uint32_t s = 0; s < LV; ++s) {
                         const uint32_t bs = 8u * (s & 3u);
                         uint32_t ws = w[s];
                         if (R > 1u && !ONE) ws &= (uint32_t)__builtin_amdgcn_sbfe((int32_t)(s < 4u ? rm0 : rm1), bs, 8u);
+                        if constexpr (EDG) Dwb[s] = (uint32_t)(P >> __builtin_amdgcn_ubfe(s < 4u ? ts0 : ts1, bs, 8u));
                         P += (uint64_t)ws << __builtin_amdgcn_ubfe(s < 4u ? sh0 : sh1, bs, 8u);
                         if (s == 3u) P3 = P;
                         Dw[s] = (uint32_t)(P >> __builtin_amdgcn_ubfe(s < 4u ? ts0 : ts1, bs, 8u));
@@ -892,7 +904,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                         TAb = u64of(qB + p3vp + p3np - dvp - dnp, qB + p3vc + p3nc - dvc - dnc);
                     }
                     /* per vote: is_quorum on its own type's sums, precedence as a level */
-                    uint32_t l0 = 0, l1 = 0;
+                    uint32_t l0 = 0, l1 = 0, lb0x = 0, lb1x = 0;
 #pragma unroll
                     for (uint32_t s = 0; s < LV; ++s) {
                         const uint32_t bs = 8u * (s & 3u);
@@ -906,6 +918,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                         l = sv > tv ? 3u : l;
                         if (s < 4u) l0 |= l << bs;
                         else l1 |= l << bs;
+                        if constexpr (EDG) {
+                            const int32_t bv = (int32_t)(Dwb[s] & 0xFFFFu), bn = (int32_t)(Dwb[s] >> 16);
+                            uint32_t lb = bv + bn > ta ? 1u : 0u;
+                            lb = bn > tn ? 2u : lb;
+                            lb = bv > tv ? 3u : lb;
+                            if (s < 4u) lb0x |= lb << bs;
+                            else lb1x |= lb << bs;
+                        }
                     }
                     if (SM) {
                         /* unit A: its running sums before the lane exceed q2 <=> the threshold on the
@@ -925,6 +945,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                     }
                     lv0 |= l0 & rm0;
                     lv1 |= l1 & rm1;
+                    if constexpr (EDG) {
+                        lvb0 |= lb0x & rm0;
+                        lvb1 |= lb1x & rm1;
+                    }
                     if (lastc) {
                         if (ONE) { /* every run of the last instance: its executors at the run's end
                                     * (the lane holding its last unit writes) */
@@ -1362,178 +1386,141 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                 }
 
                 if constexpr (EDG) {
-                    /* ---- the edge summary (agnes_tally_edges): a valid vote is an edge when its
-                     * executor's state -- code bits 0..3 | the last non-zero message << 4 --
-                     * changes (orc_edges; the HeightVotes stub, consensus_executor.rs:5).  Its
-                     * state before it: the previous valid vote of its executor for the low nibble,
-                     * the last one with a message for the high one -- in the lane, else (one
-                     * round, or runs: one executor per type per segment) the last earlier lane of
-                     * the segment holding one, else the executor's state carried in LDS (elab);
-                     * rounds revisited in the chunk: the same per (instance, round, type) key. ---- */
-                    const uint32_t vl0 = actA ? okb0 : 0u, vl1 = actB ? okb1 : 0u; /* 0xFF: valid votes */
-                    const bool fast = R1 || runs;
-                    const bool spl = R1 ? split : splitr;
-                    const uint32_t K2 = 2u * R;
-                    uint32_t prv[LV], nw[LV];
-                    uint32_t pendL = 0u, pendH = 0u;
-                    /* per class (fast: a vote type within the segment; slow: one key), in stream order */
-                    auto cls = [&](uint32_t q) -> uint32_t { /* the vote's key: instance k, round, type */
-                        const uint32_t bs = 8u * (q & 3u);
-                        const uint32_t r = ((q < 4u ? r8[0] : r8[1]) >> bs) & 0xFFu, t = ((q < 4u ? t8[0] : t8[1]) >> bs) & 1u;
-                        return (q < 4u ? kA : kB) * K2 + 2u * r + t;
+                    /* ---- the edge summary (agnes_tally_edges, orc_edges): a valid vote is an edge
+                     * when its executor's state -- code bits 0..3 | the last non-zero message << 4
+                     * -- changes.  On this route (no RoundSkip) a message belongs to one event
+                     * code (TimeoutPrevote to PolkaAny, TimeoutPrecommit to PrecommitAny, the
+                     * precommit to PolkaNil / PolkaValue at P1, the Decision to PrecommitValue at
+                     * C) and an executor's messages only switch off (P1, C), never on, so the
+                     * first vote of a code carries its message or none of the code's votes does:
+                     * the state changes exactly where the event code changes.  The code before a
+                     * vote is to_event(type, level of its executor's sums without it) -- computed
+                     * in K3 (lvb) -- so an edge needs no lookup; only its record's previous state
+                     * needs the executor's last message: the last earlier edge of the executor
+                     * with one (in the lane, else the last earlier lane of the segment, else the
+                     * state carried in LDS, elab, which changes only at edges). ---- */
+                    const uint32_t cbf0 = __builtin_amdgcn_perm(EV_HI, EV_LO, lvb0 | (ts0c >> 3));
+                    const uint32_t cbf1 = __builtin_amdgcn_perm(EV_HI, EV_LO, lvb1 | (ts1c >> 3));
+                    auto nzb = [](uint32_t x) -> uint32_t { /* 0x80 in the non-zero bytes of x */
+                        return ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu | x) & 0x80808080u;
                     };
-                    {
-                        bool hl0 = false, hl1 = false, hm0 = false, hm1 = false;
-                        uint32_t ll0 = 0u, ll1 = 0u, lm0 = 0u, lm1 = 0u;
+                    const uint32_t em0 = nzb((c0 ^ cbf0) & 0x07070707u) & (actA ? okb0 : 0u);
+                    const uint32_t em1 = nzb((c1 ^ cbf1) & 0x07070707u) & (actB ? okb1 : 0u);
+                    const uint32_t nA = (uint32_t)__builtin_popcount(em0), nB = (uint32_t)__builtin_popcount(em1);
+                    if (ballot((em0 | em1) != 0u)) {
+                        const bool fast = R1 || runs;
+                        const bool spl = R1 ? split : splitr;
+                        const uint32_t K2 = 2u * R;
+                        auto key_of = [&](uint32_t q) -> uint32_t { /* instance k, round, type */
+                            const uint32_t bs = 8u * (q & 3u);
+                            const uint32_t r = ((q < 4u ? r8[0] : r8[1]) >> bs) & 0xFFu, t = ((q < 4u ? t8[0] : t8[1]) >> bs) & 1u;
+                            return (q < 4u ? kA : kB) * K2 + 2u * r + t;
+                        };
+                        uint32_t ph[LV]; /* the last message before each edge; 0xFF: not in the lane */
+                        uint32_t emsk = 0u; /* bit q: vote q is an edge */
+#pragma unroll
+                        for (uint32_t q = 0; q < LV; ++q) emsk |= (((q < 4u ? em0 : em1) >> (8u * (q & 3u) + 7u)) & 1u) << q;
+                        bool hm0 = false, hm1 = false;
+                        uint32_t lm0 = 0u, lm1 = 0u;
 #pragma unroll
                         for (uint32_t q = 0; q < LV; ++q) {
-                            if (q == 4u && spl) { hl0 = hl1 = hm0 = hm1 = false; }
+                            if (q == 4u && spl) { hm0 = false; hm1 = false; }
                             const uint32_t bs = 8u * (q & 3u);
-                            const bool v = (((q < 4u ? vl0 : vl1) >> bs) & 1u) != 0u;
                             const bool tq = (((q < 4u ? t8[0] : t8[1]) >> bs) & 1u) != 0u;
-                            const uint32_t cb = ((q < 4u ? c0 : c1) >> bs) & 0xFFu;
-                            const bool hl = fast && (tq ? hl1 : hl0), hm = fast && (tq ? hm1 : hm0);
-                            prv[q] = (hl ? (tq ? ll1 : ll0) : 0u) | (hm ? ((tq ? lm1 : lm0) << 4) : 0u);
-                            pendL |= (v && !hl) ? 1u << q : 0u;
-                            pendH |= (v && !hm) ? 1u << q : 0u;
-                            if (v) {
-                                if (tq) { hl1 = true; ll1 = cb & 0xFu; } else { hl0 = true; ll0 = cb & 0xFu; }
-                                if (cb >> 4) {
-                                    if (tq) { hm1 = true; lm1 = cb >> 4; } else { hm0 = true; lm0 = cb >> 4; }
-                                }
+                            const uint32_t msg = ((q < 4u ? c0 : c1) >> (bs + 4u)) & 0xFu;
+                            const bool e = ((emsk >> q) & 1u) != 0u;
+                            ph[q] = (fast && (tq ? hm1 : hm0)) ? (tq ? lm1 : lm0) : 0xFFu;
+                            if (e && msg) {
+                                if (tq) { hm1 = true; lm1 = msg; } else { hm0 = true; lm0 = msg; }
                             }
                         }
-                        if (fast && ballot((pendL | pendH) != 0u)) {
-                            /* the last earlier lane of the segment with a valid vote / a message of the type */
+                        if (fast) {
                             const uint32_t sx = R1 ? (multi ? sA : 0u) : (multir ? sAr : 0u);
                             const uint64_t segm = (((1ull << lane) - 1ull) >> sx) << sx;
-                            const uint64_t L0 = ballot(hl0) & segm, L1 = ballot(hl1) & segm;
                             const uint64_t M0 = ballot(hm0) & segm, M1 = ballot(hm1) & segm;
-                            const uint32_t fl0 = shfl(ll0, L0 ? 63u - (uint32_t)__builtin_clzll(L0) : 0u);
-                            const uint32_t fl1 = shfl(ll1, L1 ? 63u - (uint32_t)__builtin_clzll(L1) : 0u);
-                            const uint32_t fm0 = shfl(lm0, M0 ? 63u - (uint32_t)__builtin_clzll(M0) : 0u);
-                            const uint32_t fm1 = shfl(lm1, M1 ? 63u - (uint32_t)__builtin_clzll(M1) : 0u);
+                            const uint32_t f0 = shfl(lm0, M0 ? 63u - (uint32_t)__builtin_clzll(M0) : 0u);
+                            const uint32_t f1 = shfl(lm1, M1 ? 63u - (uint32_t)__builtin_clzll(M1) : 0u);
 #pragma unroll
                             for (uint32_t q = 0; q < LV; ++q) {
-                                const bool pl = (pendL >> q) & 1u, ph = (pendH >> q) & 1u;
-                                if (!pl && !ph) continue;
+                                if (!((emsk >> q) & 1u) || ph[q] != 0xFFu) continue;
                                 const bool tq = (((q < 4u ? t8[0] : t8[1]) >> (8u * (q & 3u))) & 1u) != 0u;
-                                const bool cross = q < 4u || !spl;
-                                const bool gl = cross && (tq ? L1 : L0) != 0ull, gm = cross && (tq ? M1 : M0) != 0ull;
-                                const uint32_t car = (pl && !gl) || (ph && !gm) ? elab[cls(q)] : 0u;
-                                if (pl) prv[q] |= gl ? (tq ? fl1 : fl0) : (car & 0xFu);
-                                if (ph) prv[q] |= gm ? ((tq ? fm1 : fm0) << 4) : (car & 0xF0u);
+                                const bool gm = (q < 4u || !spl) && (tq ? M1 : M0) != 0ull;
+                                ph[q] = gm ? (tq ? f1 : f0) : (uint32_t)(elab[key_of(q)] >> 4);
                             }
-                            pendL = pendH = 0u;
-                        }
-                    }
-                    if (!fast) {
-                        /* rounds revisited in the chunk: one key at a time (its valid votes) */
-                        pendL = pendH = 0u;
-                        uint32_t todo = 0u;
+                            /* each (segment, type)'s last edge in the chunk carries the state out: a
+                             * later edge of the lane, or the first edge of that type in the next lane
+                             * holding one, in the same segment means it is not the last */
+                            const uint32_t segA = R1 ? kA : (kA * 16u + uA), segB = R1 ? kB : (kB * 16u + uB);
+                            uint32_t g0 = 0xFFFFFFFFu, g1 = 0xFFFFFFFFu; /* the segment of the lane's first edge per type */
 #pragma unroll
-                        for (uint32_t q = 0; q < LV; ++q) todo |= (((q < 4u ? vl0 : vl1) >> (8u * (q & 3u))) & 1u) << q;
-                        for (;;) {
-                            const uint64_t lm = ballot(todo != 0u);
-                            if (!lm) break;
-                            const uint32_t kl = (uint32_t)__builtin_ctzll(lm);
-                            const uint32_t ks = (uint32_t)__builtin_ctz(rdl(todo, kl));
-                            uint32_t mykey = cls(0u);
-#pragma unroll
-                            for (uint32_t q = 1; q < LV; ++q) mykey = ks == q ? cls(q) : mykey;
-                            const uint32_t KY = rdl(mykey, kl);
-                            bool hl = false, hm = false;
-                            uint32_t ll = 0u, lmx = 0u, inb = 0u;
-#pragma unroll
-                            for (uint32_t q = 0; q < LV; ++q) {
-                                if (!((todo >> q) & 1u) || cls(q) != KY) continue;
-                                inb |= 1u << q;
-                                const uint32_t cb = ((q < 4u ? c0 : c1) >> (8u * (q & 3u))) & 0xFFu;
-                                prv[q] = (hl ? ll : 0u) | (hm ? lmx << 4 : 0u);
-                                pendL |= hl ? 0u : 1u << q;
-                                pendH |= hm ? 0u : 1u << q;
-                                hl = true;
-                                ll = cb & 0xFu;
-                                if (cb >> 4) { hm = true; lmx = cb >> 4; }
+                            for (int q = (int)LV - 1; q >= 0; --q) {
+                                if (!((emsk >> q) & 1u)) continue;
+                                const bool tq = ((((uint32_t)q < 4u ? t8[0] : t8[1]) >> (8u * ((uint32_t)q & 3u))) & 1u) != 0u;
+                                if (tq) g1 = (uint32_t)q < 4u ? segA : segB;
+                                else g0 = (uint32_t)q < 4u ? segA : segB;
                             }
-                            todo &= ~inb;
-                            const uint64_t below = (1ull << lane) - 1ull;
-                            const uint64_t L = ballot(hl) & below, M = ballot(hm) & below;
-                            const uint32_t fl = shfl(ll, L ? 63u - (uint32_t)__builtin_clzll(L) : 0u);
-                            const uint32_t fm = shfl(lmx, M ? 63u - (uint32_t)__builtin_clzll(M) : 0u);
-                            const uint32_t car = elab[KY];
+                            const uint64_t above = ~((2ull << lane) - 1ull);
+                            const uint64_t N0 = ballot(g0 != 0xFFFFFFFFu) & above, N1 = ballot(g1 != 0xFFFFFFFFu) & above;
+                            uint32_t nx0 = shfl(g0, N0 ? (uint32_t)__builtin_ctzll(N0) : lane);
+                            uint32_t nx1 = shfl(g1, N1 ? (uint32_t)__builtin_ctzll(N1) : lane);
+                            nx0 = N0 ? nx0 : 0xFFFFFFFFu;
+                            nx1 = N1 ? nx1 : 0xFFFFFFFFu;
 #pragma unroll
-                            for (uint32_t q = 0; q < LV; ++q) {
-                                if (!((inb >> q) & 1u)) continue;
-                                if ((pendL >> q) & 1u) prv[q] |= L ? fl : (car & 0xFu);
-                                if ((pendH >> q) & 1u) prv[q] |= M ? (fm << 4) : (car & 0xF0u);
+                            for (int q = (int)LV - 1; q >= 0; --q) {
+                                if (!((emsk >> q) & 1u)) continue;
+                                const uint32_t bs = 8u * ((uint32_t)q & 3u);
+                                const bool tq = ((((uint32_t)q < 4u ? t8[0] : t8[1]) >> bs) & 1u) != 0u;
+                                const uint32_t sg = (uint32_t)q < 4u ? segA : segB;
+                                if ((tq ? nx1 : nx0) != sg) {
+                                    const uint32_t cb = (((uint32_t)q < 4u ? c0 : c1) >> bs) & 0xFFu;
+                                    elab[key_of((uint32_t)q)] = (unsigned char)((cb & 0xFu) | ((cb >> 4) ? (cb & 0xF0u) : (ph[q] << 4)));
+                                }
+                                if (tq) nx1 = sg;
+                                else nx0 = sg;
                             }
-                            pendL &= ~inb;
-                            pendH &= ~inb;
-                            /* the key's state after the chunk: its last vote's (the highest lane with one) */
-                            uint32_t fin = 0u;
+                        } else {
+                            /* rounds revisited in the chunk: the edges one key at a time */
+                            uint32_t todo = emsk;
+                            for (;;) {
+                                const uint64_t lm = ballot(todo != 0u);
+                                if (!lm) break;
+                                const uint32_t kl = (uint32_t)__builtin_ctzll(lm);
+                                const uint32_t ks = (uint32_t)__builtin_ctz(rdl(todo, kl));
+                                uint32_t mykey = key_of(0u);
 #pragma unroll
-                            for (uint32_t q = 0; q < LV; ++q) {
-                                if (!((inb >> q) & 1u)) continue;
-                                const uint32_t cb = ((q < 4u ? c0 : c1) >> (8u * (q & 3u))) & 0xFFu;
-                                fin = (cb & 0xFu) | ((cb >> 4) ? (cb & 0xF0u) : (prv[q] & 0xF0u));
+                                for (uint32_t q = 1; q < LV; ++q) mykey = ks == q ? key_of(q) : mykey;
+                                const uint32_t KY = rdl(mykey, kl);
+                                bool hm = false;
+                                uint32_t lmx = 0u, inb = 0u, fin = 0u;
+#pragma unroll
+                                for (uint32_t q = 0; q < LV; ++q) {
+                                    if (!((todo >> q) & 1u) || key_of(q) != KY) continue;
+                                    inb |= 1u << q;
+                                    const uint32_t cb = ((q < 4u ? c0 : c1) >> (8u * (q & 3u))) & 0xFFu;
+                                    ph[q] = hm ? lmx : 0xFFu;
+                                    if (cb >> 4) { hm = true; lmx = cb >> 4; }
+                                }
+                                todo &= ~inb;
+                                const uint64_t M = ballot(hm) & ((1ull << lane) - 1ull);
+                                const uint32_t fm = shfl(lmx, M ? 63u - (uint32_t)__builtin_clzll(M) : 0u);
+                                const uint32_t car = elab[KY] >> 4;
+#pragma unroll
+                                for (uint32_t q = 0; q < LV; ++q) {
+                                    if (!((inb >> q) & 1u)) continue;
+                                    if (ph[q] == 0xFFu) ph[q] = M ? fm : car;
+                                    const uint32_t cb = ((q < 4u ? c0 : c1) >> (8u * (q & 3u))) & 0xFFu;
+                                    fin = (cb & 0xFu) | ((cb >> 4) ? (cb & 0xF0u) : (ph[q] << 4));
+                                }
+                                const uint64_t H2 = ballot(inb != 0u);
+                                const uint32_t fv = rdl(fin, 63u - (uint32_t)__builtin_clzll(H2));
+                                __builtin_amdgcn_wave_barrier();
+                                if (lane == 0u) elab[KY] = (unsigned char)fv;
+                                __builtin_amdgcn_wave_barrier();
                             }
-                            const uint64_t H2 = ballot(inb != 0u);
-                            const uint32_t hl2 = 63u - (uint32_t)__builtin_clzll(H2);
-                            const uint32_t fv = rdl(fin, hl2);
-                            __builtin_amdgcn_wave_barrier();
-                            if (lane == 0u) elab[KY] = (unsigned char)fv;
-                            __builtin_amdgcn_wave_barrier();
-                        }
-                    }
-                    /* the new states and the edges */
-                    uint32_t em0 = 0u, em1 = 0u; /* 0x80 in the bytes of the edges */
-#pragma unroll
-                    for (uint32_t q = 0; q < LV; ++q) {
-                        const uint32_t bs = 8u * (q & 3u);
-                        const uint32_t cb = ((q < 4u ? c0 : c1) >> bs) & 0xFFu;
-                        nw[q] = (cb & 0xFu) | ((cb >> 4) ? (cb & 0xF0u) : (prv[q] & 0xF0u));
-                        const bool v = (((q < 4u ? vl0 : vl1) >> bs) & 1u) != 0u;
-                        const uint32_t e = (v && nw[q] != prv[q]) ? 0x80u << bs : 0u;
-                        if (q < 4u) em0 |= e;
-                        else em1 |= e;
-                    }
-                    if (fast) {
-                        /* each (segment, type)'s last vote in the chunk carries the executor's state
-                         * out (elab): a vote is its last unless a later one of the lane, or the first of
-                         * that type in the next lane holding one, is in the same segment */
-                        const uint32_t segA = R1 ? kA : (kA * 16u + uA), segB = R1 ? kB : (kB * 16u + uB);
-                        uint32_t has0 = 0u, has1 = 0u, f0 = 0xFFFFFFFFu, f1 = 0xFFFFFFFFu;
-#pragma unroll
-                        for (uint32_t q = 0; q < LV; ++q) {
-                            const uint32_t bs = 8u * (q & 3u);
-                            const bool v = (((q < 4u ? vl0 : vl1) >> bs) & 1u) != 0u;
-                            const bool tq = (((q < 4u ? t8[0] : t8[1]) >> bs) & 1u) != 0u;
-                            const uint32_t sg = q < 4u ? segA : segB;
-                            if (v && tq) { f1 = has1 ? f1 : sg; has1 = 1u; }
-                            if (v && !tq) { f0 = has0 ? f0 : sg; has0 = 1u; }
-                        }
-                        const uint64_t above = ~((2ull << lane) - 1ull);
-                        const uint64_t N0 = ballot(has0 != 0u) & above, N1 = ballot(has1 != 0u) & above;
-                        uint32_t nx0 = shfl(f0, N0 ? (uint32_t)__builtin_ctzll(N0) : lane);
-                        uint32_t nx1 = shfl(f1, N1 ? (uint32_t)__builtin_ctzll(N1) : lane);
-                        nx0 = N0 ? nx0 : 0xFFFFFFFFu;
-                        nx1 = N1 ? nx1 : 0xFFFFFFFFu;
-#pragma unroll
-                        for (int q = (int)LV - 1; q >= 0; --q) {
-                            const uint32_t bs = 8u * ((uint32_t)q & 3u);
-                            const bool v = ((((uint32_t)q < 4u ? vl0 : vl1) >> bs) & 1u) != 0u;
-                            if (!v) continue;
-                            const bool tq = ((((uint32_t)q < 4u ? t8[0] : t8[1]) >> bs) & 1u) != 0u;
-                            const uint32_t sg = (uint32_t)q < 4u ? segA : segB;
-                            if ((tq ? nx1 : nx0) != sg) elab[cls((uint32_t)q)] = (unsigned char)nw[q];
-                            if (tq) nx1 = sg; else nx0 = sg;
                         }
                         __builtin_amdgcn_wave_barrier();
-                    }
-                    /* counts (etab) and the records at the instance's segment */
-                    const uint32_t nA = (uint32_t)__builtin_popcount(em0), nB = (uint32_t)__builtin_popcount(em1);
-                    if (ballot((nA | nB) != 0u)) {
+                        /* the records at the instance's segment: rank = the instance's edges before
+                         * the chunk (etab) + the edges before it in the chunk */
                         const uint32_t Tn = split ? nB : nA + nB;
                         const uint32_t En = scan(Tn) - Tn;
                         const uint32_t rA = etab[kA] + En - (multi ? shfl(En, sA) : 0u);
@@ -1541,23 +1528,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                         const uint64_t gA = Sa + shfl(rl, kA), gB = Sa + shfl(rl, kB);
 #pragma unroll
                         for (uint32_t q = 0; q < LV; ++q) {
+                            if (!((emsk >> q) & 1u)) continue;
                             const uint32_t bs = 8u * (q & 3u);
                             const uint32_t em = q < 4u ? em0 : em1;
-                            if ((em >> (bs + 7u)) & 1u) {
-                                const uint32_t k = (q < 4u ? rA : rB) + (uint32_t)__builtin_popcount(em & ((1u << bs) - 1u));
-                                const uint32_t cb = ((q < 4u ? c0 : c1) >> bs) & 0xFFu;
-                                const uint32_t rq = ((q < 4u ? r8[0] : r8[1]) >> bs) & 0xFFu;
-                                const uint32_t tq = ((q < 4u ? t8[0] : t8[1]) >> bs) & 1u;
-                                const uint64_t j = c + o8 + q;
-                                const uint4 rec = make_uint4((uint32_t)j, (uint32_t)(j >> 32), H.s0 + (q < 4u ? kA : kB),
-                                                             rq | (tq << 8) | (cb << 16) | (prv[q] << 24));
-                                reinterpret_cast<uint4*>(a.rec_out)[(q < 4u ? gA : gB) + k] = rec;
-                            }
+                            const uint32_t k = (q < 4u ? rA : rB) + (uint32_t)__builtin_popcount(em & ((1u << bs) - 1u));
+                            const uint32_t cb = ((q < 4u ? c0 : c1) >> bs) & 0xFFu;
+                            const uint32_t rq = ((q < 4u ? r8[0] : r8[1]) >> bs) & 0xFFu;
+                            const uint32_t tq = ((q < 4u ? t8[0] : t8[1]) >> bs) & 1u;
+                            const uint32_t prev = ((((q < 4u ? cbf0 : cbf1) >> bs) & 0xFu)) | (ph[q] << 4);
+                            const uint64_t j = c + o8 + q;
+                            const uint4 rec = make_uint4((uint32_t)j, (uint32_t)(j >> 32), H.s0 + (q < 4u ? kA : kB),
+                                                         rq | (tq << 8) | (cb << 16) | (prev << 24));
+                            reinterpret_cast<uint4*>(a.rec_out)[(q < 4u ? gA : gB) + k] = rec;
                         }
+                        __builtin_amdgcn_wave_barrier();
+                        atomicAdd(etab + kA, kA == kB ? nA + nB : nA);
+                        atomicAdd(etab + kB, kA == kB ? 0u : nB);
                     }
-                    __builtin_amdgcn_wave_barrier();
-                    atomicAdd(etab + kA, kA == kB ? nA + nB : nA);
-                    atomicAdd(etab + kB, kA == kB ? 0u : nB);
                 }
 
                 if (EVC && !EDG) { /* records per unit: the votes whose event is Some (codes 1..5) */
@@ -1604,6 +1591,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                   }
               }
               ++dg_b;)
+        if (AGNES_FLOW_AHEAD == 1 && N.stage == 0u) { /* a batch without chunks: N's slot now */
+            range_of(rdl(tq, 0u), N.s0, N.e0);
+            hdr1(N);
+        }
         if (N.s0 >= N.e0) break;
         if (N.stage < 3u) { /* a short batch: the rest of the header now */
             if (N.stage == 1u) hdr2(N);
@@ -1612,9 +1603,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
         }
         H = N;
         spar ^= 1u;
+#if AGNES_FLOW_AHEAD == 1
+        /* one batch ahead only: the next slot is claimed now and read at the next chunk's
+         * top, so at the queue's end a wave holds no claimed batch beyond the next one */
+        if (lane == 0) tq = atomicAdd(ctr, 1u) + 2u * qS;
+        N.stage = 0u;
+        N.s0 = 0u;
+        N.e0 = 1u; /* (pending: not empty) */
+#else
         range_of(rdl(tq, 0u), N.s0, N.e0); /* the batch after, grabbed one batch ago */
         if (lane == 0) tq = atomicAdd(ctr, 1u) + 2u * qS;
         hdr1(N);
+#endif
     }
     flush();
     const uint32_t nb = rdl(scan(bad), 63u);
