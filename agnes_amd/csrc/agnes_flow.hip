@@ -1416,7 +1416,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                             const uint32_t r = ((q < 4u ? r8[0] : r8[1]) >> bs) & 0xFFu, t = ((q < 4u ? t8[0] : t8[1]) >> bs) & 1u;
                             return (q < 4u ? kA : kB) * K2 + 2u * r + t;
                         };
-                        uint32_t ph[LV]; /* the last message before each edge; 0xFF: not in the lane */
+                        uint32_t phw = 0u, php = 0u; /* the last message before each edge (nibble q); bit q: not yet known */
                         uint32_t emsk = 0u; /* bit q: vote q is an edge */
 #pragma unroll
                         for (uint32_t q = 0; q < LV; ++q) emsk |= (((q < 4u ? em0 : em1) >> (8u * (q & 3u) + 7u)) & 1u) << q;
@@ -1429,7 +1429,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                             const bool tq = (((q < 4u ? t8[0] : t8[1]) >> bs) & 1u) != 0u;
                             const uint32_t msg = ((q < 4u ? c0 : c1) >> (bs + 4u)) & 0xFu;
                             const bool e = ((emsk >> q) & 1u) != 0u;
-                            ph[q] = (fast && (tq ? hm1 : hm0)) ? (tq ? lm1 : lm0) : 0xFFu;
+                            if (fast && (tq ? hm1 : hm0)) phw |= (tq ? lm1 : lm0) << (4u * q);
+                            else php |= 1u << q;
                             if (e && msg) {
                                 if (tq) { hm1 = true; lm1 = msg; } else { hm0 = true; lm0 = msg; }
                             }
@@ -1442,10 +1443,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                             const uint32_t f1 = shfl(lm1, M1 ? 63u - (uint32_t)__builtin_clzll(M1) : 0u);
 #pragma unroll
                             for (uint32_t q = 0; q < LV; ++q) {
-                                if (!((emsk >> q) & 1u) || ph[q] != 0xFFu) continue;
+                                if (!((emsk & php) >> q & 1u)) continue;
                                 const bool tq = (((q < 4u ? t8[0] : t8[1]) >> (8u * (q & 3u))) & 1u) != 0u;
                                 const bool gm = (q < 4u || !spl) && (tq ? M1 : M0) != 0ull;
-                                ph[q] = gm ? (tq ? f1 : f0) : (uint32_t)(elab[key_of(q)] >> 4);
+                                phw |= (gm ? (tq ? f1 : f0) : (uint32_t)(elab[key_of(q)] >> 4)) << (4u * q);
                             }
                             /* each (segment, type)'s last edge in the chunk carries the state out: a
                              * later edge of the lane, or the first edge of that type in the next lane
@@ -1473,7 +1474,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                                 const uint32_t sg = (uint32_t)q < 4u ? segA : segB;
                                 if ((tq ? nx1 : nx0) != sg) {
                                     const uint32_t cb = (((uint32_t)q < 4u ? c0 : c1) >> bs) & 0xFFu;
-                                    elab[key_of((uint32_t)q)] = (unsigned char)((cb & 0xFu) | ((cb >> 4) ? (cb & 0xF0u) : (ph[q] << 4)));
+                                    elab[key_of((uint32_t)q)] = (unsigned char)((cb & 0xFu) | ((cb >> 4) ? (cb & 0xF0u) : (((phw >> (4u * (uint32_t)q)) & 0xFu) << 4)));
                                 }
                                 if (tq) nx1 = sg;
                                 else nx0 = sg;
@@ -1497,7 +1498,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                                     if (!((todo >> q) & 1u) || key_of(q) != KY) continue;
                                     inb |= 1u << q;
                                     const uint32_t cb = ((q < 4u ? c0 : c1) >> (8u * (q & 3u))) & 0xFFu;
-                                    ph[q] = hm ? lmx : 0xFFu;
+                                    phw &= ~(0xFu << (4u * q));
+                                    php &= ~(1u << q);
+                                    if (hm) phw |= lmx << (4u * q);
+                                    else php |= 1u << q;
                                     if (cb >> 4) { hm = true; lmx = cb >> 4; }
                                 }
                                 todo &= ~inb;
@@ -1507,9 +1511,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
 #pragma unroll
                                 for (uint32_t q = 0; q < LV; ++q) {
                                     if (!((inb >> q) & 1u)) continue;
-                                    if (ph[q] == 0xFFu) ph[q] = M ? fm : car;
+                                    if ((php >> q) & 1u) phw |= (M ? fm : car) << (4u * q);
                                     const uint32_t cb = ((q < 4u ? c0 : c1) >> (8u * (q & 3u))) & 0xFFu;
-                                    fin = (cb & 0xFu) | ((cb >> 4) ? (cb & 0xF0u) : (ph[q] << 4));
+                                    fin = (cb & 0xFu) | ((cb >> 4) ? (cb & 0xF0u) : (((phw >> (4u * q)) & 0xFu) << 4));
                                 }
                                 const uint64_t H2 = ballot(inb != 0u);
                                 const uint32_t fv = rdl(fin, 63u - (uint32_t)__builtin_clzll(H2));
@@ -1535,7 +1539,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                             const uint32_t cb = ((q < 4u ? c0 : c1) >> bs) & 0xFFu;
                             const uint32_t rq = ((q < 4u ? r8[0] : r8[1]) >> bs) & 0xFFu;
                             const uint32_t tq = ((q < 4u ? t8[0] : t8[1]) >> bs) & 1u;
-                            const uint32_t prev = ((((q < 4u ? cbf0 : cbf1) >> bs) & 0xFu)) | (ph[q] << 4);
+                            const uint32_t prev = ((((q < 4u ? cbf0 : cbf1) >> bs) & 0xFu)) | (((phw >> (4u * q)) & 0xFu) << 4);
                             const uint64_t j = c + o8 + q;
                             const uint4 rec = make_uint4((uint32_t)j, (uint32_t)(j >> 32), H.s0 + (q < 4u ? kA : kB),
                                                          rq | (tq << 8) | (cb << 16) | (prev << 24));
