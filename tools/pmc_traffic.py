@@ -18,7 +18,12 @@ import sys
 
 # engine kernel name (agnes_kernel_times) -> regex on the demangled symbol
 KERNELS = {
-    "flow": r"agnes::flow::flow<",
+    # template <PC, SM, R1, EVC, W64, REC, EDG>: the step's flow, and the record / edge
+    # variants agnes_tally_records / agnes_tally_edges launch (round 5)
+    "flow": r"agnes::flow::flow<\w+, \w+, \w+, false, \w+, false, false>",
+    "flow_counts": r"agnes::flow::flow<\w+, \w+, \w+, true, \w+, false, false>",
+    "flow_records": r"agnes::flow::flow<\w+, \w+, \w+, true, \w+, true, false>",
+    "flow_edges": r"agnes::flow::flow<\w+, \w+, \w+, true, \w+, false, true>",
     "sweep_walk": r"agnes::sweep::sweep<",
     "tally_fast": r"agnes::fast::tally_fast<",
     "apply_codes": r"agnes::apply::apply_codes<",
