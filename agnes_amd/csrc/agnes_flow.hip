@@ -1366,20 +1366,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                                 }
                             }
                         }
-                        /* the stores: one 16-B record per vote with an event */
+                        /* the stores: one 16-B record per vote with an event.  Per unit, bytewise:
+                         * kind = event + 3 (AGNES_EV_POLKA_ANY ..), the message nibble, and the
+                         * Value events (3, 5); a record's last word is assembled by two v_perm */
+                        uint4* const pA = reinterpret_cast<uint4*>(a.rec_out) + gA + rA;
+                        uint4* const pB = reinterpret_cast<uint4*>(a.rec_out) + gB + rB;
+                        const uint64_t j0 = c + o8; /* a multiple of 8: + q never carries */
+                        const uint32_t jlo = (uint32_t)j0, jhi = (uint32_t)(j0 >> 32);
+                        const uint32_t e0 = c0 & 0x07070707u, e1 = c1 & 0x07070707u;
+                        const uint32_t kd0 = e0 + 0x03030303u, kd1 = e1 + 0x03030303u;
+                        const uint32_t ms0 = (c0 >> 4) & 0x0F0F0F0Fu, ms1 = (c1 >> 4) & 0x0F0F0F0Fu;
+                        const uint32_t vm0 = zero_marks(e0 ^ 0x03030303u) | zero_marks(e0 ^ 0x05050505u);
+                        const uint32_t vm1 = zero_marks(e1 ^ 0x03030303u) | zero_marks(e1 ^ 0x05050505u);
 #pragma unroll
                         for (uint32_t q = 0; q < LV; ++q) {
-                            const uint32_t bs = 8u * (q & 3u);
+                            const uint32_t b = q & 3u, bs = 8u * b;
                             const uint32_t hm = q < 4u ? hA : hB;
                             if ((hm >> (bs + 7u)) & 1u) {
-                                const uint32_t k = (q < 4u ? rA : rB) + (uint32_t)__builtin_popcount(hm & ((1u << bs) - 1u));
-                                const uint32_t cb = ((q < 4u ? c0 : c1) >> bs) & 0xFFu;
-                                const uint32_t rq = ((q < 4u ? r8[0] : r8[1]) >> bs) & 0xFFu;
-                                const uint64_t j = c + o8 + q;
-                                const bool isv = (cb & 7u) == AGNES_CODE_POLKA_VALUE || (cb & 7u) == AGNES_CODE_PRECOMMIT_VALUE;
-                                const uint4 rec = make_uint4((uint32_t)j, (uint32_t)(j >> 32), isv ? vv[q] : AGNES_NIL,
-                                                             rq | (((cb & 7u) + 3u) << 8) | ((cb >> 4) << 16));
-                                reinterpret_cast<uint4*>(a.rec_out)[(q < 4u ? gA : gB) + k] = rec;
+                                const uint32_t k = (uint32_t)__builtin_popcount(hm & ((1u << bs) - 1u));
+                                /* [round, kind, message, 0] */
+                                const uint32_t rk = __builtin_amdgcn_perm(q < 4u ? kd0 : kd1, q < 4u ? r8[0] : r8[1],
+                                                                          b | ((4u + b) << 8) | 0x0C0C0000u);
+                                const uint32_t w3 = __builtin_amdgcn_perm(q < 4u ? ms0 : ms1, rk, 0x0C000100u | ((4u + b) << 16));
+                                const bool isv = (((q < 4u ? vm0 : vm1) >> (bs + 7u)) & 1u) != 0u;
+                                (q < 4u ? pA : pB)[k] = make_uint4(jlo | q, jhi, isv ? vv[q] : AGNES_NIL, w3);
                             }
                         }
                     }
