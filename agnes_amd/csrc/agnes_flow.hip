@@ -778,13 +778,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                 uint32_t uA = 0, uB = 0, sAr = sA;
                 bool splitr = split, multir = multi;
                 uint64_t SAr = 0, SBr = 0;
-                if (!R1 && all_ok && lo_r == 0u && hi_r == CH) {
+                if (!R1 && all_ok) {
                     uA = r8[0] & 0xFFu;
                     uB = r8[1] & 0xFFu;
+                    if (lo_r != 0u || hi_r != CH) {
+                        /* a stream's first or last chunk (round 5): the units outside it (no votes,
+                         * weight 0) take the round of the nearest unit inside, so they extend its
+                         * run and never start one */
+                        const uint32_t rf = rdl(((lo_r >> 2) & 1u) ? uB : uA, lo_r >> 3);
+                        const uint32_t rz = rdl((((hi_r - 1u) >> 2) & 1u) ? uB : uA, (hi_r - 1u) >> 3);
+                        if (!actA) uA = o8 < lo_r ? rf : rz;
+                        if (!actB) uB = o8 + 4u < lo_r ? rf : rz;
+                    }
                     const uint32_t pA = shfl(uB, lane - 1u); /* the unit before unit A (lane 0: none) */
                     const bool iA = ((SA >> lane) & 1ull) != 0ull, iB = ((SBm >> lane) & 1ull) != 0ull;
                     const bool rsA = lane != 0u && !iA && uA != pA, rsB = !iB && uB != uA;
-                    const bool badr = r8[0] != uA * 0x01010101u || r8[1] != uB * 0x01010101u ||
+                    const bool badr = (actA && r8[0] != uA * 0x01010101u) || (actB && r8[1] != uB * 0x01010101u) ||
                                       (rsA && uA < pA) || (rsB && uB < uA);
                     if (!ballot(badr)) {
                         runs = true;
