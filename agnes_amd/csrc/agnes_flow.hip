@@ -248,7 +248,10 @@ __device__ __attribute__((noinline)) uint32_t label_back(const uint32_t* inst_co
 #define AGNES_FLOW_WPE 3
 #endif
 #ifndef AGNES_FLOW_XWPE
-#define AGNES_FLOW_XWPE 3 /* the records / edges variants */
+#define AGNES_FLOW_XWPE 3 /* the records / edges variants, one round */
+#endif
+#ifndef AGNES_FLOW_XWPE_R
+#define AGNES_FLOW_XWPE_R 2 /* ... several rounds (their registers spill at 3 waves per SIMD) */
 #endif
 /* REC (agnes_tally_records): the event records themselves, segmented by instance.
  * EDG (agnes_tally_edges): the edge summary instead -- etab counts each instance's
@@ -256,7 +259,7 @@ __device__ __attribute__((noinline)) uint32_t label_back(const uint32_t* inst_co
  * definition, orc_edges: a valid vote is an edge when its executor's state, level |
  * last message << 4, changes). */
 template <bool PC, bool SM, bool R1, bool EVC, bool W64, bool REC = false, bool EDG = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES_FLOW_W64_WPE : ((REC || EDG) ? AGNES_FLOW_XWPE : AGNES_FLOW_WPE)))) void flow(agnes_tally_args a, uint32_t lds_per_wave) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES_FLOW_W64_WPE : ((REC || EDG) ? (R1 ? AGNES_FLOW_XWPE : AGNES_FLOW_XWPE_R) : AGNES_FLOW_WPE)))) void flow(agnes_tally_args a, uint32_t lds_per_wave) {
     static_assert(!REC || (EVC && !W64), "records: with the record counts, u32 sums");
     static_assert(!EDG || (EVC && !W64 && !REC), "edges: the counts are the edges', u32 sums");
     constexpr uint32_t RW = W64 ? RECW64 : RECW; /* record words */
