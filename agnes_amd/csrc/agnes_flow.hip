@@ -1372,8 +1372,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                                 } else {
                                     const uint32_t rq = ((q < 4u ? r8[0] : r8[1]) >> bs) & 0xFFu;
                                     const uint64_t gq = q < 4u ? gA : gB;
+                                    /* fast: the segment's votes in the chunk before this one hold no
+                                     * match (the lane's part and lanes [sx, lane) were searched), so the
+                                     * walk starts at the segment's first lane (unit B of a split lane) */
+                                    const uint64_t js = !fast ? c + o8 + q : ((q >= 4u && spl) ? c + o8 + 4u : c + 8u * sx);
                                     vv[q] = label_back(a.vb.instance, a.vb.round, a.vb.type, a.vb.value, a.vb.validator, gq,
-                                                       c + o8 + q, H.s0 + (q < 4u ? kA : kB), rq, tq ? 1u : 0u,
+                                                       js, H.s0 + (q < 4u ? kA : kB), rq, tq ? 1u : 0u,
                                                        q < 4u ? recA.z : recB.z);
                                 }
                             }
