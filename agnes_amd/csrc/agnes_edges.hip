@@ -65,11 +65,8 @@ __device__ __forceinline__ void load_win(const uint8_t* col, uint64_t w, uint64_
  * is then a 64-bit shift and xor, not an LDS round trip the next vote of the same
  * executor waits on */
 template <bool EMIT, uint32_t W, bool REG>
-__global__ __launch_bounds__(64) void edge_walk(EdgeArgs a) {
+__device__ __forceinline__ uint64_t walk_one(const EdgeArgs& a, uint32_t i, uint32_t lane, uint64_t base) {
     uint32_t* const tab = reinterpret_cast<uint32_t*>(agnes_smem);
-    const uint32_t lane = threadIdx.x;
-    const uint32_t i = blockIdx.x * 64u + lane;
-    if (i >= a.vb.n_instances) return;
     uint64_t st = 0; /* (REG) VoteCount::new: level 0 */
     if (!REG)
         for (uint32_t s = 0; s < a.nslots; ++s) tab[s * 64u + lane] = 0u; /* VoteCount::new: level 0 */
@@ -77,7 +74,6 @@ __global__ __launch_bounds__(64) void edge_walk(EdgeArgs a) {
     uint64_t lo = a.vb.offsets[i], hi = a.vb.offsets[i + 1u];
     lo = lo < NV ? lo : NV;
     hi = hi < NV ? hi : NV;
-    const uint64_t base = EMIT ? a.offs[i] : 0u;
     uint64_t cnt = 0;
     for (uint64_t w = lo & ~(uint64_t)(W - 1u); w < hi; w += W) {
         uint32_t c[W / 4u], r[W / 4u], t[W / 4u];
@@ -114,16 +110,24 @@ __global__ __launch_bounds__(64) void edge_walk(EdgeArgs a) {
             }
         }
     }
-    if (!EMIT) a.offs[i + 1u] = cnt;
+    return cnt;
+}
+
+template <bool EMIT, uint32_t W, bool REG>
+__global__ __launch_bounds__(64) void edge_walk(EdgeArgs a) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t i = blockIdx.x * 64u + lane;
+    if (i >= a.vb.n_instances) return;
+    if (EMIT) walk_one<true, W, REG>(a, i, lane, a.offs[i]);
+    else a.offs[i + 1u] = walk_one<false, W, REG>(a, i, lane, 0u);
 }
 
 /* the segmented edges (agnes_tally_edges) of every instance, or of the ones on a list
  * (the flow route's walk list): instance i's at out[offsets[i] + k], k < counts[i]
- * (a vote is at most one edge), one lane per instance, the same walk */
-template <bool LIST>
+ * (a vote is at most one edge), one lane per instance, the same windowed walk */
+template <bool LIST, uint32_t W, bool REG>
 __global__ __launch_bounds__(64) void edge_seg_walk(EdgeArgs a, const uint32_t* list, const uint32_t* list_n,
                                                     uint64_t* counts) {
-    uint32_t* const tab = reinterpret_cast<uint32_t*>(agnes_smem);
     const uint32_t lane = threadIdx.x;
     uint32_t i;
     if (LIST) {
@@ -134,29 +138,7 @@ __global__ __launch_bounds__(64) void edge_seg_walk(EdgeArgs a, const uint32_t* 
         i = blockIdx.x * 64u + lane;
         if (i >= a.vb.n_instances) return;
     }
-    for (uint32_t s = 0; s < a.nslots; ++s) tab[s * 64u + lane] = 0u; /* VoteCount::new: level 0 */
-    const uint64_t NV = a.vb.n_votes;
-    uint64_t lo = a.vb.offsets[i], hi = a.vb.offsets[i + 1u];
-    lo = lo < NV ? lo : NV;
-    hi = hi < NV ? hi : NV;
-    agnes_edge* const out = a.out + a.vb.offsets[i];
-    uint64_t cnt = 0;
-    for (uint64_t j = lo; j < hi; ++j) {
-        const uint32_t cb = a.codes[j], rb = a.vb.round[j], tb = a.vb.type[j];
-        const uint32_t ev = cb & AGNES_CODE_EVENT_MASK, key = rb * 2u + tb;
-        if (ev == AGNES_CODE_INVALID || ev == AGNES_CODE_REJECTED || tb > 1u || key >= a.keys) continue;
-        uint32_t* const p = tab + (key >> 2) * 64u + lane;
-        const uint32_t x = *p, sh = 8u * (key & 3u), old = (x >> sh) & 0xFFu;
-        const uint32_t msg = cb >> AGNES_CODE_MSG_SHIFT;
-        const uint32_t nb = (cb & 0xFu) | (msg ? msg << AGNES_CODE_MSG_SHIFT : old & 0xF0u);
-        if (nb != old) {
-            *reinterpret_cast<uint4*>(out + cnt) = make_uint4((uint32_t)j, (uint32_t)(j >> 32), i,
-                                                              rb | (tb << 8) | (cb << 16) | (old << 24));
-            ++cnt;
-            *p = x ^ ((old ^ nb) << sh);
-        }
-    }
-    counts[i] = cnt;
+    counts[i] = walk_one<true, W, REG>(a, i, lane, a.vb.offsets[i]);
 }
 
 /* the dense summary from the segmented one: wave w copies instances 32w .. 32w + 31 */
@@ -306,12 +288,21 @@ hipError_t agnes_launch_edge_seg_walk(const agnes_vote_batch* vb, const uint8_t*
     const uint32_t n = vb->n_instances;
     if (n == 0) return hipSuccess;
     EdgeArgs a{*vb, codes, nullptr, seg, 2u * max_rounds, (2u * max_rounds + 3u) / 4u};
-    const size_t lds = (size_t)a.nslots * 64u * sizeof(uint32_t);
+    const bool w16 = ((reinterpret_cast<uintptr_t>(codes) | reinterpret_cast<uintptr_t>(vb->round) |
+                       reinterpret_cast<uintptr_t>(vb->type)) & 15u) == 0u;
+    const bool reg = a.keys <= 8u;
+    const size_t lds = reg ? 0u : (size_t)a.nslots * 64u * sizeof(uint32_t);
+    const dim3 grid((n + 63u) / 64u), blk(64);
     AgnesKt kt("edge_seg_walk", st);
-    if (list)
-        hipLaunchKernelGGL((edge_seg_walk<true>), dim3((n + 63u) / 64u), dim3(64), lds, st, a, list, list_n, counts);
-    else
-        hipLaunchKernelGGL((edge_seg_walk<false>), dim3((n + 63u) / 64u), dim3(64), lds, st, a, list, list_n, counts);
+#define AGNES_EDGE_SEG(L, W_, R_) hipLaunchKernelGGL((edge_seg_walk<L, W_, R_>), grid, blk, lds, st, a, list, list_n, counts)
+    if (list) {
+        if (reg) { if (w16) AGNES_EDGE_SEG(true, EW, true); else AGNES_EDGE_SEG(true, 4u, true); }
+        else { if (w16) AGNES_EDGE_SEG(true, EW, false); else AGNES_EDGE_SEG(true, 4u, false); }
+    } else {
+        if (reg) { if (w16) AGNES_EDGE_SEG(false, EW, true); else AGNES_EDGE_SEG(false, 4u, true); }
+        else { if (w16) AGNES_EDGE_SEG(false, EW, false); else AGNES_EDGE_SEG(false, 4u, false); }
+    }
+#undef AGNES_EDGE_SEG
     return hipGetLastError();
 }
 

@@ -43,6 +43,10 @@ struct EvArgs {
     uint64_t* offs; /* n_instances + 1 */
     agnes_vote_event* out;
     uint32_t keys;  /* 2 * max_rounds */
+    /* (SEG emit) the segmented records: seg[mult * offsets[i] + k], k < counts[i] */
+    uint4* seg;
+    uint64_t* counts;
+    uint32_t mult;
 };
 
 /* W consecutive bytes of a u8 column from w (W = 4: one dword; W >= 16: 16-B loads
@@ -541,7 +545,12 @@ __device__ __forceinline__ void load_pass_v(const EvArgs& a, uint64_t j0, uint64
     }
 }
 
-template <uint32_t V, uint32_t WPE>
+/* SEG (agnes_tally_records on the routes whose tally does not write the records): the
+ * same pass, each record to its instance's segment instead of the dense stream -- the
+ * dense position d of instance i's record (offs: the count pass + scan) moves to
+ * seg + d + mult * offsets[i] - offs[i] (per batch instance in LDS, where the staging
+ * area was), and the batch's counts[i] = offs[i + 1] - offs[i] */
+template <uint32_t V, uint32_t WPE, bool SEG = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void event_emit_stream(EvArgs a) {
     constexpr uint32_t P = 64u * V; /* votes per pass */
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -551,9 +560,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     /* per wave: the value slots [EB][keys], then the record staging area */
     uint32_t* const lab = reinterpret_cast<uint32_t*>(agnes_smem) + wave * (EB * keys + 6u * EV_STAGE);
     uint32_t* const stage = lab + EB * keys;
+    uint64_t* const dl = reinterpret_cast<uint64_t*>(stage); /* (SEG) [EB] */
     uint32_t b = blockIdx.x * 4u + wave;
     if (b >= NB) return; /* wave-uniform */
     EvBatch B = ev_batch(a, b, ev_load(a, b, lane));
+    auto seg_batch = [&](const EvBatch& X) {
+        if (SEG && lane < X.m) {
+            const uint32_t i = X.s0 + lane;
+            const uint64_t o = a.offs[i];
+            a.counts[i] = a.offs[i + 1u] - o;
+            dl[lane] = (uint64_t)a.mult * a.vb.offsets[i] - o;
+        }
+    };
+    seg_batch(B);
     uint32_t nb = b + BS;
     EvRaw NR = nb < NB ? ev_load(a, nb, lane) : EvRaw{0u, 0u};
     uint64_t ncnt = nb < NB ? a.offs[nb * EB] : 0u;
@@ -754,7 +773,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
              * stores (a record is 3 of them), or straight out when the pass has more than
              * the area holds */
             const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-            const bool staged = total <= EV_STAGE;
+            const bool staged = !SEG && total <= EV_STAGE;
             auto emit = [&](agnes_vote_event* dst) {
                 uint32_t o = incl - n_rec;
 #pragma unroll
@@ -773,7 +792,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                     }
                 }
             };
-            if (staged) /* (two instantiations: LDS stores here, global ones below) */
+            if constexpr (SEG) {
+                uint32_t o = incl - n_rec;
+#pragma unroll
+                for (uint32_t s = 0; s < V; ++s) {
+                    const uint32_t two = ((skm >> s) & 1u) | (((hasm >> s) & 1u) << 1);
+                    if (two) {
+                        const uint32_t cb = byte_at(cur.c4, s), ev = cb & AGNES_CODE_EVENT_MASK;
+                        const uint32_t rb = byte_at(cur.r4, s), msg = cb >> AGNES_CODE_MSG_SHIFT;
+                        const uint64_t j = c + p0 + s;
+                        uint4* const d = a.seg + (cnt + o + dl[kk[s]]);
+                        if (two & 1u) put_seg(d, j, AGNES_NIL, rb, AGNES_EV_ROUND_SKIP, msg);
+                        if (two & 2u) {
+                            const bool val = ev == AGNES_CODE_POLKA_VALUE || ev == AGNES_CODE_PRECOMMIT_VALUE;
+                            put_seg(d + (two & 1u), j, val ? slot[s] : AGNES_NIL, rb, kind_of(ev), msg);
+                        }
+                        o += (two & 1u) + (two >> 1);
+                    }
+                }
+            } else if (staged) /* (two instantiations: LDS stores here, global ones below) */
                 emit(reinterpret_cast<agnes_vote_event*>(stage));
             else
                 emit(a.out + cnt);
@@ -797,6 +834,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             }
             __builtin_amdgcn_wave_barrier();
             for (uint32_t k = lane; k < EB * keys; k += 64u) lab[k] = 0u;
+            seg_batch(B);
             __builtin_amdgcn_wave_barrier();
         }
         c = nc;
@@ -875,6 +913,31 @@ hipError_t agnes_launch_events(const agnes_vote_batch* vb, const uint8_t* codes,
         hipLaunchKernelGGL(event_emit_wave, dim3(blocks), dim3(256), lds_w, st, a);
     } else
         hipLaunchKernelGGL((event_walk<true, 4u, false>), grid, blk, lds, st, a);
+    return hipGetLastError();
+}
+
+bool agnes_seg_emit_ok(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds) {
+    return ((reinterpret_cast<uintptr_t>(codes) | reinterpret_cast<uintptr_t>(vb->round) |
+             reinterpret_cast<uintptr_t>(vb->type) | reinterpret_cast<uintptr_t>(vb->value)) & 15u) == 0u &&
+           2u * max_rounds <= 64u;
+}
+
+hipError_t agnes_launch_seg_emit(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds, uint32_t mult,
+                                 const uint64_t* offs, uint64_t* counts, void* seg, hipStream_t st) {
+    using namespace agnes::events;
+    const uint32_t n = vb->n_instances;
+    if (n == 0) return hipSuccess;
+    if (!agnes_seg_emit_ok(vb, codes, max_rounds)) return hipErrorInvalidValue;
+    EvArgs a{*vb, codes, const_cast<uint64_t*>(offs), nullptr, 2u * max_rounds, reinterpret_cast<uint4*>(seg), counts, mult};
+    const uint32_t NB = (n + EB - 1u) / EB;
+    const size_t lds_s = (size_t)4u * (EB * a.keys + 6u * EV_STAGE) * sizeof(uint32_t);
+    const void* fn = reinterpret_cast<const void*>(&event_emit_stream<4u, 5u, true>);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds_s) != hipSuccess || per_cu < 1) per_cu = 1;
+    const uint32_t cap = EV_PREFETCH ? 256u * (uint32_t)per_cu : 0xFFFFFFFFu;
+    const uint32_t sblocks = (NB + 3u) / 4u < cap ? (NB + 3u) / 4u : cap;
+    AgnesKt kt("seg_emit", st);
+    hipLaunchKernelGGL((event_emit_stream<4u, 5u, true>), dim3(sblocks), dim3(256), lds_s, st, a);
     return hipGetLastError();
 }
 
