@@ -1442,67 +1442,65 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                             const uint32_t r = ((q < 4u ? r8[0] : r8[1]) >> bs) & 0xFFu, t = ((q < 4u ? t8[0] : t8[1]) >> bs) & 1u;
                             return (q < 4u ? kA : kB) * K2 + 2u * r + t;
                         };
+                        /* the lane's edges one at a time (a chunk holds few: 2 % of C2's votes) */
+                        auto byteq = [](uint32_t x0, uint32_t x1, uint32_t q) -> uint32_t {
+                            return ((q < 4u ? x0 : x1) >> (8u * (q & 3u))) & 0xFFu;
+                        };
+                        auto nib = [](uint32_t x) -> uint32_t { return ((x * 0x01020408u) >> 24) & 0xFu; };
+                        const uint32_t emsk = nib(em0 >> 7) | (nib(em1 >> 7) << 4); /* bit q: vote q is an edge */
+                        const uint32_t segA = R1 ? kA : (kA * 16u + uA), segB = R1 ? kB : (kB * 16u + uB);
                         uint32_t phw = 0u, php = 0u; /* the last message before each edge (nibble q); bit q: not yet known */
-                        uint32_t emsk = 0u; /* bit q: vote q is an edge */
-#pragma unroll
-                        for (uint32_t q = 0; q < LV; ++q) emsk |= (((q < 4u ? em0 : em1) >> (8u * (q & 3u) + 7u)) & 1u) << q;
-                        bool hm0 = false, hm1 = false;
+                        bool hm0 = false, hm1 = false, rs = false;
                         uint32_t lm0 = 0u, lm1 = 0u;
-#pragma unroll
-                        for (uint32_t q = 0; q < LV; ++q) {
-                            if (q == 4u && spl) { hm0 = false; hm1 = false; }
-                            const uint32_t bs = 8u * (q & 3u);
-                            const bool tq = (((q < 4u ? t8[0] : t8[1]) >> bs) & 1u) != 0u;
-                            const uint32_t msg = ((q < 4u ? c0 : c1) >> (bs + 4u)) & 0xFu;
-                            const bool e = ((emsk >> q) & 1u) != 0u;
+                        uint32_t g0 = 0xFFFFFFFFu, g1 = 0xFFFFFFFFu; /* the segment of the lane's first edge per type */
+                        for (uint32_t m = emsk; m; m &= m - 1u) {
+                            const uint32_t q = (uint32_t)__builtin_ctz(m);
+                            if (spl && q >= 4u && !rs) { hm0 = false; hm1 = false; rs = true; }
+                            const bool tq = (byteq(t8[0], t8[1], q) & 1u) != 0u;
+                            const uint32_t msg = byteq(c0, c1, q) >> 4;
+                            const uint32_t sg = q < 4u ? segA : segB;
                             if (fast && (tq ? hm1 : hm0)) phw |= (tq ? lm1 : lm0) << (4u * q);
                             else php |= 1u << q;
-                            if (e && msg) {
+                            if (msg) {
                                 if (tq) { hm1 = true; lm1 = msg; } else { hm0 = true; lm0 = msg; }
                             }
+                            if (tq) g1 = g1 == 0xFFFFFFFFu ? sg : g1;
+                            else g0 = g0 == 0xFFFFFFFFu ? sg : g0;
                         }
+                        if (spl && !rs) { hm0 = false; hm1 = false; } /* the lane's last part: unit B */
                         if (fast) {
                             const uint32_t sx = R1 ? (multi ? sA : 0u) : (multir ? sAr : 0u);
                             const uint64_t segm = (((1ull << lane) - 1ull) >> sx) << sx;
                             const uint64_t M0 = ballot(hm0) & segm, M1 = ballot(hm1) & segm;
                             const uint32_t f0 = shfl(lm0, M0 ? 63u - (uint32_t)__builtin_clzll(M0) : 0u);
                             const uint32_t f1 = shfl(lm1, M1 ? 63u - (uint32_t)__builtin_clzll(M1) : 0u);
-#pragma unroll
-                            for (uint32_t q = 0; q < LV; ++q) {
-                                if (!((emsk & php) >> q & 1u)) continue;
-                                const bool tq = (((q < 4u ? t8[0] : t8[1]) >> (8u * (q & 3u))) & 1u) != 0u;
-                                const bool gm = (q < 4u || !spl) && (tq ? M1 : M0) != 0ull;
-                                phw |= (gm ? (tq ? f1 : f0) : (uint32_t)(elab[key_of(q)] >> 4)) << (4u * q);
+                            for (uint32_t m = emsk & php; m; m &= m - 1u) {
+                                const uint32_t q = (uint32_t)__builtin_ctz(m);
+                                const uint32_t tb = byteq(t8[0], t8[1], q) & 1u;
+                                const bool gm = (q < 4u || !spl) && (tb ? M1 : M0) != 0ull;
+                                const uint32_t key = (q < 4u ? kA : kB) * K2 + 2u * byteq(r8[0], r8[1], q) + tb;
+                                phw |= (gm ? (tb ? f1 : f0) : (uint32_t)(elab[key] >> 4)) << (4u * q);
                             }
                             /* each (segment, type)'s last edge in the chunk carries the state out: a
                              * later edge of the lane, or the first edge of that type in the next lane
                              * holding one, in the same segment means it is not the last */
-                            const uint32_t segA = R1 ? kA : (kA * 16u + uA), segB = R1 ? kB : (kB * 16u + uB);
-                            uint32_t g0 = 0xFFFFFFFFu, g1 = 0xFFFFFFFFu; /* the segment of the lane's first edge per type */
-#pragma unroll
-                            for (int q = (int)LV - 1; q >= 0; --q) {
-                                if (!((emsk >> q) & 1u)) continue;
-                                const bool tq = ((((uint32_t)q < 4u ? t8[0] : t8[1]) >> (8u * ((uint32_t)q & 3u))) & 1u) != 0u;
-                                if (tq) g1 = (uint32_t)q < 4u ? segA : segB;
-                                else g0 = (uint32_t)q < 4u ? segA : segB;
-                            }
                             const uint64_t above = ~((2ull << lane) - 1ull);
                             const uint64_t N0 = ballot(g0 != 0xFFFFFFFFu) & above, N1 = ballot(g1 != 0xFFFFFFFFu) & above;
                             uint32_t nx0 = shfl(g0, N0 ? (uint32_t)__builtin_ctzll(N0) : lane);
                             uint32_t nx1 = shfl(g1, N1 ? (uint32_t)__builtin_ctzll(N1) : lane);
                             nx0 = N0 ? nx0 : 0xFFFFFFFFu;
                             nx1 = N1 ? nx1 : 0xFFFFFFFFu;
-#pragma unroll
-                            for (int q = (int)LV - 1; q >= 0; --q) {
-                                if (!((emsk >> q) & 1u)) continue;
-                                const uint32_t bs = 8u * ((uint32_t)q & 3u);
-                                const bool tq = ((((uint32_t)q < 4u ? t8[0] : t8[1]) >> bs) & 1u) != 0u;
-                                const uint32_t sg = (uint32_t)q < 4u ? segA : segB;
-                                if ((tq ? nx1 : nx0) != sg) {
-                                    const uint32_t cb = (((uint32_t)q < 4u ? c0 : c1) >> bs) & 0xFFu;
-                                    elab[key_of((uint32_t)q)] = (unsigned char)((cb & 0xFu) | ((cb >> 4) ? (cb & 0xF0u) : (((phw >> (4u * (uint32_t)q)) & 0xFu) << 4)));
+                            for (uint32_t m = emsk; m;) {
+                                const uint32_t q = 31u - (uint32_t)__builtin_clz(m);
+                                m &= ~(1u << q);
+                                const uint32_t tb = byteq(t8[0], t8[1], q) & 1u;
+                                const uint32_t sg = q < 4u ? segA : segB;
+                                if ((tb ? nx1 : nx0) != sg) {
+                                    const uint32_t cb = byteq(c0, c1, q);
+                                    const uint32_t key = (q < 4u ? kA : kB) * K2 + 2u * byteq(r8[0], r8[1], q) + tb;
+                                    elab[key] = (unsigned char)((cb & 0xFu) | ((cb >> 4) ? (cb & 0xF0u) : (((phw >> (4u * q)) & 0xFu) << 4)));
                                 }
-                                if (tq) nx1 = sg;
+                                if (tb) nx1 = sg;
                                 else nx0 = sg;
                             }
                         } else {
@@ -1556,16 +1554,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                         const uint32_t rA = etab[kA] + En - (multi ? shfl(En, sA) : 0u);
                         const uint32_t rB = split ? etab[kB] : rA + nA;
                         const uint64_t gA = Sa + shfl(rl, kA), gB = Sa + shfl(rl, kB);
-#pragma unroll
-                        for (uint32_t q = 0; q < LV; ++q) {
-                            if (!((emsk >> q) & 1u)) continue;
-                            const uint32_t bs = 8u * (q & 3u);
-                            const uint32_t em = q < 4u ? em0 : em1;
-                            const uint32_t k = (q < 4u ? rA : rB) + (uint32_t)__builtin_popcount(em & ((1u << bs) - 1u));
-                            const uint32_t cb = ((q < 4u ? c0 : c1) >> bs) & 0xFFu;
-                            const uint32_t rq = ((q < 4u ? r8[0] : r8[1]) >> bs) & 0xFFu;
-                            const uint32_t tq = ((q < 4u ? t8[0] : t8[1]) >> bs) & 1u;
-                            const uint32_t prev = ((((q < 4u ? cbf0 : cbf1) >> bs) & 0xFu)) | (((phw >> (4u * q)) & 0xFu) << 4);
+                        for (uint32_t m = emsk; m; m &= m - 1u) {
+                            const uint32_t q = (uint32_t)__builtin_ctz(m);
+                            const uint32_t k = (q < 4u ? rA : rB) + (uint32_t)__builtin_popcount(emsk & ((1u << q) - 1u) & (q < 4u ? 0x0Fu : 0xF0u));
+                            const uint32_t cb = byteq(c0, c1, q), rq = byteq(r8[0], r8[1], q), tq = byteq(t8[0], t8[1], q) & 1u;
+                            const uint32_t prev = (byteq(cbf0, cbf1, q) & 0xFu) | (((phw >> (4u * q)) & 0xFu) << 4);
                             const uint64_t j = c + o8 + q;
                             const uint4 rec = make_uint4((uint32_t)j, (uint32_t)(j >> 32), H.s0 + (q < 4u ? kA : kB),
                                                          rq | (tq << 8) | (cb << 16) | (prev << 24));
