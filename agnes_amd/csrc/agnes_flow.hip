@@ -80,6 +80,10 @@ constexpr uint32_t F_INST = 0, F_VALUE = 2048, F_VAL = 4096, F_ROUND = 6144, F_T
 #ifndef AGNES_FLOW_FAST_START
 #define AGNES_FLOW_FAST_START 1 /* static first batches, the first chunk's DMA before the set constants */
 #endif
+#ifndef AGNES_FLOW_QN
+#define AGNES_FLOW_QN AGNES_QUEUE_N /* work-queue counters (the blocks of one share its batches) */
+#endif
+static_assert(AGNES_FLOW_QN >= 1 && AGNES_FLOW_QN <= AGNES_QUEUE_N, "flow queue counters");
 #ifndef AGNES_FLOW_SMALLB
 #define AGNES_FLOW_SMALLB 4
 #endif
@@ -304,7 +308,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
     const uint32_t RK = (128u - R) * 0x01010101u;
 
     /* ---- work queue: batches of FB, then SMALLB ones for the tail ---- */
-    const uint32_t qn = gridDim.x < QN ? gridDim.x : QN;
+    const uint32_t qn = gridDim.x < AGNES_FLOW_QN ? gridDim.x : AGNES_FLOW_QN;
     const uint32_t qk = blockIdx.x % qn;
     uint32_t* const ctr = a.list_count + 1u + qk;
     /* batch size: FB, or (launcher) fewer for a batch too small to give every wave
