@@ -39,7 +39,13 @@ KERNELS = {
     "edge_emit": r"agnes::edges::edge_walk<true,",
     "event_count": r"agnes::events::event_walk<false,",
     "event_count_list": r"agnes::events::event_count_list<",
-    "event_emit": r"agnes::events::(event_emit_stream|event_emit_wave|event_walk<true,)",
+    "event_emit": r"agnes::events::(event_emit_stream<\w+, \w+, false>|event_emit_wave|event_walk<true,)",
+    # agnes_tally_records off the flow route (round 5): the emit writing the segments
+    "seg_emit": r"agnes::events::event_emit_stream<\w+, \w+, true>",
+    "seg_walk": r"agnes::events::seg_walk<",
+    "seg_compact": r"agnes::events::seg_compact",
+    "edge_seg_walk": r"agnes::edges::edge_seg_walk<",
+    "edge_compact": r"agnes::edges::edge_compact",
 }
 
 
