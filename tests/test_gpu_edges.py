@@ -190,7 +190,7 @@ def test_edges_offsets_going_back(eng, R):
 
 # ------------------------------------------------ round 5: agnes_tally_edges (fused)
 
-def _tally_edges_check(eng, cfg, hb, power, states=None):
+def _tally_edges_check(eng, cfg, hb, power, states=None, shift=0):
     """agnes_tally_edges: the tally and its edge summary in one call, segmented by
     instance (the flow kernel finds and writes them on the C2 / C3 route), against the
     checker's codes, States and orc_edges over them; then agnes_edges_compact's dense
@@ -198,6 +198,12 @@ def _tally_edges_check(eng, cfg, hb, power, states=None):
     eng.upload_power(power)
     db = DeviceBatch.from_host(hb, eng.device)
     n = max(hb.n_votes, 1)
+    if shift:  # round / type off a 16-B boundary: the windowed walks' 4-B path
+        def shifted(t):
+            buf = torch.zeros(t.numel() + 16, dtype=torch.uint8, device=eng.device)
+            buf[shift:shift + t.numel()] = t
+            return buf[shift:shift + t.numel()]
+        db.round, db.type = shifted(db.round), shifted(db.type)
     codes = torch.full((n,), 0xEE, dtype=torch.uint8, device=eng.device)
     dst = None if states is None else states_to_device(states, eng.device)
     seg = torch.full((n, 16), 0xCD, dtype=torch.uint8, device=eng.device)
@@ -235,6 +241,15 @@ def test_tally_edges_generated(eng, name):
     states = _start_states(p.n_instances) if cfg.flags & abi.FLAG_STATE_MACHINE else None
     recs = _tally_edges_check(eng, cfg, hb, power, states)
     assert len(recs) > 0
+
+
+@pytest.mark.parametrize("shift", [4, 8])
+def test_tally_edges_unaligned_columns(eng, shift):
+    """C4's route with the round / type columns off a 16-B boundary: the segmented
+    edges from the 4-B-window walk"""
+    p, hb, power, cfg = _make("c4_small")
+    states = _start_states(p.n_instances) if cfg.flags & abi.FLAG_STATE_MACHINE else None
+    assert len(_tally_edges_check(eng, cfg, hb, power, states, shift)) > 0
 
 
 @pytest.mark.parametrize("nil", [300, 700])

@@ -205,6 +205,47 @@ def test_tally_records_revisited_rounds(eng, nil):
     _check(eng, abi.config(abi.MODE_REFERENCE, 0, 5), hb, power)
 
 
+def _shifted(eng, t, shift):
+    """a copy of the u8 column t placed `shift` bytes past a 16-B boundary"""
+    n = t.numel()
+    buf = torch.zeros(n + 16, dtype=torch.uint8, device=eng.device)
+    buf[shift:shift + n] = t
+    return buf[shift:shift + n]
+
+
+@pytest.mark.parametrize("shift", [4, 8])
+def test_tally_records_unaligned_columns(eng, shift):
+    """DEDUP + RoundSkip with the round / type columns off a 16-B boundary: the
+    segmented records come from the lane-per-instance walk (seg_walk) instead of the
+    stream emit, same records"""
+    p = abi.gen_params(seed=63, n_instances=1500, n_vals=90, rounds_min=1, rounds_max=3, nil_permille=300,
+                       dup_permille=100, equiv_permille=100, higher_permille=50)
+    hb = ol.gen_batch(p)
+    power = ol.gen_power(63, 1, 90, abi.POWER_UNIFORM, 1, 5000)
+    cfg = abi.config(abi.MODE_DEDUP, abi.FLAG_STATE_MACHINE | abi.FLAG_ROUND_SKIP, 4)
+    st = abi.new_states(1500, 1, abi.STEP_PREVOTE)
+    eng.upload_power(power)
+    db = DeviceBatch.from_host(hb, eng.device)
+    db.round, db.type = _shifted(eng, db.round, shift), _shifted(eng, db.type, shift)
+    o_codes, o_states, _, o_offs, o_ev = ol.events(cfg, hb, power, None, st, threads=THREADS)
+    _check_records(eng, cfg, hb, db, st, True, o_codes, o_states, o_offs, o_ev)
+
+
+def test_tally_records_many_keys(eng):
+    """40 rounds (80 keys: more than the stream emit's LDS value slots hold) on the
+    DEDUP route: the segments from seg_walk"""
+    p = abi.gen_params(seed=64, n_instances=400, n_vals=20, rounds_min=1, rounds_max=40, nil_permille=300,
+                       dup_permille=50, equiv_permille=50)
+    hb = ol.gen_batch(p)
+    power = ol.gen_power(64, 1, 20, abi.POWER_UNIFORM, 1, 100)
+    cfg = abi.config(abi.MODE_DEDUP, 0, 40)
+    eng.upload_power(power)
+    db = DeviceBatch.from_host(hb, eng.device)
+    o_codes, o_states, _, o_offs, o_ev = ol.events(cfg, hb, power, None, None, threads=THREADS)
+    assert len(o_ev) > 0
+    _check_records(eng, cfg, hb, db, None, True, o_codes, o_states, o_offs, o_ev)
+
+
 def test_tally_events_fifteen_rounds(eng):
     """max_rounds 15 with the State machine: the counts do not fit the flow kernel's
     LDS, so the count pass runs (same records)"""
