@@ -251,6 +251,9 @@ __device__ __attribute__((noinline)) uint32_t label_back(const uint32_t* inst_co
 #ifndef AGNES_FLOW_WPE
 #define AGNES_FLOW_WPE 3
 #endif
+#ifndef AGNES_FLOW_CODE_VMCNT
+#define AGNES_FLOW_CODE_VMCNT 1
+#endif
 #ifndef AGNES_FLOW_XWPE
 #define AGNES_FLOW_XWPE 3 /* the records / edges variants, one round */
 #endif
@@ -406,14 +409,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
         h.stage = 3;
     };
     uint32_t spar = 0; /* States staging buffer of the current batch */
+    /* the last flush sent a whole chunk's codes as ONE store with every lane active and
+     * no DMA has been issued since: the chunk top's wait may leave that store in flight */
+    bool dc_one = false;
     auto dma_states = [&](const Hdr& h, uint32_t par) { /* the batch's States into LDS (64 B each) */
         const uint32_t m = h.e0 - h.s0;
+        dc_one = false;
         if (!SM || m == 0u) return;
         const unsigned char* const g = reinterpret_cast<const unsigned char*>(st_in + h.s0);
         glds16(g + 16u * (lane < 4u * m ? lane : 0u), sb + par * (FB * 64u));
         if (m > 16u) glds16(g + 16u * (64u + lane < 4u * m ? 64u + lane : 0u), sb + par * (FB * 64u) + 1024u);
     };
     auto dma_chunk = [&](uint64_t c, uint32_t lo, uint32_t lim) { /* the chunk's votes lo..lim into the slot */
+        dc_one = false;
         __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): the slot's LDS reads are done */
         if (lo == 0u && lim >= CH) {
             sdma_chunk(a.vb.instance + c, a.vb.value + c, a.vb.validator + c, a.vb.round + c, a.vb.type + c, o16, o4,
@@ -442,10 +450,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
     uint64_t dc_at = ~0ull;
     uint32_t dc0 = 0, dc1 = 0, dc_act = 0; /* dc_act: bit 0 unit A, bit 1 unit B active */
     auto flush = [&]() {
+        dc_one = false;
         if (dc_at != ~0ull) {
-            if (dc_act == 3u) sstore8(a.codes + dc_at, o8, dc0, dc1);
-            else if (dc_act == 1u) sstore4(a.codes + dc_at, o8, dc0);
-            else if (dc_act == 2u) sstore4(a.codes + dc_at, o8 + 4u, dc1);
+            if (AGNES_FLOW_CODE_VMCNT && !ballot(dc_act != 3u)) {
+                sstore8(a.codes + dc_at, o8, dc0, dc1);
+                dc_one = true;
+            } else {
+                if (dc_act == 3u) sstore8(a.codes + dc_at, o8, dc0, dc1);
+                else if (dc_act == 1u) sstore4(a.codes + dc_at, o8, dc0);
+                else if (dc_act == 2u) sstore4(a.codes + dc_at, o8 + 4u, dc1);
+            }
             dc_at = ~0ull;
         }
     };
@@ -557,8 +571,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                 FDIAG(++dg_c;)
                 const uint64_t c = Sa + rc;
                 const uint32_t lo_r = rc == 0u ? lead : 0u; /* the chunk's active votes: lo_r .. hi_r */
-                if (pf_at != c) dma_chunk(c, lo_r, Lend - rc); /* not prefetched: a wave's first chunk */
-                dma_wait(); /* this chunk's DMA (and a new batch's States) have landed */
+                const bool fresh = pf_at != c;
+                if (fresh) dma_chunk(c, lo_r, Lend - rc); /* not prefetched: a wave's first chunk */
+                /* this chunk's DMA (and a new batch's States) have landed; a whole-chunk code
+                 * store issued behind that DMA may stay in flight */
+                if (AGNES_FLOW_CODE_VMCNT && dc_one && !fresh) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+                else dma_wait();
+                dc_one = false;
                 /* raised priority from here until the next chunk's DMA and the deferred code
                  * store are out: a wave's memory traffic goes out ahead of the other waves'
                  * K2-K4 work (same-box A/B: flow -1 % on C2 and C3) */
