@@ -38,8 +38,6 @@ struct agnes_ctx {
     uint32_t list_cap = 0;
     uint64_t* d_scan = nullptr; /* edge-offset scan: block totals */
     uint64_t scan_cap = 0;
-    uint64_t* d_eoffs = nullptr; /* (agnes_tally_records, unfused routes) the dense offsets */
-    uint64_t eoffs_cap = 0;
     void* d_dd = nullptr;       /* agnes_dedup_first: bucket counts, scan scratch, (key, index) pairs */
     uint64_t dd_cap = 0;
     int32_t* d_edtab = nullptr; /* Ed25519 fixed-base table (agnes_wire_ingest), built on first use */
@@ -244,7 +242,6 @@ void agnes_ctx_destroy(agnes_ctx* c) {
     if (c->d_err) (void)hipFree(c->d_err);
     if (c->d_list) (void)hipFree(c->d_list);
     if (c->d_scan) (void)hipFree(c->d_scan);
-    if (c->d_eoffs) (void)hipFree(c->d_eoffs);
     if (c->d_dd) (void)hipFree(c->d_dd);
     if (c->d_edtab) (void)hipFree(c->d_edtab);
     if (c->order_ev) (void)hipEventDestroy(c->order_ev);
@@ -714,30 +711,10 @@ int agnes_tally_records(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_
                                                reinterpret_cast<const uint32_t*>(c->d_err + AGNES_ERR_BYTES / 8) +
                                                    AGNES_WALK_COUNT,
                                                counts, out, st));
-    if (b->n_instances && agnes_seg_emit_ok(b, codes, cfg->max_rounds)) {
-        /* the event stream's count pass + scan into the context's dense offsets, then its
-         * emit pass writing each record to its instance's segment */
-        const uint64_t words = agnes_edges_scratch_words(b->n_instances), need = (uint64_t)b->n_instances + 1u;
-        if (words > c->scan_cap || need > c->eoffs_cap) {
-            AGNES_TRY(hipStreamSynchronize(st));
-            if (words > c->scan_cap) {
-                if (c->d_scan) AGNES_TRY(hipFree(c->d_scan));
-                c->d_scan = nullptr;
-                c->scan_cap = 0;
-                AGNES_TRY(hipMalloc(&c->d_scan, words * sizeof(uint64_t)));
-                c->scan_cap = words;
-            }
-            if (need > c->eoffs_cap) {
-                if (c->d_eoffs) AGNES_TRY(hipFree(c->d_eoffs));
-                c->d_eoffs = nullptr;
-                c->eoffs_cap = 0;
-                AGNES_TRY(hipMalloc(&c->d_eoffs, need * sizeof(uint64_t)));
-                c->eoffs_cap = need;
-            }
-        }
-        AGNES_TRY(agnes_launch_events(b, codes, cfg->max_rounds, c->d_eoffs, nullptr, c->d_scan, st));
-        return status_of(agnes_launch_seg_emit(b, codes, cfg->max_rounds, mult, c->d_eoffs, counts, out, st));
-    }
+    if (b->n_instances && agnes_seg_emit_ok(b, codes, cfg->max_rounds))
+        /* the event stream's emit pass writing each record to its instance's segment
+         * (and the counts): no count pass before it */
+        return status_of(agnes_launch_seg_emit(b, codes, cfg->max_rounds, mult, counts, out, st));
     return status_of(agnes_launch_seg_walk(b, codes, cfg->max_rounds, mult, nullptr, nullptr, counts, out, st));
 }
 

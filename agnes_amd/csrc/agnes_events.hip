@@ -546,10 +546,13 @@ __device__ __forceinline__ void load_pass_v(const EvArgs& a, uint64_t j0, uint64
 }
 
 /* SEG (agnes_tally_records on the routes whose tally does not write the records): the
- * same pass, each record to its instance's segment instead of the dense stream -- the
- * dense position d of instance i's record (offs: the count pass + scan) moves to
- * seg + d + mult * offsets[i] - offs[i] (per batch instance in LDS, where the staging
- * area was), and the batch's counts[i] = offs[i + 1] - offs[i] */
+ * same pass, each record to its instance's segment instead of the dense stream, with no
+ * count pass before it.  Positions are batch-relative: the pass where instance k's first
+ * vote lies gives its first record's position fpos[k] (the records of the pass before
+ * that vote: the lane's exclusive scan and its masks, read from the lane holding it), so
+ * a record at batch-relative position d goes to seg + d + (mult * offsets[i] - fpos[k])
+ * (per batch instance in LDS, where the staging area was), and at the batch's end
+ * counts[i] = fpos[k + 1] - fpos[k] (the batch's total for its last instance) */
 template <uint32_t V, uint32_t WPE, bool SEG = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void event_emit_stream(EvArgs a) {
     constexpr uint32_t P = 64u * V; /* votes per pass */
@@ -561,22 +564,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     uint32_t* const lab = reinterpret_cast<uint32_t*>(agnes_smem) + wave * (EB * keys + 6u * EV_STAGE);
     uint32_t* const stage = lab + EB * keys;
     uint64_t* const dl = reinterpret_cast<uint64_t*>(stage); /* (SEG) [EB] */
+    uint32_t* const fpos = stage + 2u * EB;                  /* (SEG) [EB] */
     uint32_t b = blockIdx.x * 4u + wave;
     if (b >= NB) return; /* wave-uniform */
     EvBatch B = ev_batch(a, b, ev_load(a, b, lane));
+    /* (SEG) the batch's first instance starts at position 0 */
     auto seg_batch = [&](const EvBatch& X) {
-        if (SEG && lane < X.m) {
-            const uint32_t i = X.s0 + lane;
-            const uint64_t o = a.offs[i];
-            a.counts[i] = a.offs[i + 1u] - o;
-            dl[lane] = (uint64_t)a.mult * a.vb.offsets[i] - o;
+        if (SEG && lane == 0u) {
+            fpos[0] = 0u;
+            dl[0] = (uint64_t)a.mult * (((uint64_t)X.ohi << 32) | X.olo);
+        }
+    };
+    /* (SEG) the batch's counts from its instances' first positions and its total */
+    auto seg_counts = [&](const EvBatch& X, uint32_t total) {
+        if constexpr (SEG) {
+            __builtin_amdgcn_wave_barrier();
+            const uint64_t ol = ((uint64_t)X.ohi << 32) | X.olo;
+            /* an instance starting at the batch's end (no vote left) starts at the total */
+            const uint32_t st = lane == 0u ? 0u : (ol >= X.Om ? total : fpos[lane < EB ? lane : 0u]);
+            const uint32_t nx = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane + 1u) << 2), (int)st);
+            if (lane < X.m) a.counts[X.s0 + lane] = (uint64_t)((lane + 1u < X.m ? nx : total) - st);
         }
     };
     seg_batch(B);
     uint32_t nb = b + BS;
     EvRaw NR = nb < NB ? ev_load(a, nb, lane) : EvRaw{0u, 0u};
-    uint64_t ncnt = nb < NB ? a.offs[nb * EB] : 0u;
-    uint64_t cnt = a.offs[B.s0]; /* the batch's first record */
+    uint64_t ncnt = (!SEG && nb < NB) ? a.offs[nb * EB] : 0u;
+    uint64_t cnt = SEG ? 0u : a.offs[B.s0]; /* the batch's first record (SEG: batch-relative) */
     uint64_t c = B.O0 & ~(uint64_t)(V - 1u);
     PassV<V> cur;
     load_pass_v<V>(a, c + V * lane, NV, cur);
@@ -666,6 +680,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 fr[1] = (nn && tb && fr[1] == 0xFFFFFFFFu) ? rid[s] : fr[1];
             }
             const uint32_t incl = wave_scan_incl(n_rec);
+            if constexpr (SEG) {
+                /* the first positions of the batch's instances starting in this pass */
+                uint64_t rest = __builtin_amdgcn_ballot_w64(lane >= 1u && lane < B.m && ol >= c && ol < c + P);
+                const uint32_t ex = incl - n_rec;
+                while (rest) {
+                    const uint32_t k = (uint32_t)__builtin_ctzll(rest);
+                    rest &= rest - 1ull;
+                    const uint32_t ks = (uint32_t)__builtin_amdgcn_readlane(B.olo, k) - (uint32_t)c; /* [0, P) */
+                    const uint32_t L = ks / V, below = (1u << (ks % V)) - 1u;
+                    const uint32_t pos = (uint32_t)cnt + (uint32_t)__builtin_amdgcn_readlane(ex, L) +
+                                         (uint32_t)__builtin_popcount((uint32_t)__builtin_amdgcn_readlane(hasm, L) & below) +
+                                         (uint32_t)__builtin_popcount((uint32_t)__builtin_amdgcn_readlane(skm, L) & below);
+                    const uint64_t okk = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(B.ohi, k) << 32) |
+                                         (uint32_t)__builtin_amdgcn_readlane(B.olo, k);
+                    if (lane == 0u) {
+                        fpos[k] = pos;
+                        dl[k] = (uint64_t)a.mult * okk - pos;
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
             uint32_t slot[V];
 #pragma unroll
             for (uint32_t s = 0; s < V; ++s) slot[s] = 0u;
@@ -822,6 +857,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             }
             cnt += total;
         }
+        if (sw) seg_counts(B, (uint32_t)cnt);
         if (last) break;
         if (sw) { /* the wave's next batch */
             b = nb;
@@ -830,7 +866,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             nb = b + BS;
             if (nb < NB) {
                 NR = ev_load(a, nb, lane);
-                ncnt = a.offs[nb * EB];
+                ncnt = SEG ? 0u : a.offs[nb * EB];
             }
             __builtin_amdgcn_wave_barrier();
             for (uint32_t k = lane; k < EB * keys; k += 64u) lab[k] = 0u;
@@ -923,12 +959,13 @@ bool agnes_seg_emit_ok(const agnes_vote_batch* vb, const uint8_t* codes, uint32_
 }
 
 hipError_t agnes_launch_seg_emit(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds, uint32_t mult,
-                                 const uint64_t* offs, uint64_t* counts, void* seg, hipStream_t st) {
+                                 uint64_t* counts, void* seg, hipStream_t st) {
     using namespace agnes::events;
     const uint32_t n = vb->n_instances;
     if (n == 0) return hipSuccess;
     if (!agnes_seg_emit_ok(vb, codes, max_rounds)) return hipErrorInvalidValue;
-    EvArgs a{*vb, codes, const_cast<uint64_t*>(offs), nullptr, 2u * max_rounds, reinterpret_cast<uint4*>(seg), counts, mult};
+    static_assert(6u * EV_STAGE >= 3u * EB, "the (SEG) per-instance deltas and positions fit the staging area");
+    EvArgs a{*vb, codes, nullptr, nullptr, 2u * max_rounds, reinterpret_cast<uint4*>(seg), counts, mult};
     const uint32_t NB = (n + EB - 1u) / EB;
     const size_t lds_s = (size_t)4u * (EB * a.keys + 6u * EV_STAGE) * sizeof(uint32_t);
     const void* fn = reinterpret_cast<const void*>(&event_emit_stream<4u, 5u, true>);

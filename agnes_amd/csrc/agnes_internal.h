@@ -109,11 +109,11 @@ hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t
  * list (the flow route's walk list; list_n on the device), one lane per instance; and
  * the dense stream from them (offs: the exclusive scan of the counts) */
 /* (agnes_tally_records, routes without the fused records) the emit pass writing the
- * segmented records from the dense offsets of the count pass + scan; the columns
- * 16-B aligned and 2 * max_rounds <= 64 (agnes_seg_emit_ok), else the walk */
+ * segmented records and the counts (no count pass); the columns 16-B aligned and
+ * 2 * max_rounds <= 64 (agnes_seg_emit_ok), else the walk */
 bool agnes_seg_emit_ok(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds);
 hipError_t agnes_launch_seg_emit(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds, uint32_t mult,
-                                 const uint64_t* offs, uint64_t* counts, void* seg, hipStream_t st);
+                                 uint64_t* counts, void* seg, hipStream_t st);
 hipError_t agnes_launch_seg_walk(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds, uint32_t mult,
                                  const uint32_t* list, const uint32_t* list_n, uint64_t* counts, void* seg,
                                  hipStream_t stream);

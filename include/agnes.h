@@ -730,9 +730,9 @@ uint64_t agnes_events_capacity(const agnes_config* cfg, const agnes_vote_batch* 
  * Instance i's records are out[seg(i) + k], k < counts[i], in vote order, with
  * seg(i) = batch->offsets[i] (2 * offsets[i] with AGNES_FLAG_ROUND_SKIP); the slots
  * between an instance's last record and the next segment are left as they were.  Every
- * other route counts them (the event stream's count pass + scan, into a context buffer)
- * and writes the segments with the stream emit pass (a lane-per-instance walk for the
- * flow route's walk-list instances, columns off 16-B alignment, or max_rounds > 32).
+ * other route writes the segments and the counts with the event stream's emit pass (no
+ * count pass; a lane-per-instance walk for the flow route's walk-list instances,
+ * columns off 16-B alignment, or max_rounds > 32).
  * counts (DEVICE, n_instances u64); out (DEVICE, 16-B aligned) must hold
  * agnes_events_capacity(cfg, batch) records; the segments are the instances' vote
  * ranges, so offsets must not go back (overlapping ranges overlap their segments).
