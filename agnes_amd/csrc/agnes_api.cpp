@@ -294,6 +294,15 @@ int64_t agnes_lds_bytes_per_wave(const agnes_config* cfg, uint32_t n_vals) {
     return b > AGNES_MAX_LDS_PER_WAVE ? AGNES_E_UNSUPPORTED : b;
 }
 
+#ifndef AGNES_REC_FUSED_MIN_VOTES
+#define AGNES_REC_FUSED_MIN_VOTES (1ull << 28) /* several rounds: smaller batches take the emit pass */
+#endif
+/* the environment variable of the same name overrides it (the tests run both routes) */
+static uint64_t rec_fused_min_votes() {
+    const char* e = std::getenv("AGNES_REC_FUSED_MIN_VOTES");
+    return e && *e ? std::strtoull(e, nullptr, 0) : (uint64_t)AGNES_REC_FUSED_MIN_VOTES;
+}
+
 static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b,
                       uint8_t* codes, const agnes_state* states_in, agnes_state* states,
                       agnes_carry_rec* carry, const agnes_set_info* sets, uint32_t n_sets, uint32_t sets_dom,
@@ -378,10 +387,19 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     /* agnes_tally_events: the flow route counts each instance's event records as it goes */
     if (ev_counts) {
         const uint32_t route = (cfg->flags >> AGNES_ROUTE_SHIFT) & AGNES_ROUTE_MASK;
-        const bool flow = !wide_all && !w64 && route == AGNES_ROUTE_AUTO && cfg->mode == AGNES_MODE_REFERENCE &&
-                          !(cfg->flags & AGNES_FLAG_ROUND_SKIP) && agnes_flow_counts_events(cfg->flags, cfg->max_rounds, edges);
+        bool flow = !wide_all && !w64 && route == AGNES_ROUTE_AUTO && cfg->mode == AGNES_MODE_REFERENCE &&
+                    !(cfg->flags & AGNES_FLAG_ROUND_SKIP) && agnes_flow_counts_events(cfg->flags, cfg->max_rounds, edges);
         if (flow) a.ev_counts = ev_counts;
         if (flow && rec_out) a.rec_out = rec_out; /* agnes_tally_records / _edges: the flow kernel writes them too */
+        /* several rounds: the fused records variant runs at 2 waves per SIMD (its VGPRs),
+         * which pays on a large batch but not on a small one, where the tally's tail
+         * grows with it: C3 (7.5e8 votes) 4.83 ms fused vs 5.19 through the emit pass,
+         * its 8-GPU shard (9.4e7) 0.95 vs 0.80 */
+        if (rec_out && !edges && cfg->max_rounds > 1u && b->n_votes < rec_fused_min_votes()) {
+            a.ev_counts = nullptr;
+            a.rec_out = nullptr;
+            flow = false;
+        }
         if (flow && edges) a.edges = 1u;
         if (counted) *counted = flow;
     }

@@ -64,6 +64,14 @@ def _check(eng, cfg, hb, power, states=None, in_place=True):
     assert np.array_equal(e_offs.cpu().numpy().view(np.uint64), g_offs)
     assert e_recs.cpu().numpy().tobytes() == out[:n].cpu().numpy().tobytes()
     _check_records(eng, cfg, hb, db, states, in_place, o_codes, o_states, o_offs, o_ev)
+    if cfg.max_rounds > 1:
+        # several rounds: batches under AGNES_REC_FUSED_MIN_VOTES take the emit pass;
+        # the fused records variant of the flow kernel with the threshold at 0
+        os.environ["AGNES_REC_FUSED_MIN_VOTES"] = "0"
+        try:
+            _check_records(eng, cfg, hb, db, states, in_place, o_codes, o_states, o_offs, o_ev)
+        finally:
+            del os.environ["AGNES_REC_FUSED_MIN_VOTES"]
     return o_ev
 
 
