@@ -725,8 +725,10 @@ uint64_t agnes_events_capacity(const agnes_config* cfg, const agnes_vote_batch* 
 
 /* The same records SEGMENTED by instance (round 5): no scan between the tally and the
  * records, so on the flow route (REFERENCE without RoundSkip, max_rounds <= 15, every
- * offset a multiple of 4 -- the C2 / C3 streams) the tally kernel writes them itself
- * while the votes are in registers: the records cost no second pass over the votes.
+ * offset a multiple of 4 -- the C2 / C3 streams; with several rounds, batches of at
+ * least 2^28 votes, or the AGNES_REC_FUSED_MIN_VOTES environment variable's count) the
+ * tally kernel writes them itself while the votes are in registers: the records cost no
+ * second pass over the votes.
  * Instance i's records are out[seg(i) + k], k < counts[i], in vote order, with
  * seg(i) = batch->offsets[i] (2 * offsets[i] with AGNES_FLAG_ROUND_SKIP); the slots
  * between an instance's last record and the next segment are left as they were.  Every
