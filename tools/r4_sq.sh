@@ -4,7 +4,7 @@
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/sq && export TMPDIR=/tmp
 P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY"
 P2="SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_SCA SQ_WAIT_ANY SQ_INSTS_VMEM SQ_ACTIVE_INST_ANY"
-for spec in ${LIBS:-alias=agnes_amd/_exp/lib_alias.so cur=-}; do
+for spec in ${LIBS:-cur=-}; do
   name=${spec%%=*}; path=${spec#*=}
   if [ "$path" = "-" ]; then run="python3 bench.py"; else run="python3 tools/withlib.py $path bench.py"; fi
   i=0

@@ -1,5 +1,6 @@
 #!/bin/bash
-# round-5 GPU call F: records / edges parity, then the c2 / c3 records and edges timings
+# one GPU call: the records / edges GPU parity tests, then per workload (CFGS) the step, the
+# fused records and edges calls and the round-4 edge walks (ms per call)
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/r5
 timeout -k 10 900 python -u -m pytest tests -q -m "gpu and not slow" --timeout 200 --timeout-method thread -k "edges or tally_events" > gpurun_out/r5/tests_f.log 2>&1
 rc=$?

@@ -1,5 +1,6 @@
 #!/bin/bash
-# round-5: SQ counters of the step's flow and of the records / edges variants (CFG, default c2)
+# one GPU call: SQ counters of the flow variants of one workload (CFG, default c2): the step, the
+# record counts, the records and the edges (KS: ";"-separated kernel-name substrings)
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/r5
 CNT=${CNT:-"SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU"}
 rm -rf gpurun_out/r5/sq_${CFG:-c2}
