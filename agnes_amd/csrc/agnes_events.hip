@@ -237,22 +237,53 @@ __global__ __launch_bounds__(64) void seg_walk(EvArgs a, const uint32_t* list, c
     counts[i] = cnt;
 }
 
-/* the dense stream from the segmented one: wave w copies instances 32w .. 32w + 31,
- * each instance's records by the 64 lanes, adding the instance id (agnes_vote_event) */
+/* the dense stream from the segmented one, adding the instance id (agnes_vote_event):
+ * wave w writes the dense records of instances 32w .. 32w + 31 -- one contiguous range,
+ * offs[32w] .. offs[32w + 32] -- 64 at a time, lane l the record at position p: its
+ * instance by a 5-step binary search over the wave's offsets (one per lane, relative
+ * to the range's start), then one 16-B read of that instance's segment.  Every lane
+ * has a record in every step but the last (one instance per step left lanes idle) */
 __global__ __launch_bounds__(256) void seg_compact(agnes_vote_batch vb, uint32_t mult, const uint4* seg,
                                                    const uint64_t* offs, agnes_vote_event* out) {
     const uint32_t lane = threadIdx.x & 63u, w = blockIdx.x * 4u + (threadIdx.x >> 6);
-    const uint32_t n = vb.n_instances;
-    for (uint32_t i = 32u * w; i < n && i < 32u * w + 32u; ++i) {
-        const uint64_t o = offs[i], cnt = offs[i + 1u] - o;
-        const uint4* const src = seg + (uint64_t)mult * vb.offsets[i];
-        for (uint64_t k = lane; k < cnt; k += 64u) {
-            const uint4 r = src[k];
-            uint2* const q = reinterpret_cast<uint2*>(out + o + k);
-            q[0] = make_uint2(r.x, r.y);
-            q[1] = make_uint2(i, r.z);
-            q[2] = make_uint2(r.w, 0u);
+    const uint32_t n = vb.n_instances, i0 = 32u * w;
+    if (i0 >= n) return; /* wave-uniform */
+    const uint32_t m = n - i0 < 32u ? n - i0 : 32u;
+    uint2* const stage = reinterpret_cast<uint2*>(agnes_smem) + (threadIdx.x >> 6) * 192u; /* 1.5 KB per wave */
+    const uint64_t base = offs[i0], total = offs[i0 + m] - base;
+    /* lane k < m: instance i0 + k's first dense position (relative) and its segment */
+    const uint32_t rk = lane < m ? (uint32_t)(offs[i0 + lane] - base) : 0xFFFFFFFFu;
+    const uint64_t sk = lane < m ? (uint64_t)mult * vb.offsets[i0 + lane] : 0ull;
+    for (uint64_t p0 = 0; p0 < total; p0 += 64u) {
+        const uint32_t p = (uint32_t)p0 + lane;
+        uint32_t k = 0; /* the last instance starting at or before p */
+#pragma unroll
+        for (uint32_t step = 16u; step; step >>= 1) {
+            const uint32_t t = k + step;
+            const uint32_t o = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(t << 2), (int)rk);
+            k = o <= p ? t : k; /* lanes >= m hold 0xFFFFFFFF: never taken */
         }
+        const uint32_t rkk = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)rk);
+        const uint32_t slo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)(uint32_t)sk);
+        const uint32_t shi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)(uint32_t)(sk >> 32));
+        /* the step's 64 records staged in LDS as 24-B records, then out as three
+         * contiguous 512-B runs of 8-B words (the lanes' own 24-B records would be
+         * three stores strided by 24 B) */
+        const uint32_t nrec = total - p0 < 64u ? (uint32_t)(total - p0) : 64u;
+        if (lane < nrec) {
+            const uint4 r = seg[(((uint64_t)shi << 32) | slo) + (p - rkk)];
+            stage[3u * lane] = make_uint2(r.x, r.y);
+            stage[3u * lane + 1u] = make_uint2(i0 + k, r.z);
+            stage[3u * lane + 2u] = make_uint2(r.w, 0u);
+        }
+        __builtin_amdgcn_wave_barrier();
+        uint2* const q = reinterpret_cast<uint2*>(out + base + p0);
+#pragma unroll
+        for (uint32_t j = 0; j < 3u; ++j) {
+            const uint32_t x = 64u * j + lane;
+            if (x < 3u * nrec) q[x] = stage[x];
+        }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -1002,7 +1033,7 @@ hipError_t agnes_launch_seg_compact(const agnes_vote_batch* vb, uint32_t mult, c
     if (n == 0) return hipSuccess;
     const uint32_t waves = (n + 31u) / 32u, blocks = (waves + 3u) / 4u;
     AgnesKt kt("seg_compact", st);
-    hipLaunchKernelGGL(agnes::events::seg_compact, dim3(blocks), dim3(256), 0, st, *vb, mult,
+    hipLaunchKernelGGL(agnes::events::seg_compact, dim3(blocks), dim3(256), 4u * 192u * sizeof(uint2), st, *vb, mult,
                        reinterpret_cast<const uint4*>(seg), offs, out);
     return hipGetLastError();
 }
