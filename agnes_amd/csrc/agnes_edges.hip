@@ -141,15 +141,36 @@ __global__ __launch_bounds__(64) void edge_seg_walk(EdgeArgs a, const uint32_t* 
     counts[i] = walk_one<true, W, REG>(a, i, lane, a.vb.offsets[i]);
 }
 
-/* the dense summary from the segmented one: wave w copies instances 32w .. 32w + 31 */
+/* the dense summary from the segmented one: wave w writes the edges of instances
+ * 32w .. 32w + 31 -- one contiguous range, offs[32w] .. offs[32w + 32] -- 64 at a time,
+ * lane l the edge at position p: its instance by a 5-step binary search over the
+ * wave's offsets (one per lane, relative to the range's start), then one 16-B read of
+ * that instance's segment and one 16-B store (a few edges per instance: one instance
+ * per step left most lanes idle) */
 __global__ __launch_bounds__(256) void edge_compact(agnes_vote_batch vb, const agnes_edge* seg, const uint64_t* offs,
                                                     agnes_edge* out) {
     const uint32_t lane = threadIdx.x & 63u, w = blockIdx.x * 4u + (threadIdx.x >> 6);
-    const uint32_t n = vb.n_instances;
-    for (uint32_t i = 32u * w; i < n && i < 32u * w + 32u; ++i) {
-        const uint64_t o = offs[i], cnt = offs[i + 1u] - o;
-        const uint4* const src = reinterpret_cast<const uint4*>(seg + vb.offsets[i]);
-        for (uint64_t k = lane; k < cnt; k += 64u) reinterpret_cast<uint4*>(out + o)[k] = src[k];
+    const uint32_t n = vb.n_instances, i0 = 32u * w;
+    if (i0 >= n) return; /* wave-uniform */
+    const uint32_t m = n - i0 < 32u ? n - i0 : 32u;
+    const uint64_t base = offs[i0], total = offs[i0 + m] - base;
+    const uint32_t rk = lane < m ? (uint32_t)(offs[i0 + lane] - base) : 0xFFFFFFFFu;
+    const uint64_t sk = lane < m ? vb.offsets[i0 + lane] : 0ull;
+    const uint4* const src = reinterpret_cast<const uint4*>(seg);
+    uint4* const dst = reinterpret_cast<uint4*>(out + base);
+    for (uint64_t p0 = 0; p0 < total; p0 += 64u) {
+        const uint32_t p = (uint32_t)p0 + lane;
+        uint32_t k = 0; /* the last instance starting at or before p */
+#pragma unroll
+        for (uint32_t step = 16u; step; step >>= 1) {
+            const uint32_t t = k + step;
+            const uint32_t o = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(t << 2), (int)rk);
+            k = o <= p ? t : k; /* lanes >= m hold 0xFFFFFFFF: never taken */
+        }
+        const uint32_t rkk = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)rk);
+        const uint32_t slo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)(uint32_t)sk);
+        const uint32_t shi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)(uint32_t)(sk >> 32));
+        if ((uint64_t)p < total) dst[p] = src[(((uint64_t)shi << 32) | slo) + (p - rkk)];
     }
 }
 
