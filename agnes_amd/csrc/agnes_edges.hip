@@ -154,6 +154,14 @@ __global__ __launch_bounds__(256) void edge_compact(agnes_vote_batch vb, const a
     if (i0 >= n) return; /* wave-uniform */
     const uint32_t m = n - i0 < 32u ? n - i0 : 32u;
     const uint64_t base = offs[i0], total = offs[i0 + m] - base;
+    if (total > 0xFFFFFF00ull) { /* positions past u32 (4e9 edges in 32 instances): per instance */
+        for (uint32_t i = i0; i < i0 + m; ++i) {
+            const uint64_t o = offs[i], cnt = offs[i + 1u] - o;
+            const uint4* const s = reinterpret_cast<const uint4*>(seg + vb.offsets[i]);
+            for (uint64_t k = lane; k < cnt; k += 64u) reinterpret_cast<uint4*>(out + o)[k] = s[k];
+        }
+        return;
+    }
     const uint32_t rk = lane < m ? (uint32_t)(offs[i0 + lane] - base) : 0xFFFFFFFFu;
     const uint64_t sk = lane < m ? vb.offsets[i0 + lane] : 0ull;
     const uint4* const src = reinterpret_cast<const uint4*>(seg);

@@ -251,6 +251,20 @@ __global__ __launch_bounds__(256) void seg_compact(agnes_vote_batch vb, uint32_t
     const uint32_t m = n - i0 < 32u ? n - i0 : 32u;
     uint2* const stage = reinterpret_cast<uint2*>(agnes_smem) + (threadIdx.x >> 6) * 192u; /* 1.5 KB per wave */
     const uint64_t base = offs[i0], total = offs[i0 + m] - base;
+    if (total > 0xFFFFFF00ull) { /* positions past u32 (4e9 records in 32 instances): per instance */
+        for (uint32_t i = i0; i < i0 + m; ++i) {
+            const uint64_t o = offs[i], cnt = offs[i + 1u] - o;
+            const uint4* const src = seg + (uint64_t)mult * vb.offsets[i];
+            for (uint64_t k = lane; k < cnt; k += 64u) {
+                const uint4 r = src[k];
+                uint2* const q = reinterpret_cast<uint2*>(out + o + k);
+                q[0] = make_uint2(r.x, r.y);
+                q[1] = make_uint2(i, r.z);
+                q[2] = make_uint2(r.w, 0u);
+            }
+        }
+        return;
+    }
     /* lane k < m: instance i0 + k's first dense position (relative) and its segment */
     const uint32_t rk = lane < m ? (uint32_t)(offs[i0 + lane] - base) : 0xFFFFFFFFu;
     const uint64_t sk = lane < m ? (uint64_t)mult * vb.offsets[i0 + lane] : 0ull;
