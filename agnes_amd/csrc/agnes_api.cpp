@@ -307,7 +307,7 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
                       uint8_t* codes, const agnes_state* states_in, agnes_state* states,
                       agnes_carry_rec* carry, const agnes_set_info* sets, uint32_t n_sets, uint32_t sets_dom,
                       hipStream_t st, uint64_t* ev_counts = nullptr, bool* counted = nullptr,
-                      void* rec_out = nullptr, bool edges = false) {
+                      void* rec_out = nullptr, bool edges = false, bool* fast_counted = nullptr) {
     if (!c || !cfg_ok(cfg) || !b || !b->offsets) return AGNES_E_INVALID;
     if (b->n_votes && (!codes || !b->instance || !b->round || !b->type || !b->value ||
                        !b->validator))
@@ -402,6 +402,14 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
         }
         if (flow && edges) a.edges = 1u;
         if (counted) *counted = flow;
+        /* the per-instance route (DEDUP, RoundSkip, or forced) counts them in tally_fast:
+         * every instance it runs; the ones it defers to the i64 LIST kernel are the
+         * caller's to count (agnes_tally_events: a list pass) */
+        const bool fast = !flow && !wide_all && !rec_out && route != AGNES_ROUTE_WIDE &&
+                          (cfg->mode == AGNES_MODE_DEDUP || (cfg->flags & AGNES_FLAG_ROUND_SKIP) ||
+                           route == AGNES_ROUTE_INSTANCE || route == AGNES_ROUTE_SPLIT);
+        if (fast) a.ev_counts = ev_counts;
+        if (fast_counted) *fast_counted = fast;
     }
     return status_of(agnes_launch_tally(&a, cfg->mode, c->num_cus, wide_all, st));
 }
@@ -681,9 +689,9 @@ int agnes_tally_events(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_b
     if (b->n_votes && (!b->value || ((uintptr_t)b->value & 3u))) return AGNES_E_INVALID;
     if (cfg_ok(cfg) && cfg->max_rounds > 64u) return AGNES_E_UNSUPPORTED; /* the emit's value slots in LDS */
     const hipStream_t st = (hipStream_t)stream;
-    bool counted = false;
+    bool counted = false, fast_counted = false;
     const int rc = tally_impl(c, cfg, b, codes, states_in, states_out, nullptr, c->d_sets, c->n_sets, c->sets_dom, st,
-                              offsets + 1, &counted);
+                              offsets + 1, &counted, nullptr, false, &fast_counted);
     if (rc != AGNES_OK) return rc;
     const uint64_t words = agnes_edges_scratch_words(b->n_instances);
     if (words > c->scan_cap) {
@@ -694,12 +702,16 @@ int agnes_tally_events(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_b
         AGNES_TRY(hipMalloc(&c->d_scan, words * sizeof(uint64_t)));
         c->scan_cap = words;
     }
-    if (counted) {
-        /* the flow kernel counted its batches' records; the walk list's instances here */
+    if (counted || fast_counted) {
+        /* the tally counted its instances' records; the flow kernel's walk list, or the
+         * instances tally_fast deferred to the LIST kernel, here */
         AGNES_TRY(hipMemsetAsync(offsets, 0, sizeof(uint64_t), st));
-        AGNES_TRY(agnes_launch_event_count_list(b, codes, c->d_list + (size_t)c->list_cap,
-                                                reinterpret_cast<const uint32_t*>(c->d_err + AGNES_ERR_BYTES / 8) + AGNES_WALK_COUNT,
-                                                offsets, c->num_cus, st));
+        const uint32_t* const lc = reinterpret_cast<const uint32_t*>(c->d_err + AGNES_ERR_BYTES / 8);
+        if (counted)
+            AGNES_TRY(agnes_launch_event_count_list(b, codes, c->d_list + (size_t)c->list_cap, lc + AGNES_WALK_COUNT,
+                                                    offsets, c->num_cus, st));
+        else
+            AGNES_TRY(agnes_launch_event_count_list(b, codes, c->d_list, lc, offsets, c->num_cus, st));
         AgnesKt kt("event_scan", st);
         AGNES_TRY(agnes_launch_offsets_scan(offsets, b->n_instances, c->d_scan, st));
     } else {

@@ -282,6 +282,7 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
             }
         }
         if (len == 0) run = false;
+        uint32_t evn = 0; /* (a.ev_counts: agnes_tally_events) the lane's records of this instance */
         if (run) {
         if (TABLES) {
             if (++ep > emax) { /* epoch space used up: recycle the tables */
@@ -668,6 +669,12 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
             dc_code = code[0] | (code[1] << 8) | (code[2] << 16) | (code[3] << 24);
             dc_pos = x.pos;
             dc_at = c;
+            if (a.ev_counts) { /* records: an event 1..5, plus its RoundSkip bit; none for INVALID / REJECTED */
+                const uint32_t e = dc_code & 0x07070707u;
+                const uint32_t ok = ~(e + 0x7A7A7A7Au) & ((dc_pos * 0x00204081u) & 0x01010101u) << 7;
+                evn += (uint32_t)__builtin_popcount((e + 0x7F7F7F7Fu) & ok) +
+                       (uint32_t)__builtin_popcount((dc_code << 4) & ok);
+            }
             __builtin_amdgcn_wave_barrier();
         }
         if (SM && sm_changed) { /* State back (deferred) */
@@ -675,6 +682,10 @@ __global__ __launch_bounds__(256) void tally_fast(agnes_tally_args a, uint32_t l
             ds_word = stv;
         }
         } /* run */
+        if (a.ev_counts) { /* the instance's record count (a deferred one's is the count pass's) */
+            const uint32_t tot = rdl(scan(evn), 63u);
+            if (lane == 0) a.ev_counts[I.i] = tot;
+        }
         issue_hnn();
         /* advance the stream */
         if (q + 1u < qe) {
