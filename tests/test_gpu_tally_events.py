@@ -146,6 +146,21 @@ def test_tally_events_dedup_skip(eng):
     assert (ev["kind"] == abi.EV_ROUND_SKIP).any()
 
 
+@pytest.mark.parametrize("route", [abi.ROUTE_INSTANCE, abi.ROUTE_SPLIT, abi.ROUTE_WIDE])
+def test_tally_events_forced_routes(eng, route):
+    """the record counts by route: tally_fast counts them itself on the per-instance
+    routes (INSTANCE / SPLIT, here with REFERENCE and with DEDUP + RoundSkip), the
+    wide kernel's route takes the count pass; same records"""
+    p = abi.gen_params(seed=65, n_instances=1200, n_vals=80, rounds_min=1, rounds_max=3, nil_permille=300,
+                       dup_permille=80, equiv_permille=80, higher_permille=40)
+    hb = ol.gen_batch(p)
+    power = ol.gen_power(65, 1, 80, abi.POWER_UNIFORM, 1, 5000)
+    for mode, flags in [(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE),
+                        (abi.MODE_DEDUP, abi.FLAG_STATE_MACHINE | abi.FLAG_ROUND_SKIP)]:
+        _check(eng, abi.config(mode, flags | abi.FLAG_ROUTE(route), 4), hb, power,
+               abi.new_states(1200, 1, abi.STEP_PREVOTE))
+
+
 def _ragged(seed, n_inst, max_len, n_vals, rounds, zero_every=7, bad=0.02):
     rng = np.random.default_rng(seed)
     lens = rng.integers(0, max_len, n_inst)
