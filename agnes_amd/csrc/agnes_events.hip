@@ -198,7 +198,7 @@ __device__ __forceinline__ void put_seg(uint4* o, uint64_t j, uint32_t value, ui
     *o = make_uint4((uint32_t)j, (uint32_t)(j >> 32), value, round | (kind << 8) | (msg << 16));
 }
 
-template <bool LIST>
+template <bool LIST, uint32_t W, bool A16>
 __global__ __launch_bounds__(64) void seg_walk(EvArgs a, const uint32_t* list, const uint32_t* list_n, uint32_t mult,
                                                uint4* seg, uint64_t* counts) {
     uint32_t* const lab = reinterpret_cast<uint32_t*>(agnes_smem);
@@ -219,19 +219,29 @@ __global__ __launch_bounds__(64) void seg_walk(EvArgs a, const uint32_t* list, c
     hi = hi < NV ? hi : NV;
     uint4* const out = seg + (uint64_t)mult * a.vb.offsets[i];
     uint64_t cnt = 0;
-    for (uint64_t j = lo; j < hi; ++j) {
-        const uint32_t cb = a.codes[j], ev = cb & AGNES_CODE_EVENT_MASK;
-        if (ev == AGNES_CODE_INVALID || ev == AGNES_CODE_REJECTED) continue; /* not added by the tally */
-        const uint32_t rb = a.vb.round[j], tb = a.vb.type[j], key = rb * 2u + tb;
-        if (tb > 1u || key >= a.keys) continue; /* (never for a code the tally wrote) */
-        uint32_t* const p = lab + key * 64u + lane;
-        const uint32_t v = a.vb.value[j];
-        if (v != AGNES_NIL) *p = v; /* the value slot, last writer wins (round_votes.rs:50-54) */
-        const uint32_t msg = cb >> AGNES_CODE_MSG_SHIFT;
-        if ((cb >> 3) & 1u) put_seg(out + cnt++, j, AGNES_NIL, rb, AGNES_EV_ROUND_SKIP, msg);
-        if (ev != AGNES_CODE_NONE) {
-            const bool val = ev == AGNES_CODE_POLKA_VALUE || ev == AGNES_CODE_PRECOMMIT_VALUE;
-            put_seg(out + cnt++, j, val ? *p : AGNES_NIL, rb, kind_of(ev), msg);
+    /* W-vote windows of every column (event_walk's order and rules) */
+    for (uint64_t w = lo & ~(uint64_t)(W - 1u); w < hi; w += W) {
+        uint32_t c[W / 4u], r[W / 4u], t[W / 4u], v[W];
+        load_bytes<W>(a.codes, w, NV, c);
+        load_bytes<W>(a.vb.round, w, NV, r);
+        load_bytes<W>(a.vb.type, w, NV, t);
+        load_words<W, A16>(a.vb.value, w, NV, v);
+#pragma unroll
+        for (uint32_t b = 0; b < W; ++b) {
+            const uint64_t j = w + b;
+            const uint32_t sh8 = 8u * (b & 3u);
+            const uint32_t cb = (c[b >> 2] >> sh8) & 0xFFu, ev = cb & AGNES_CODE_EVENT_MASK;
+            if (j < lo || j >= hi || ev == AGNES_CODE_INVALID || ev == AGNES_CODE_REJECTED) continue; /* not added */
+            const uint32_t rb = (r[b >> 2] >> sh8) & 0xFFu, tb = (t[b >> 2] >> sh8) & 0xFFu, key = rb * 2u + tb;
+            if (tb > 1u || key >= a.keys) continue; /* (never for a code the tally wrote) */
+            uint32_t* const p = lab + key * 64u + lane;
+            if (v[b] != AGNES_NIL) *p = v[b]; /* the value slot, last writer wins (round_votes.rs:50-54) */
+            const uint32_t msg = cb >> AGNES_CODE_MSG_SHIFT;
+            if ((cb >> 3) & 1u) put_seg(out + cnt++, j, AGNES_NIL, rb, AGNES_EV_ROUND_SKIP, msg);
+            if (ev != AGNES_CODE_NONE) {
+                const bool val = ev == AGNES_CODE_POLKA_VALUE || ev == AGNES_CODE_PRECOMMIT_VALUE;
+                put_seg(out + cnt++, j, val ? *p : AGNES_NIL, rb, kind_of(ev), msg);
+            }
         }
     }
     counts[i] = cnt;
@@ -1031,13 +1041,21 @@ hipError_t agnes_launch_seg_walk(const agnes_vote_batch* vb, const uint8_t* code
     if (n == 0) return hipSuccess;
     EvArgs a{*vb, codes, nullptr, nullptr, 2u * max_rounds};
     const size_t lds = (size_t)a.keys * 64u * sizeof(uint32_t);
+    /* 16-vote windows when the u8 columns are 16-B aligned, else 4-vote ones; the value
+     * column is 16-B aligned (agnes_tally_records' requirement) */
+    const bool w16 = ((reinterpret_cast<uintptr_t>(codes) | reinterpret_cast<uintptr_t>(vb->round) |
+                       reinterpret_cast<uintptr_t>(vb->type)) & 15u) == 0u;
+    const bool a16 = (reinterpret_cast<uintptr_t>(vb->value) & 15u) == 0u;
+    const dim3 grid((n + 63u) / 64u), blk(64);
+    uint4* const sg = reinterpret_cast<uint4*>(seg);
     AgnesKt kt("seg_walk", st);
-    if (list)
-        hipLaunchKernelGGL((seg_walk<true>), dim3((n + 63u) / 64u), dim3(64), lds, st, a, list, list_n, mult,
-                           reinterpret_cast<uint4*>(seg), counts);
-    else
-        hipLaunchKernelGGL((seg_walk<false>), dim3((n + 63u) / 64u), dim3(64), lds, st, a, list, list_n, mult,
-                           reinterpret_cast<uint4*>(seg), counts);
+#define AGNES_SEG_WALK(L, W_, A_) hipLaunchKernelGGL((seg_walk<L, W_, A_>), grid, blk, lds, st, a, list, list_n, mult, sg, counts)
+    if (list) {
+        if (w16 && a16) AGNES_SEG_WALK(true, 16u, true); else if (a16) AGNES_SEG_WALK(true, 4u, true); else AGNES_SEG_WALK(true, 4u, false);
+    } else {
+        if (w16 && a16) AGNES_SEG_WALK(false, 16u, true); else if (a16) AGNES_SEG_WALK(false, 4u, true); else AGNES_SEG_WALK(false, 4u, false);
+    }
+#undef AGNES_SEG_WALK
     return hipGetLastError();
 }
 
