@@ -8,7 +8,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 NIL = 0xFFFFFFFF
 
 OK, E_INVALID, E_UNSUPPORTED, E_DEVICE, E_NOMEM, E_NODEVICE = 0, -1, -2, -3, -4, -5
@@ -40,6 +40,7 @@ TYPE_MASKED = 0xFE  # agnes_dedup_mask's type byte of a later duplicate (AGNES_T
 FLAG_MASKED_REJECTED = 0x20  # agnes_tally_carried: AGNES_TYPE_MASKED votes -> REJECTED in the pass (agnes_dedup_reject inside)
 # route override (agnes.h AGNES_ROUTE_*): diagnostics / route-equivalence tests
 ROUTE_SHIFT, ROUTE_AUTO, ROUTE_INSTANCE, ROUTE_SPLIT, ROUTE_WIDE = 8, 0, 1, 2, 3
+FLAG_RECORDS_FUSED = 0x400  # agnes_tally_records: the flow kernel writes the records at any batch size
 EPOCH_BITS_SHIFT = 16
 
 
@@ -111,7 +112,8 @@ class GenParams(C.Structure):
                 ("rounds_min", C.c_uint32), ("rounds_max", C.c_uint32),
                 ("nil_permille", C.c_uint32), ("dup_permille", C.c_uint32),
                 ("equiv_permille", C.c_uint32), ("higher_permille", C.c_uint32),
-                ("order", C.c_uint32), ("instance_base", C.c_uint32)]
+                ("order", C.c_uint32), ("instance_base", C.c_uint32),
+                ("absent_permille", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 assert C.sizeof(Vote) == 16
@@ -120,7 +122,7 @@ assert C.sizeof(Message) == 24
 assert C.sizeof(StateRec) == 64
 assert C.sizeof(Config) == 16
 assert C.sizeof(VoteBatch) == 80
-assert C.sizeof(GenParams) == 48
+assert C.sizeof(GenParams) == 56
 
 # numpy views of the same records (for device<->host copies of state arrays)
 STATE_DTYPE = np.dtype([
@@ -159,9 +161,10 @@ assert VOTE_COUNT_DTYPE.itemsize == 24
 
 def gen_params(seed=0xA6E5, n_instances=1, n_vals=4, rounds_min=1, rounds_max=1, nil_permille=0,
                dup_permille=0, equiv_permille=0, higher_permille=0, order=ORDER_SHUFFLED,
-               instance_base=0) -> GenParams:
+               instance_base=0, absent_permille=0) -> GenParams:
     return GenParams(seed, n_instances, n_vals, rounds_min, rounds_max, nil_permille,
-                     dup_permille, equiv_permille, higher_permille, order, instance_base)
+                     dup_permille, equiv_permille, higher_permille, order, instance_base,
+                     absent_permille, 0)
 
 
 def config(mode=MODE_REFERENCE, flags=0, max_rounds=1, reserved=0) -> Config:

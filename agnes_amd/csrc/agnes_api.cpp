@@ -122,7 +122,7 @@ bool cfg_ok(const agnes_config* cfg) {
     return cfg && cfg->max_rounds >= 1 && cfg->max_rounds <= 256 && cfg->mode <= AGNES_MODE_DEDUP &&
            (cfg->flags & ~(AGNES_FLAG_ROUND_SKIP | AGNES_FLAG_STATE_MACHINE | AGNES_FLAG_DISTINCT_VALUES |
                            AGNES_FLAG_ONE_INSTANCE | AGNES_FLAG_WEIGHTS_CACHED | AGNES_FLAG_MASKED_REJECTED |
-                           (AGNES_ROUTE_MASK << AGNES_ROUTE_SHIFT) |
+                           (AGNES_ROUTE_MASK << AGNES_ROUTE_SHIFT) | AGNES_FLAG_RECORDS_FUSED |
                            AGNES_FLAG_EPOCH_BITS(0x1F))) == 0;
 }
 
@@ -297,12 +297,6 @@ int64_t agnes_lds_bytes_per_wave(const agnes_config* cfg, uint32_t n_vals) {
 #ifndef AGNES_REC_FUSED_MIN_VOTES
 #define AGNES_REC_FUSED_MIN_VOTES (1ull << 28) /* several rounds: smaller batches take the emit pass */
 #endif
-/* the environment variable of the same name overrides it (the tests run both routes) */
-static uint64_t rec_fused_min_votes() {
-    const char* e = std::getenv("AGNES_REC_FUSED_MIN_VOTES");
-    return e && *e ? std::strtoull(e, nullptr, 0) : (uint64_t)AGNES_REC_FUSED_MIN_VOTES;
-}
-
 static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b,
                       uint8_t* codes, const agnes_state* states_in, agnes_state* states,
                       agnes_carry_rec* carry, const agnes_set_info* sets, uint32_t n_sets, uint32_t sets_dom,
@@ -395,7 +389,8 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
          * which pays on a large batch but not on a small one, where the tally's tail
          * grows with it: C3 (7.5e8 votes) 4.83 ms fused vs 5.19 through the emit pass,
          * its 8-GPU shard (9.4e7) 0.95 vs 0.80 */
-        if (rec_out && !edges && cfg->max_rounds > 1u && b->n_votes < rec_fused_min_votes()) {
+        if (rec_out && !edges && cfg->max_rounds > 1u && b->n_votes < AGNES_REC_FUSED_MIN_VOTES &&
+            !(cfg->flags & AGNES_FLAG_RECORDS_FUSED)) {
             a.ev_counts = nullptr;
             a.rec_out = nullptr;
             flow = false;

@@ -548,6 +548,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
             if (lane == 0) w0 = atomicAdd(a.list_count + AGNES_WALK_COUNT, m);
             w0 = rdl(w0, 0u);
             if (lane < m) a.walk[w0 + lane] = H.s0 + lane;
+            /* the walk kernel works in place on a.states: bring the batch's input States over */
+            if (SM && a.states_in && a.states_in != a.states)
+                for (uint32_t j = lane; j < 4u * m; j += 64u)
+                    reinterpret_cast<uint4*>(a.states + H.s0)[j] = reinterpret_cast<const uint4*>(a.states_in + H.s0)[j];
         } else {
             /* the instance records' constants (written at the first chunk's top, once the
              * batch before has been finalized from its records) */

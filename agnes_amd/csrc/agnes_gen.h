@@ -16,6 +16,10 @@
  *     [.., +H)       early votes tagged round r+1                     (C4: RoundSkip)
  *   positions inside the round permuted by a keyed Feistel bijection (order SHUFFLED),
  *   or prevotes-then-precommits (PHASED), or identity (SORTED).
+ *   Abstention (absent_permille > 0): round r of instance gi keeps only its first M_r =
+ *   M - A_r positions, A_r ~ U[0, 2 M absent / 1000] hashed from (gi, r) -- with the
+ *   SHUFFLED order a uniformly random subset of its votes is absent -- so instance
+ *   lengths (and the offsets of a batch) take any value, not multiples of the round.
  * Not part of the tally hot path.
  */
 #ifndef AGNES_GEN_H
@@ -119,12 +123,30 @@ AGNES_HD static inline agnes_gen_vote agnes_gen_base(uint64_t seed, uint32_t gi,
     return v;
 }
 
+/* votes of round r of instance gi: M less its absent ones (see the header) */
+AGNES_HD static inline uint32_t agnes_gen_round_votes(uint64_t seed, uint32_t gi, uint32_t r, agnes_gen_shape s,
+                                                      uint32_t absent_pm) {
+    if (!absent_pm) return s.M;
+    const uint64_t span = ((uint64_t)s.M * absent_pm * 2u) / 1000u;
+    const uint64_t A = agnes_hash4(seed, 0x414253454E54ull, gi, r) % (span + 1u);
+    return A < s.M ? s.M - (uint32_t)A : 0u;
+}
+
 /* vote at position t (0-based) of instance gi */
 AGNES_HD static inline agnes_gen_vote agnes_gen_vote_at(uint64_t seed, uint32_t gi, uint64_t t,
                                                         agnes_gen_shape s, uint32_t nil_pm,
-                                                        uint32_t order) {
-    const uint32_t r = (uint32_t)(t / s.M);
-    const uint32_t pos = (uint32_t)(t % s.M);
+                                                        uint32_t order, uint32_t absent_pm) {
+    uint32_t r, pos;
+    if (!absent_pm) {
+        r = (uint32_t)(t / s.M);
+        pos = (uint32_t)(t % s.M);
+    } else { /* the round holding position t (the instance's rounds are few) */
+        r = 0;
+        for (uint32_t mr = agnes_gen_round_votes(seed, gi, 0u, s, absent_pm); t >= mr;
+             mr = agnes_gen_round_votes(seed, gi, ++r, s, absent_pm))
+            t -= mr;
+        pos = (uint32_t)t;
+    }
     const uint64_t key = agnes_hash4(seed, 0x5045524Dull, gi, r);
     uint32_t q;
     if (order == 2u) {

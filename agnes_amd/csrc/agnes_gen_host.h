@@ -14,7 +14,7 @@
 
 static inline int agnes_gen_params_ok(const agnes_gen_params* p) {
     if (!p || p->n_vals == 0 || p->rounds_min > p->rounds_max || p->rounds_max > 255u) return 0;
-    if (p->nil_permille > 1000u) return 0;
+    if (p->nil_permille > 1000u || p->absent_permille > 500u) return 0;
     if (p->higher_permille && p->rounds_max + 1u > 255u) return 0;
     if ((uint64_t)p->n_vals * 2u > 0x40000000ull) return 0;
     return 1;
@@ -26,8 +26,12 @@ static inline agnes_gen_shape agnes_gen_shape_p(const agnes_gen_params* p) {
 
 static inline uint64_t agnes_gen_host_instance_votes(const agnes_gen_params* p, uint32_t i) {
     agnes_gen_shape s = agnes_gen_shape_p(p);
-    uint32_t R = agnes_gen_rounds(p->seed, p->instance_base + i, p->rounds_min, p->rounds_max);
-    return (uint64_t)R * s.M;
+    const uint32_t gi = p->instance_base + i;
+    const uint32_t R = agnes_gen_rounds(p->seed, gi, p->rounds_min, p->rounds_max);
+    if (!p->absent_permille) return (uint64_t)R * s.M;
+    uint64_t n = 0;
+    for (uint32_t r = 0; r < R; ++r) n += agnes_gen_round_votes(p->seed, gi, r, s, p->absent_permille);
+    return n;
 }
 
 static inline int agnes_gen_host_offsets(const agnes_gen_params* p, uint64_t* offsets) {
@@ -50,7 +54,7 @@ static inline int agnes_gen_host_votes(const agnes_gen_params* p, const uint64_t
         const uint32_t gi = p->instance_base + i;
         for (uint64_t j = offsets[i]; j < offsets[i + 1]; ++j) {
             agnes_gen_vote v =
-                agnes_gen_vote_at(p->seed, gi, j - offsets[i], s, p->nil_permille, p->order);
+                agnes_gen_vote_at(p->seed, gi, j - offsets[i], s, p->nil_permille, p->order, p->absent_permille);
             instance[j] = i;
             round[j] = (uint8_t)v.round;
             type[j] = (uint8_t)v.type;

@@ -1188,7 +1188,8 @@ __global__ __launch_bounds__(256) void gen_kernel(agnes_gen_params p, agnes_gen_
             else hi = mid;
         }
         const agnes_gen_vote v =
-            agnes_gen_vote_at(p.seed, p.instance_base + lo, j - off[lo], sh, p.nil_permille, p.order);
+            agnes_gen_vote_at(p.seed, p.instance_base + lo, j - off[lo], sh, p.nil_permille, p.order,
+                              p.absent_permille);
         instance[j] = lo;
         round[j] = (uint8_t)v.round;
         type[j] = (uint8_t)v.type;

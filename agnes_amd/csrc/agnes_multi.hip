@@ -314,7 +314,7 @@ int check_collective(agnes_multi* m, uint32_t d, XOp op, int64_t* recv, uint64_t
     const uint64_t n = op == X_GATHER ? (uint64_t)D * count : count;
     std::vector<uint64_t> want((size_t)n), got((size_t)n);
     int rc = AGNES_OK;
-    if (m->test_corrupt & (1u << op)) { /* test hook: one received element flipped */
+    if (m->test_corrupt & (0x11u << op)) { /* test hook: one received element flipped */
         if (hipMemsetAsync(recv, 0x5A, 1, dv.st) != hipSuccess) rc = AGNES_E_DEVICE;
     }
     if (rc == AGNES_OK && hipMemcpyAsync(got.data(), recv, 8u * n, hipMemcpyDeviceToHost, dv.st) != hipSuccess)
@@ -339,7 +339,9 @@ int check_collective(agnes_multi* m, uint32_t d, XOp op, int64_t* recv, uint64_t
 int exchange(agnes_multi* m, uint32_t d, XOp op, const int64_t* send, int64_t* recv, uint64_t count, int mine) {
     Dev& dv = m->dev[d];
     const uint32_t D = (uint32_t)m->dev.size();
-    if (!m->comms.empty()) {
+    /* once a self-check has failed (rccl_bad, published between two barriers, so every
+     * thread sees the same value) the call's later collectives take the host exchange too */
+    if (!m->comms.empty() && !m->rccl_bad) {
         const bool check = !(m->rccl_checked & (1u << op));
         if (check && mine == AGNES_OK) mine = stage_send(m, d, send, count);
         if (!agree_ok(m, d, mine)) return mine != AGNES_OK ? mine : AGNES_E_DEVICE;
@@ -360,6 +362,10 @@ int exchange(agnes_multi* m, uint32_t d, XOp op, const int64_t* send, int64_t* r
         }
         m->used_rccl = true;
         if (check) return check_collective(m, d, op, recv, count);
+        if (m->test_corrupt & (0x10u << op)) { /* test hook: an RCCL that is really broken */
+            if (hipMemsetAsync(recv, 0x5A, 1, dv.st) != hipSuccess || hipStreamSynchronize(dv.st) != hipSuccess)
+                return AGNES_E_DEVICE;
+        }
         return AGNES_OK;
     }
     const uint64_t bytes = 8u * count;
@@ -739,9 +745,9 @@ int agnes_multi_exchange(agnes_multi* m, uint32_t mode) {
 }
 
 int agnes_multi_test_corrupt(agnes_multi* m, uint32_t ops) {
-    if (!m || ops > 15u) return AGNES_E_INVALID;
+    if (!m || ops > 255u) return AGNES_E_INVALID;
     m->test_corrupt = ops;
-    m->rccl_checked = 0u; /* the next collective of each kind is checked again */
+    m->rccl_checked &= ~(ops & 15u); /* the next collective of each kind in bits 0..3 is checked again */
     return AGNES_OK;
 }
 

@@ -67,8 +67,9 @@ class MultiEngine:
         check(self.lib.agnes_multi_exchange(self.h, mode), "agnes_multi_exchange")
 
     def test_corrupt(self, ops: int):
-        """Test hook: bit k flips the first received byte of the next checked RCCL
-        collective of kind k (0 MIN u64, 1 MIN i64, 2 MAX i64, 3 all-gather), so the
+        """Test hook: bit k re-arms the self-check of kind k (0 MIN u64, 1 MIN i64, 2 MAX
+        i64, 3 all-gather) and flips the first received byte of its next RCCL collective;
+        bit 4 + k flips it in every RCCL collective of kind k (a broken RCCL), so the
         self-check's fallback (stats['exchange'] & abi.MULTI_X_FALLBACK) can be tested."""
         check(self.lib.agnes_multi_test_corrupt(self.h, ops), "agnes_multi_test_corrupt")
 

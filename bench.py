@@ -92,6 +92,21 @@ WORKLOADS = {
                              nil_permille=300),
                     power=(abi.POWER_UNIFORM, 1, 1000, 1024), mode=abi.MODE_REFERENCE,
                     flags=abi.FLAG_STATE_MACHINE, max_rounds=4, scaling="weak"),
+    # round 6: the same shapes with 5 % abstention -- each round drops a random subset of
+    # its votes (absent validators), so instance lengths and offsets take any value: the
+    # ragged streams a real validator set produces (no 4-aligned instance starts)
+    "c2r": dict(desc="C2x100 with 5% abstention: 1M instances x 100 weighted validators x 1 round, "
+                     "ragged lengths (absent validators), 80/20 value/nil, shuffled",
+                gen=dict(n_instances=10_000 * 100, n_vals=100, rounds_min=1, rounds_max=1,
+                         nil_permille=200, absent_permille=50),
+                power=(abi.POWER_UNIFORM, 1, 1000, 1), mode=abi.MODE_REFERENCE,
+                flags=abi.FLAG_STATE_MACHINE, max_rounds=1, scaling="weak"),
+    "c3r": dict(desc="C3 8-GPU shard with 5% abstention: 125k instances x 150 validators x 1..4 rounds, "
+                     "30% nil, 1024 power sets, ragged lengths (absent validators)",
+                gen=dict(n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4,
+                         nil_permille=300, absent_permille=50),
+                power=(abi.POWER_UNIFORM, 1, 1000, 1024), mode=abi.MODE_REFERENCE,
+                flags=abi.FLAG_STATE_MACHINE, max_rounds=4, scaling="weak"),
     # the C2 shape with i64 stakes: powers U[2^28, 2^34], set totals ~8.6e11 > 2^32 (the
     # reference's i64 arithmetic, round_votes.rs:9,16-18,31-33), through the route the
     # engine picks for a set outside the u32 domain

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define AGNES_ABI_VERSION 7u
+#define AGNES_ABI_VERSION 8u
 
 /* ---------------------------------------------------------------------------
  * Status codes (reference never fails, state_machine.rs:212; these report
@@ -214,6 +214,11 @@ typedef struct agnes_state {
 #define AGNES_ROUTE_SPLIT 2u
 #define AGNES_ROUTE_WIDE 3u
 #define AGNES_FLAG_ROUTE(r) ((uint32_t)(r) << AGNES_ROUTE_SHIFT)
+/* agnes_tally_records with several rounds: the flow kernel writes the records whatever
+ * the batch's size (without it, batches under 2^28 votes take the emit pass: the fused
+ * variant's 2 waves per SIMD only pay on large batches).  Identical records either way;
+ * the route-equivalence tests set it. */
+#define AGNES_FLAG_RECORDS_FUSED 0x400u
 /* Bits 16..20 of agnes_config.flags: minimum bits the DEDUP / RoundSkip first-vote
  * tables spend on a vote's index inside its instance (0 = just enough for the
  * batch).  More index bits leave fewer epochs per table fill, so the tables are
@@ -616,9 +621,11 @@ int agnes_multi_exchange(agnes_multi* m, uint32_t mode);
 #define AGNES_MULTI_X_RCCL 1u
 #define AGNES_MULTI_X_FALLBACK 2u
 #define AGNES_MULTI_X_HOST 4u
-/* Test hook (not for production): bit k of ops flips the first received byte of the
- * next checked RCCL collective of kind k (0 MIN u64, 1 MIN i64, 2 MAX i64, 3 all-gather)
- * before the self-check, so tests can drive the fallback path. */
+/* Test hook (not for production): bit k of ops re-arms the self-check of kind k (0 MIN
+ * u64, 1 MIN i64, 2 MAX i64, 3 all-gather) and flips the first received byte of its next
+ * RCCL collective before the check; bit 4 + k flips it in EVERY RCCL collective of kind
+ * k, checked or not (an RCCL that is really broken: once a check fails, the call's later
+ * collectives must take the host exchange), so tests can drive the fallback path. */
 int agnes_multi_test_corrupt(agnes_multi* m, uint32_t ops);
 
 /* ---------------------------------------------------------------------------
@@ -726,7 +733,7 @@ uint64_t agnes_events_capacity(const agnes_config* cfg, const agnes_vote_batch* 
 /* The same records SEGMENTED by instance (round 5): no scan between the tally and the
  * records, so on the flow route (REFERENCE without RoundSkip, max_rounds <= 15, every
  * offset a multiple of 4 -- the C2 / C3 streams; with several rounds, batches of at
- * least 2^28 votes, or the AGNES_REC_FUSED_MIN_VOTES environment variable's count) the
+ * least 2^28 votes, or with AGNES_FLAG_RECORDS_FUSED) the
  * tally kernel writes them itself while the votes are in registers: the records cost no
  * second pass over the votes.
  * Instance i's records are out[seg(i) + k], k < counts[i], in vote order, with
@@ -775,13 +782,16 @@ typedef struct agnes_gen_params {
     uint32_t higher_permille; /* extra votes tagged round+1 per round            */
     uint32_t order;           /* AGNES_ORDER_*                                   */
     uint32_t instance_base;   /* global id of local instance 0 (sharding)        */
+    uint32_t absent_permille; /* abstention (<= 500): round r keeps M - A_r votes, A_r ~
+                                 U[0, 2 M absent / 1000] -- instance lengths take any value */
+    uint32_t reserved;
 } agnes_gen_params;
 
 #define AGNES_ORDER_SHUFFLED 0u /* random permutation of each round's votes       */
 #define AGNES_ORDER_PHASED 1u   /* each round: shuffled prevotes, then precommits */
 #define AGNES_ORDER_SORTED 2u   /* each round: prevotes by validator, then precommits */
 
-/* votes per instance (all instances of one params share the per-round count) */
+/* votes per instance (without abstention every round of one params has the same count) */
 uint64_t agnes_gen_instance_votes(const agnes_gen_params* p, uint32_t local_instance);
 /* host: offsets[n_instances+1] */
 int agnes_gen_offsets(const agnes_gen_params* p, uint64_t* offsets);

@@ -7,6 +7,7 @@ between host and device.
   C2  1M instances x 100 validators x 1 round (the bench's c2 batch), State machine
   C2w the same with i64 stakes U[2^28, 2^34] (the bench's c2w batch, u64 sums)
   C3  a 125k-instance shard of 1M x 150 validators x 1..4 rounds, 1024 power sets
+  C3r the C3 shard with 5 % abstention (ragged instance lengths, round 6); C2r likewise
   C3w the same with i64 stakes U[2^28, 2^34] (the bench's c3w batch, flow<W64> runs mode)
   C4  125k instances, Zipf power, 10 % duplicates + 10 % equivocations + 5 %
       next-round votes, DEDUP + RoundSkip + State machine
@@ -90,6 +91,26 @@ def test_full_c3_shard(eng):
     power = ol.gen_power(0xA6E5, 1024, 150, abi.POWER_UNIFORM, 1, 1000)
     _, st = _compare(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 4), p, power, 1024)
     assert st["decided"].sum() > 0
+
+
+def test_full_c3r_shard(eng):
+    """The bench's c3r batch (round 6): the C3 shard with 5 % abstention -- every round
+    drops a random subset of its votes, so instance lengths and offsets take any value
+    (no 4-aligned stream), as a real validator set with absent validators produces."""
+    p = abi.gen_params(seed=0xA6E5, n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4,
+                       nil_permille=300, absent_permille=50)
+    power = ol.gen_power(0xA6E5, 1024, 150, abi.POWER_UNIFORM, 1, 1000)
+    _, st = _compare(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 4), p, power, 1024)
+    assert st["decided"].sum() > 0
+
+
+def test_full_c2r(eng):
+    """The bench's c2r batch (round 6): C2 with 5 % abstention (ragged 1-round instances)."""
+    p = abi.gen_params(seed=0xA6E5, n_instances=1_000_000, n_vals=100, rounds_min=1, rounds_max=1,
+                       nil_permille=200, absent_permille=50)
+    power = ol.gen_power(0xA6E5, 1, 100, abi.POWER_UNIFORM, 1, 1000)
+    codes, st = _compare(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 1), p, power, 1)
+    assert st["decided"].sum() > 0 and ((codes >> abi.CODE_MSG_SHIFT) != 0).any()
 
 
 def test_full_c3w_shard(eng):

@@ -162,6 +162,31 @@ def test_multi_rccl_selfcheck_fallback(ops):
         m.close()
 
 
+def test_multi_rccl_broken_every_collective():
+    """An RCCL that corrupts EVERY collective (hook bits 4..7), with only the first
+    kind's self-check re-armed: once that check fails, the call's later collectives
+    (already checked kinds included) must take the host exchange, so the results stay
+    exact and the call reports AGNES_MULTI_X_FALLBACK (a failed check had
+    only replaced the one collective it checked)."""
+    hb = _c5_batch(8, 4096, True)
+    power = ol.gen_power(8, 1, 4096, abi.POWER_ZIPF, 1, 1_000_000)
+    cfg = abi.config(abi.MODE_DEDUP, abi.FLAG_STATE_MACHINE, 1)
+    st0 = abi.new_states(1, 1, abi.STEP_PREVOTE)
+    want, want_st, _ = ol.tally(cfg, hb, power, None, st0)
+    m = MultiEngine([0])
+    try:
+        m.exchange(abi.MULTI_EXCHANGE_RCCL)
+        m.upload_power(power)
+        codes, st, _, stats = m.tally_one(cfg, hb, st0, segments=33)  # every kind checked, clean
+        assert int(stats["exchange"][0]) == abi.MULTI_X_RCCL
+        m.test_corrupt(0x1 | 0xF0)  # DEDUP's MIN u64 (the call's first) re-checked; every kind broken
+        codes, st, _, stats = m.tally_one(cfg, hb, st0, segments=33)
+        assert np.array_equal(codes, want) and st.tobytes() == want_st.tobytes()
+        assert int(stats["exchange"][0]) & abi.MULTI_X_FALLBACK
+    finally:
+        m.close()
+
+
 @pytest.mark.parametrize("n_dev", [1, 3])
 def test_multi_edges_gathered(n_dev):
     """The edge summary of the last agnes_multi_tally, gathered from every range in

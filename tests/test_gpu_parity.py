@@ -233,6 +233,20 @@ CONFIGS = {
     "w64_revisit": (dict(n_instances=2000, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300,
                          dup_permille=100, equiv_permille=100, higher_permille=50),
                     (abi.POWER_UNIFORM, 1 << 28, 1 << 34, 5), (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 5)),
+    # round 6: abstention (absent_permille) -- ragged instance lengths, offsets at any
+    # residue: the flow kernel's unaligned-stream variant (c2r / c3r shapes)
+    "c2r_small": (dict(n_instances=3000, n_vals=100, rounds_min=1, rounds_max=1, nil_permille=200,
+                       absent_permille=50),
+                  (abi.POWER_UNIFORM, 1, 1000, 1), (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 1)),
+    "c3r_small": (dict(n_instances=3000, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300,
+                       absent_permille=50),
+                  (abi.POWER_UNIFORM, 1, 1000, 1024), (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 4)),
+    "c3r_plain": (dict(n_instances=2500, n_vals=101, rounds_min=1, rounds_max=4, nil_permille=350,
+                       absent_permille=120),
+                  (abi.POWER_ZIPF, 1, 4000, 5), (abi.MODE_REFERENCE, 0, 4)),
+    "c4r_ref": (dict(n_instances=2000, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300,
+                     dup_permille=100, equiv_permille=100, higher_permille=50, absent_permille=30),
+                (abi.POWER_UNIFORM, 1, 1000, 64), (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 5)),
     "many_rounds": (dict(n_instances=200, n_vals=20, rounds_min=30, rounds_max=60,
                          nil_permille=300, higher_permille=100),
                     (abi.POWER_UNIFORM, 1, 100, 5),
@@ -347,7 +361,7 @@ def test_determinism_and_sharding(eng):
     assert np.array_equal(outs[0][0], outs[1][0])
     assert outs[0][1].tobytes() == outs[1][1].tobytes()
     # shard = instances [1000, 2000) generated with instance_base
-    p2 = abi.gen_params(**{f: getattr(p, f) for f, _ in abi.GenParams._fields_})
+    p2 = abi.gen_params(**{f: getattr(p, f) for f, _ in abi.GenParams._fields_ if f != "reserved"})
     p2.n_instances, p2.instance_base = 1000, 1000
     shard = eng.gen_batch(p2)
     codes = torch.zeros(shard.n_votes, dtype=torch.uint8, device=eng.device)
@@ -389,6 +403,32 @@ def test_ragged_tiny_and_empty_instances(eng, mode, flags):
     st = _start_states(hb.n_instances) if flags & abi.FLAG_STATE_MACHINE else None
     g, o = run_both(eng, cfg, hb, power, None, st)
     assert_same(g, o)
+
+
+@pytest.mark.parametrize("lengths", [[0, 1, 2, 3, 5, 8, 13, 63, 65, 130, 201],  # walk list + unaligned streams
+                                     [0, 97, 150, 203, 299, 301, 411]])        # unaligned streams only
+def test_ragged_states_out_of_place(eng, lengths):
+    """agnes_tally_states with distinct input and output State arrays on ragged
+    batches: every instance's State must come from states_in, including the instances
+    of batches the flow kernel hands to another kernel (the walk list, the unaligned
+    stream variant) -- the output array starts as garbage."""
+    hb = _ragged_batch(23, 12000, 9, 3, lengths)
+    power = ol.gen_power(23, 13, 9, abi.POWER_UNIFORM, 1, 20)
+    cfg = abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 3)
+    st = _start_states(hb.n_instances)
+    eng.upload_power(power)
+    db = DeviceBatch.from_host(hb, eng.device)
+    codes = torch.zeros(max(hb.n_votes, 1), dtype=torch.uint8, device=eng.device)
+    s_in = states_to_device(st, eng.device)
+    s_out = torch.full_like(s_in, 0x5A)
+    eng.tally_states(cfg, db, codes, s_in, s_out)
+    torch.cuda.synchronize()
+    o_codes, o_states, _ = ol.tally(cfg, hb, power, None, st, threads=8)
+    assert np.array_equal(codes[:hb.n_votes].cpu().numpy(), o_codes)
+    g_st = states_to_host(s_out)
+    bad = np.nonzero(g_st.view(np.uint8).reshape(-1, 64).any(axis=1) !=
+                     o_states.view(np.uint8).reshape(-1, 64).any(axis=1))[0]
+    assert g_st.tobytes() == o_states.tobytes(), f"States differ (first mismatched instance near {bad[:3]})"
 
 
 @pytest.mark.parametrize("mode,flags", [
@@ -530,7 +570,7 @@ def test_c3_shard_parity(eng):
 
 @pytest.mark.parametrize("route", list(ROUTES))
 @pytest.mark.parametrize("name", ["c2_sm", "c3_small", "c4_small", "c2w_small", "w64_dedup_skip", "c3w_small",
-                                  "w64_revisit"])
+                                  "w64_revisit", "c2r_small", "c3r_small", "c4r_ref"])
 def test_routes_generated(eng, route, name):
     p, hb, power, cfg = _make(name)
     cfg = abi.config(cfg.mode, cfg.flags | ROUTES[route], cfg.max_rounds)

@@ -65,13 +65,10 @@ def _check(eng, cfg, hb, power, states=None, in_place=True):
     assert e_recs.cpu().numpy().tobytes() == out[:n].cpu().numpy().tobytes()
     _check_records(eng, cfg, hb, db, states, in_place, o_codes, o_states, o_offs, o_ev)
     if cfg.max_rounds > 1:
-        # several rounds: batches under AGNES_REC_FUSED_MIN_VOTES take the emit pass;
-        # the fused records variant of the flow kernel with the threshold at 0
-        os.environ["AGNES_REC_FUSED_MIN_VOTES"] = "0"
-        try:
-            _check_records(eng, cfg, hb, db, states, in_place, o_codes, o_states, o_offs, o_ev)
-        finally:
-            del os.environ["AGNES_REC_FUSED_MIN_VOTES"]
+        # several rounds: batches under 2^28 votes take the emit pass; the fused records
+        # variant of the flow kernel at any size with AGNES_FLAG_RECORDS_FUSED
+        fused = abi.config(cfg.mode, cfg.flags | abi.FLAG_RECORDS_FUSED, cfg.max_rounds, cfg.reserved)
+        _check_records(eng, fused, hb, db, states, in_place, o_codes, o_states, o_offs, o_ev)
     return o_ev
 
 

@@ -4,6 +4,7 @@ cross-checks it against the independent Python restatement (tests/pyref.py).
 CPU only.  The reference's golden vectors are its two unit tests
 (round_votes.rs:107-132, state_machine.rs:331-345); see tests/golden/.
 """
+import ctypes as C
 import json
 import os
 
@@ -305,3 +306,27 @@ def test_generator_shape():
         assert len(keys) == int(off[i + 1] - off[i]) == R * 26
         # rounds are sequential blocks
         assert (np.diff(b.round[seg].astype(int)) >= 0).all()
+
+
+def test_generator_abstention():
+    """absent_permille (round 6): each round keeps a prefix of its permuted order, so
+    instance lengths take any value (offsets off multiples of 4, the ragged streams a
+    real validator set produces when some validators do not vote); every kept vote is a
+    distinct (round, type, validator) of the full round, rounds stay in order, and the
+    instance's length is the sum of its rounds' kept counts."""
+    full = abi.gen_params(seed=5, n_instances=400, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300)
+    p = abi.gen_params(seed=5, n_instances=400, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300,
+                       absent_permille=50)
+    b, bf = ol.gen_batch(p), ol.gen_batch(full)
+    lens, lf = np.diff(b.offsets.astype(np.int64)), np.diff(bf.offsets.astype(np.int64))
+    assert (lens <= lf).all() and (lens < lf).mean() > 0.9
+    assert 0.9 < lens.sum() / lf.sum() < 0.99
+    assert len(set((b.offsets % 4).tolist())) == 4  # every residue: no 4-aligned stream
+    for i in range(0, 400, 7):
+        seg = slice(int(b.offsets[i]), int(b.offsets[i + 1]))
+        keys = list(zip(b.round[seg].tolist(), b.type[seg].tolist(), b.validator[seg].tolist()))
+        assert len(set(keys)) == len(keys)
+        assert (np.diff(b.round[seg].astype(int)) >= 0).all()
+        assert (b.instance[seg] == i).all()
+    L = ol.lib()
+    assert [int(L.orc_gen_instance_votes(C.byref(p), i)) for i in range(5)] == lens[:5].tolist()
