@@ -134,6 +134,9 @@ __device__ __forceinline__ uint32_t zero_marks(uint32_t x) { /* 0x80 in the byte
     const uint32_t t = (x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
     return ((t | x) & 0x80808080u) ^ 0x80808080u;
 }
+__device__ __forceinline__ uint32_t nz_marks(uint32_t x) { /* 0x80 in the bytes of x that are not zero */
+    return (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+}
 __device__ __forceinline__ uint32_t mark_bytes(uint32_t m) { /* 0x80 marks -> 0xFF bytes (no multiply) */
     return (m << 1) - (m >> 7);
 }
@@ -217,6 +220,9 @@ struct Hdr {
     uint32_t fa, ln;    /* lane k: set fast flag (W64: w64 flag; 2: no such set), length */
     uint32_t stage;     /* 1, 2, 3 (ready)                                       */
     uint32_t stream;    /* stage 2: the offsets pass; stage 3: walked by this kernel */
+    uint32_t rag;       /* stage 2: some offset is not a multiple of 4 (the U kernel's batch);
+                           (U) 2: it also holds an instance of 1 .. 7 votes (the walk list) */
+    uint32_t go;        /* stage 3: this kernel walks it as one stream                        */
 };
 
 /* The value slot of executor (inst, r, t) after the votes before j (round_votes.rs:
@@ -265,10 +271,22 @@ __device__ __attribute__((noinline)) uint32_t label_back(const uint32_t* inst_co
  * edges and the 16-B agnes_edge records go to the instance's segment (agnes_edges.hip's
  * definition, orc_edges: a valid vote is an edge when its executor's state, level |
  * last message << 4, changes). */
-template <bool PC, bool SM, bool R1, bool EVC, bool W64, bool REC = false, bool EDG = false>
+/* U (round 6): the batches whose instance offsets are NOT all multiples of 4 -- the ragged
+ * streams of validator sets with absent validators.  The same chunk walk, but a lane's
+ * eight votes split at any position: the instance (or, in runs mode, the round run)
+ * starting inside the lane owns votes sp .. 7 (its PART B), the one running into the
+ * lane votes 0 .. sp - 1 (PART A); the per-vote choices the aligned kernel makes by the
+ * unit (vote < 4) it makes by the part (vote < sp).  Every instance of such a batch holds
+ * 0 or at least 8 votes, so a lane holds at most one instance start (else the batch goes
+ * to the walk list).  The aligned kernel (U = false) runs first and leaves these batches
+ * to this one (flag AGNES_RAG_FLAG): the aligned kernel's code is unchanged by them. */
+template <bool PC, bool SM, bool R1, bool EVC, bool W64, bool REC = false, bool EDG = false, bool U = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES_FLOW_W64_WPE : ((REC || EDG) ? (R1 ? AGNES_FLOW_XWPE : AGNES_FLOW_XWPE_R) : AGNES_FLOW_WPE)))) void flow(agnes_tally_args a, uint32_t lds_per_wave) {
     static_assert(!REC || (EVC && !W64), "records: with the record counts, u32 sums");
     static_assert(!EDG || (EVC && !W64 && !REC), "edges: the counts are the edges', u32 sums");
+    static_assert(!U || (!W64 && !REC && !EDG), "unaligned streams: u32 sums, codes and record counts");
+    /* the unaligned kernel: nothing to do unless the aligned one left it batches */
+    if (U && *(volatile const uint32_t*)(a.list_count + AGNES_RAG_FLAG) == 0u) return;
     constexpr uint32_t RW = W64 ? RECW64 : RECW; /* record words */
 
     const uint32_t lane = lane_id();
@@ -313,7 +331,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
     /* ---- work queue: batches of FB, then SMALLB ones for the tail ---- */
     const uint32_t qn = gridDim.x < AGNES_FLOW_QN ? gridDim.x : AGNES_FLOW_QN;
     const uint32_t qk = blockIdx.x % qn;
-    uint32_t* const ctr = a.list_count + 1u + qk;
+    uint32_t* const ctr = a.list_count + (U ? (uint32_t)AGNES_RAG_QUEUE : 1u) + qk; /* (U: its own counters) */
     /* batch size: FB, or (launcher) fewer for a batch too small to give every wave
      * several batches -- the makespan is a wave's last batch */
     const uint32_t fb = a.batch && a.batch < FB ? a.batch : FB;
@@ -349,6 +367,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
         h.hs = hs;
         h.stage = 1;
         h.stream = 0;
+        h.rag = 0;
+        h.go = 0;
     };
     auto hdr2 = [&](Hdr& h) { /* stage 2: lengths, offset checks; set constants requested */
         const uint32_t m = h.e0 - h.s0;
@@ -377,9 +397,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
         h.q2h = q2h;
         h.mph = mph;
         h.fa = fa;
-        const bool badl = (lane <= m && (h.olo & 3u) != 0u) || (lane < m && oe < ob);
+        /* (the two kernels classify a batch alike: stream = the offsets and, at stage 3, the
+         * sets in the flow domain; rag = some offset off a multiple of 4) */
+        const bool badl = lane < m && oe < ob;
         const uint64_t O0 = u64of(rdl(h.olo, 0u), rdl(h.ohi, 0u)), Om = u64of(rdl(h.olo, m), rdl(h.ohi, m));
         h.stream = m > 0u && !ballot(badl) && Om - O0 < (1ull << 30);
+        h.rag = ballot(lane <= m && (h.olo & 3u) != 0u) != 0ull;
+        if (U) h.rag = h.rag ? 1u + (ballot(il && len > 0ull && len < 8ull) != 0ull) : 0u;
         h.stage = 2;
     };
     auto hdr3 = [&](Hdr& h) { /* stage 3: quorum thresholds; a flow stream or the walk list */
@@ -407,6 +431,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
         h.q2 = q2;
         h.stream = h.stream && !ballot(!fl);
         h.stage = 3;
+        /* which kernel walks it: the aligned one its aligned streams; with a.ragged the U one
+         * the others (U: those whose instances all hold 0 or >= 8 votes; rag 2 -> the walk list) */
+        h.go = U ? (h.stream && h.rag == 1u) : (h.stream && !h.rag);
     };
     uint32_t spar = 0; /* States staging buffer of the current batch */
     /* the last flush sent a whole chunk's codes as ONE store with every lane active and
@@ -426,16 +453,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
         if (lo == 0u && lim >= CH) {
             sdma_chunk(a.vb.instance + c, a.vb.value + c, a.vb.validator + c, a.vb.round + c, a.vb.type + c, o16, o4,
                        slotl);
-        } else { /* a stream's first or last chunk: only its lanes load (4-vote groups; the
-                  * rest of the slot is never read as active) */
-            if (4u * lane >= lo && 4u * lane < lim) {
+        } else { /* a stream's first or last chunk: only the 4-vote groups holding its votes
+                  * load (the rest of the slot is never read as active).  An unaligned stream's
+                  * first / last group also reads a neighbour's votes, inside the same 16-B
+                  * aligned block of every column, so never past the columns' last page */
+            if (4u * lane + 4u > lo && 4u * lane < lim) {
                 sdma16(a.vb.instance + c, o16, slotl + F_INST);
                 sdma16(a.vb.value + c, o16, slotl + F_VALUE);
                 sdma16(a.vb.validator + c, o16, slotl + F_VAL);
                 sdma4(a.vb.round + c, o4, slotl + F_ROUND);
                 sdma4(a.vb.type + c, o4, slotl + F_TYPE);
             }
-            if (256u + 4u * lane >= lo && 256u + 4u * lane < lim) {
+            if (256u + 4u * lane + 4u > lo && 256u + 4u * lane < lim) {
                 sdma16(a.vb.instance + c + 256u, o16, slotl + F_INST + 1024u);
                 sdma16(a.vb.value + c + 256u, o16, slotl + F_VALUE + 1024u);
                 sdma16(a.vb.validator + c + 256u, o16, slotl + F_VAL + 1024u);
@@ -449,6 +478,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
      * retires in issue order) */
     uint64_t dc_at = ~0ull;
     uint32_t dc0 = 0, dc1 = 0, dc_act = 0; /* dc_act: bit 0 unit A, bit 1 unit B active */
+    uint32_t dcm0 = 0, dcm1 = 0;           /* (U) the active votes' bytes (a lane that is not all active) */
     auto flush = [&]() {
         dc_one = false;
         if (dc_at != ~0ull) {
@@ -456,8 +486,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                 sstore8(a.codes + dc_at, o8, dc0, dc1);
                 dc_one = true;
             } else {
-                if (dc_act == 3u) sstore8(a.codes + dc_at, o8, dc0, dc1);
-                else if (dc_act == 1u) sstore4(a.codes + dc_at, o8, dc0);
+                if (dc_act == 3u) {
+                    sstore8(a.codes + dc_at, o8, dc0, dc1);
+                } else if (U) { /* a stream's first or last lanes: byte stores, the neighbours' codes are another wave's */
+#pragma unroll
+                    for (uint32_t q = 0; q < LV; ++q)
+                        if ((((q < 4u ? dcm0 : dcm1) >> (8u * (q & 3u))) & 1u) != 0u)
+                            a.codes[dc_at + o8 + q] = (uint8_t)((q < 4u ? dc0 : dc1) >> (8u * (q & 3u)));
+                } else if (dc_act == 1u) sstore4(a.codes + dc_at, o8, dc0);
                 else if (dc_act == 2u) sstore4(a.codes + dc_at, o8 + 4u, dc1);
             }
             dc_at = ~0ull;
@@ -539,19 +575,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
         FDIAG(const uint32_t dg_c0 = dg_c; const unsigned long long dg_t = __builtin_amdgcn_s_memrealtime();)
         unsigned char* const sbh = sb + spar * (FB * 64u);
         bool smf = SM; /* the State views are not yet set up from the staged States */
-        if (!H.stream) { /* not one flow stream: the walk list (agnes_sweep.hip) */
+        if (!H.go) { /* not this kernel's stream */
             if (pf_at != ~0ull) { /* an early first-chunk DMA of this batch: drained, dropped */
                 dma_wait();
                 pf_at = ~0ull;
             }
-            uint32_t w0 = 0;
-            if (lane == 0) w0 = atomicAdd(a.list_count + AGNES_WALK_COUNT, m);
-            w0 = rdl(w0, 0u);
-            if (lane < m) a.walk[w0 + lane] = H.s0 + lane;
-            /* the walk kernel works in place on a.states: bring the batch's input States over */
-            if (SM && a.states_in && a.states_in != a.states)
-                for (uint32_t j = lane; j < 4u * m; j += 64u)
-                    reinterpret_cast<uint4*>(a.states + H.s0)[j] = reinterpret_cast<const uint4*>(a.states_in + H.s0)[j];
+            /* the aligned kernel leaves the unaligned streams to the U kernel (a.ragged), which
+             * leaves the aligned ones and the rest to the aligned kernel; the walk list
+             * (agnes_sweep.hip) takes the batches that are no stream of either */
+            const bool walk = U ? (H.stream && H.rag == 2u) : (!H.stream || !a.ragged);
+            if (!U && !walk && lane == 0) a.list_count[AGNES_RAG_FLAG] = 1u; /* (a plain store: idempotent) */
+            if (walk) {
+                uint32_t w0 = 0;
+                if (lane == 0) w0 = atomicAdd(a.list_count + AGNES_WALK_COUNT, m);
+                w0 = rdl(w0, 0u);
+                if (lane < m) a.walk[w0 + lane] = H.s0 + lane;
+                /* the walk kernel works in place on a.states: bring the batch's input States over */
+                if (SM && a.states_in && a.states_in != a.states)
+                    for (uint32_t j = lane; j < 4u * m; j += 64u)
+                        reinterpret_cast<uint4*>(a.states + H.s0)[j] = reinterpret_cast<const uint4*>(a.states_in + H.s0)[j];
+            }
         } else {
             /* the instance records' constants (written at the first chunk's top, once the
              * batch before has been finalized from its records) */
@@ -628,7 +671,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                         hdr2(N);
                     } else if (N.stage == 2u) {
                         hdr3(N);
-                        if (N.stream) dma_states(N, spar ^ 1u);
+                        if (N.go) dma_states(N, spar ^ 1u);
                     }
                 }
 
@@ -641,21 +684,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                 const uint32_t left = Lend - rc;
                 const bool lastc = left > CH && !ballot(tj == CH);
                 const uint32_t hi_r = left < CH ? left : CH;
-                const bool actA = o8 >= lo_r && o8 < hi_r, actB = o8 + 4u >= lo_r && o8 + 4u < hi_r;
+                /* the lane's votes inside the stream: whole units (aligned), or (U) bytes */
+                uint32_t act0, act1;
+                if (U) {
+                    const int32_t nlo = (int32_t)lo_r - (int32_t)o8, nhi = (int32_t)hi_r - (int32_t)o8;
+                    act0 = below_bytes(nhi) & ~below_bytes(nlo);
+                    act1 = below_bytes(nhi - 4) & ~below_bytes(nlo - 4);
+                } else {
+                    act0 = o8 >= lo_r && o8 < hi_r ? 0xFFFFFFFFu : 0u;
+                    act1 = o8 + 4u >= lo_r && o8 + 4u < hi_r ? 0xFFFFFFFFu : 0u;
+                }
+                const bool actA = act0 != 0u, actB = act1 != 0u;
                 uint32_t kA = k0, kB = k0, sA = 0, klast = k0, slast = 0;
                 bool split = false;
-                uint64_t SA = 0, SBm = 0; /* units A / B (lane bits) that start an instance */
+                /* lanes whose unit A / B starts an instance; (U) unit A = the lane's votes before
+                 * spI, the position of the instance start inside the lane (8: none), unit B the rest */
+                uint64_t SA = 0, SBm = 0;
+                uint32_t spI = 8u;
                 if (multi) {
                     uint32_t segw = k0, D = 0;
                     while (bk) {
                         const uint32_t k = (uint32_t)__builtin_ctzll(bk);
                         bk &= bk - 1ull;
                         ++D;
-                        const uint32_t u = rdl(tj, k) >> 2; /* its first unit */
-                        const uint32_t L = u >> 1;
-                        if (u & 1u) SBm |= 1ull << L;
-                        else SA |= 1ull << L;
-                        segw = lane == D ? (k | (L << 8)) : segw;
+                        uint32_t L;
+                        if (U) { /* its lane and position in the lane */
+                            const uint32_t t = rdl(tj, k);
+                            L = t >> 3;
+                            if (t & 7u) SBm |= 1ull << L;
+                            else SA |= 1ull << L;
+                            segw = lane == D ? (k | (L << 8) | ((t & 7u) << 16)) : segw;
+                        } else {
+                            const uint32_t u = rdl(tj, k) >> 2; /* its first unit */
+                            L = u >> 1;
+                            if (u & 1u) SBm |= 1ull << L;
+                            else SA |= 1ull << L;
+                            segw = lane == D ? (k | (L << 8)) : segw;
+                        }
                         klast = k;
                         slast = L;
                     }
@@ -664,9 +729,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                     split = ((SBm >> lane) & 1ull) != 0ull;
                     const uint32_t wA = shfl(segw, dA), wB = shfl(segw, dA + (split ? 1u : 0u));
                     kA = wA & 0xFFu;
-                    sA = wA >> 8;
+                    sA = (wA >> 8) & 0xFFu;
                     kB = wB & 0xFFu;
+                    if (U && split) spI = wB >> 16;
                 }
+                /* vote s of the lane in unit B: the aligned kernel's unit is fixed (s >= 4), the U
+                 * kernel's starts at spI (no start: 8, and kB == kA) */
+                auto inB = [&](uint32_t s) -> bool { return U ? s >= spI : s >= 4u; };
                 const uint4 recA = *reinterpret_cast<const uint4*>(itab + RW * kA); /* q2, pbase, nv, State.round (0x100: none) */
                 const uint4 recB = multi ? *reinterpret_cast<const uint4*>(itab + RW * kB) : recA;
 
@@ -677,7 +746,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                     if (rc + CH < Lend) {
                         nc = c + CH;
                         nl = Lend - rc - CH;
-                    } else if (N.s0 < N.e0 && N.stage == 3u && N.stream) {
+                    } else if (N.s0 < N.e0 && N.stage == 3u && N.go) {
                         const uint32_t mN = N.e0 - N.s0;
                         const uint64_t n0 = u64of(rdl(N.olo, 0u), rdl(N.ohi, 0u));
                         nc = n0 & ~127ull;
@@ -726,7 +795,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                         const uint32_t pbA = recA.y, pbB = recB.y;
 #pragma unroll
                         for (uint32_t s = 0; s < LV; ++s) {
-                            const uint32_t v = val[s], pb = s < 4u ? pbA : pbB, nvs = s < 4u ? recA.z : recB.z;
+                            const uint32_t v = val[s], pb = inB(s) ? pbB : pbA, nvs = inB(s) ? recB.z : recA.z;
                             const uint32_t idx = v < nvs ? pb + v : 0u;
                             if constexpr (W64)
                                 wq[s] = PC ? reinterpret_cast<const uint64_t*>(agnes_smem)[idx] : (uint64_t)a.power[idx];
@@ -746,23 +815,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                                                   : (t8[0] & 0xFEFEFEFEu) | ((r8[0] | ((r8[0] & 0x7F7F7F7Fu) + RK)) & 0x80808080u);
                     const uint32_t bad1 = R == 1u ? (t8[1] & 0xFEFEFEFEu) | r8[1]
                                                   : (t8[1] & 0xFEFEFEFEu) | ((r8[1] | ((r8[1] & 0x7F7F7F7Fu) + RK)) & 0x80808080u);
-                    const uint32_t mA = max(max(val[0], val[1]), max(val[2], val[3]));
-                    const uint32_t mB = max(max(val[4], val[5]), max(val[6], val[7]));
-                    /* a unit names its instance: the OR of the four ids XOR the id is zero (three
-                     * bitwise ops, not four compares whose lane masks are rebuilt as bits) */
-                    const uint32_t dA = (inst[0] ^ idA) | (inst[1] ^ idA) | (inst[2] ^ idA) | (inst[3] ^ idA);
-                    const uint32_t dB = (inst[4] ^ idB) | (inst[5] ^ idB) | (inst[6] ^ idB) | (inst[7] ^ idB);
-                    const bool okA = (bad0 | dA) == 0u && mA < recA.z;
-                    const bool okB = (bad1 | dB) == 0u && mB < recB.z;
-                    all_ok = !ballot((actA && !okA) || (actB && !okB));
-                    okb0 = actA ? 0xFFFFFFFFu : 0u;
-                    okb1 = actB ? 0xFFFFFFFFu : 0u;
+                    if (U) {
+                        /* the unit's instance and set per vote: the lane is checked as a whole (a
+                         * lane with votes outside the stream fails and takes the exact path) */
+                        uint32_t d = bad0 | bad1;
+                        bool vin = true;
+#pragma unroll
+                        for (uint32_t s = 0; s < LV; ++s) {
+                            d |= inst[s] ^ (inB(s) ? idB : idA);
+                            vin = vin && val[s] < (inB(s) ? recB.z : recA.z);
+                        }
+                        all_ok = !ballot((actA || actB) && !(d == 0u && vin));
+                    } else {
+                        const uint32_t mA = max(max(val[0], val[1]), max(val[2], val[3]));
+                        const uint32_t mB = max(max(val[4], val[5]), max(val[6], val[7]));
+                        /* a unit names its instance: the OR of the four ids XOR the id is zero (three
+                         * bitwise ops, not four compares whose lane masks are rebuilt as bits) */
+                        const uint32_t dA = (inst[0] ^ idA) | (inst[1] ^ idA) | (inst[2] ^ idA) | (inst[3] ^ idA);
+                        const uint32_t dB = (inst[4] ^ idB) | (inst[5] ^ idB) | (inst[6] ^ idB) | (inst[7] ^ idB);
+                        const bool okA = (bad0 | dA) == 0u && mA < recA.z;
+                        const bool okB = (bad1 | dB) == 0u && mB < recB.z;
+                        all_ok = !ballot((actA && !okA) || (actB && !okB));
+                    }
+                    okb0 = act0;
+                    okb1 = act1;
                     if (!all_ok) { /* the exact per-vote checks */
                         uint32_t o0 = 0, o1 = 0;
 #pragma unroll
                         for (uint32_t s = 0; s < 4u; ++s) {
-                            const bool g0 = ((bad0 >> (8u * s)) & 0xFFu) == 0u && inst[s] == idA && val[s] < recA.z;
-                            const bool g1 = ((bad1 >> (8u * s)) & 0xFFu) == 0u && inst[4u + s] == idB && val[4u + s] < recB.z;
+                            const uint32_t iA = inB(s) ? idB : idA, iB = inB(4u + s) ? idB : idA;
+                            const uint32_t nA = inB(s) ? recB.z : recA.z, nB = inB(4u + s) ? recB.z : recA.z;
+                            const bool g0 = ((bad0 >> (8u * s)) & 0xFFu) == 0u && inst[s] == iA && val[s] < nA;
+                            const bool g1 = ((bad1 >> (8u * s)) & 0xFFu) == 0u && inst[4u + s] == iB && val[4u + s] < nB;
                             o0 |= g0 ? 0xFFu << (8u * s) : 0u;
                             o1 |= g1 ? 0xFFu << (8u * s) : 0u;
                         }
@@ -808,7 +892,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                 uint32_t uA = 0, uB = 0, sAr = sA;
                 bool splitr = split, multir = multi;
                 uint64_t SAr = 0, SBr = 0;
-                if (!R1 && all_ok) {
+                uint32_t spR = spI; /* (U) the position of the run start inside the lane (8: none) */
+                if (U && !R1 && all_ok) {
+                    /* (U) runs at any position: a lane may hold one run start after its first
+                     * vote (an instance start or a round change), and the rounds of an instance
+                     * only increase inside the chunk */
+                    uint32_t q0 = r8[0], q1 = r8[1];
+                    if (lo_r != 0u || hi_r != CH) { /* the votes outside the stream take the nearest round inside */
+                        const uint32_t hz = hi_r - 1u;
+                        const uint32_t rf = (rdl(((lo_r >> 2) & 1u) ? r8[1] : r8[0], lo_r >> 3) >> (8u * (lo_r & 3u))) & 0xFFu;
+                        const uint32_t rz = (rdl(((hz >> 2) & 1u) ? r8[1] : r8[0], hz >> 3) >> (8u * (hz & 3u))) & 0xFFu;
+                        const int32_t nlo = (int32_t)lo_r - (int32_t)o8;
+                        const uint32_t bl0 = below_bytes(nlo), bl1 = below_bytes(nlo - 4);
+                        q0 = (q0 & act0) | (~act0 & ((bl0 & (rf * 0x01010101u)) | (~bl0 & (rz * 0x01010101u))));
+                        q1 = (q1 & act1) | (~act1 & ((bl1 & (rf * 0x01010101u)) | (~bl1 & (rz * 0x01010101u))));
+                    }
+                    const uint32_t pl = shfl(q1, lane - 1u) >> 24; /* the previous lane's last round */
+                    const uint32_t pw0 = (q0 << 8) | (lane ? pl : (q0 & 0xFFu)), pw1 = (q1 << 8) | (q0 >> 24);
+                    const uint32_t ch0 = nz_marks(q0 ^ pw0), ch1 = nz_marks(q1 ^ pw1); /* round changes */
+                    const uint32_t ge0 = ((q0 | 0x80808080u) - pw0) & 0x80808080u; /* round >= the one before */
+                    const uint32_t ge1 = ((q1 | 0x80808080u) - pw1) & 0x80808080u;
+                    const bool iA = ((SA >> lane) & 1ull) != 0ull;
+                    const uint32_t is0 = (iA ? 0x80u : 0u) | (spI < 4u ? 0x80u << (8u * spI) : 0u);
+                    const uint32_t is1 = (spI >= 4u && spI < 8u) ? 0x80u << (8u * (spI - 4u)) : 0u;
+                    const uint32_t in0 = (ch0 | is0) & ~0x80u, in1 = ch1 | is1; /* run starts after vote 0 */
+                    const bool badr = ((ch0 & ~ge0 & ~is0) | (ch1 & ~ge1 & ~is1)) != 0u ||
+                                      __builtin_popcount(in0) + __builtin_popcount(in1) > 1;
+                    if (!ballot(badr)) {
+                        runs = true;
+                        const bool rsA = (ch0 & 0x80u) != 0u && !iA;
+                        spR = in0 ? (uint32_t)__builtin_ctz(in0) >> 3 : (in1 ? 4u + ((uint32_t)__builtin_ctz(in1) >> 3) : 8u);
+                        splitr = spR < 8u;
+                        SAr = SA | ballot(rsA);
+                        SBr = ballot(splitr);
+                        multir = (SAr | SBr) != 0ull;
+                        uA = q0 & 0xFFu;
+                        uB = splitr ? ((spR < 4u ? q0 : q1) >> (8u * (spR & 3u))) & 0xFFu : uA;
+                        const uint64_t mA = SAr & ((2ull << lane) - 1ull), mB = SBr & ((1ull << lane) - 1ull);
+                        const uint32_t la = mA ? 63u - (uint32_t)__builtin_clzll(mA) : 0u;
+                        const uint32_t lb = mB ? 63u - (uint32_t)__builtin_clzll(mB) : 0u;
+                        sAr = la > lb ? la : lb;
+                    }
+                } else if (!R1 && all_ok) {
                     uA = r8[0] & 0xFFu;
                     uB = r8[1] & 0xFFu;
                     if (lo_r != 0u || hi_r != CH) {
@@ -859,6 +984,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                     constexpr bool ONE = decltype(one_t)::value;
                     const uint32_t sAx = ONE ? sAr : sA;
                     const bool splitx = ONE ? splitr : split, multix = ONE ? multir : multi;
+                    /* (U) the lane's segment split: a run start in runs mode, else an instance start */
+                    const uint32_t spx = ONE ? spR : spI;
+                    auto inBx = [&](uint32_t s) -> bool { return U ? s >= spx : s >= 4u; };
                     uint32_t sh0 = sh0c, sh1 = sh1c, ts0 = ts0c, ts1 = ts1c;
                     if (!R1) asm volatile("" : "+v"(sh0), "+v"(sh1), "+v"(ts0), "+v"(ts1)); /* extracts stay per pass */
                     /* 0xFF in the bytes of this round's votes */
@@ -877,7 +1005,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                         if (R > 1u && !ONE) ws &= (uint32_t)__builtin_amdgcn_sbfe((int32_t)(s < 4u ? rm0 : rm1), bs, 8u);
                         if constexpr (EDG) Dwb[s] = (uint32_t)(P >> __builtin_amdgcn_ubfe(s < 4u ? ts0 : ts1, bs, 8u));
                         P += (uint64_t)ws << __builtin_amdgcn_ubfe(s < 4u ? sh0 : sh1, bs, 8u);
-                        if (s == 3u) P3 = P;
+                        if (U) { /* P3: the prefix of unit A (through vote spx - 1) */
+                            if (s < 7u) P3 = s < spx ? P : P3;
+                        } else if (s == 3u) {
+                            P3 = P;
+                        }
                         Dw[s] = (uint32_t)(P >> __builtin_amdgcn_ubfe(s < 4u ? ts0 : ts1, bs, 8u));
                     }
                     /* the lane's last segment (unit B alone when it starts a segment) */
@@ -948,9 +1080,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                     for (uint32_t s = 0; s < LV; ++s) {
                         const uint32_t bs = 8u * (s & 3u);
                         const uint32_t tsh = __builtin_amdgcn_ubfe(s < 4u ? ts0 : ts1, bs, 8u);
-                        const int32_t tv = (int32_t)(uint32_t)((s < 4u ? TVa : TVb) >> tsh);
-                        const int32_t tn = (int32_t)(uint32_t)((s < 4u ? TNa : TNb) >> tsh);
-                        const int32_t ta = (int32_t)(uint32_t)((s < 4u ? TAa : TAb) >> tsh);
+                        const int32_t tv = (int32_t)(uint32_t)((inBx(s) ? TVb : TVa) >> tsh);
+                        const int32_t tn = (int32_t)(uint32_t)((inBx(s) ? TNb : TNa) >> tsh);
+                        const int32_t ta = (int32_t)(uint32_t)((inBx(s) ? TAb : TAa) >> tsh);
                         const int32_t sv = (int32_t)(Dw[s] & 0xFFFFu), sn = (int32_t)(Dw[s] >> 16);
                         uint32_t l = sv + sn > ta ? 1u : 0u;
                         l = sn > tn ? 2u : l;
@@ -977,7 +1109,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                         const int32_t tvc = (int32_t)(uint32_t)(TVa >> 32);
                         cf |= (eA_ && (tvp < 0 || tnp < 0)) ? 1u : 0u;
                         cf |= tvc < 0 ? 2u : 0u;
-                        if (!splitx) {
+                        if (!U && !splitx) { /* (U: K4 takes the lane's unit A whole) */
                             cf |= (eB_ && ((int32_t)p3vp > tvp || (int32_t)p3np > tnp)) ? 4u : 0u;
                             cf |= (int32_t)p3vc > tvc ? 8u : 0u;
                         }
@@ -1215,8 +1347,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                 uint32_t c0 = __builtin_amdgcn_perm(EV_HI, EV_LO, lv0 | (ts0c >> 3));
                 uint32_t c1 = __builtin_amdgcn_perm(EV_HI, EV_LO, lv1 | (ts1c >> 3));
                 if (!all_ok) {
-                    c0 = (c0 & okb0) | ((actA ? ~okb0 : 0u) & (AGNES_CODE_INVALID * 0x01010101u));
-                    c1 = (c1 & okb1) | ((actB ? ~okb1 : 0u) & (AGNES_CODE_INVALID * 0x01010101u));
+                    c0 = (c0 & okb0) | ((act0 & ~okb0) & (AGNES_CODE_INVALID * 0x01010101u));
+                    c1 = (c1 & okb1) | ((act1 & ~okb1) & (AGNES_CODE_INVALID * 0x01010101u));
                 }
 
                 /* ---- K4: State::apply(v.round, event) in stream order ---- */
@@ -1235,6 +1367,92 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                                            (eqb | (X_C * 0x01010101u));
                         return act ? x : 0u;
                     };
+                    if constexpr (U) {
+                        /* (U) the lane's two PARTS as 8-byte masks: unit A = votes before spk (the
+                         * split of the tally pass: a run start in runs mode, else an instance
+                         * start), unit B the rest; the same derivation as the aligned units below */
+                        const uint32_t spk = (!R1 && runs) ? spR : spI;
+                        const uint64_t pmA = u64of(below_bytes((int32_t)spk), below_bytes((int32_t)spk - 4));
+                        const uint64_t xA = u64of(roles(eA.x, eA.y, r8[0], c0, true) & act0, roles(eA.x, eA.y, r8[1], c1, true) & act1);
+                        const uint64_t xB = kB == kA ? xA
+                                                     : u64of(roles(eB.x, eB.y, r8[0], c0, true) & act0,
+                                                             roles(eB.x, eB.y, r8[1], c1, true) & act1);
+                        const uint64_t XPA = xA & pmA, XPB = xB & ~pmA;
+                        if (ballot((XPA | XPB) != 0ull)) {
+                            constexpr uint64_t B8 = 0x0101010101010101ull;
+                            const uint32_t pos0 = rc + o8; /* stream-relative position of the lane's vote 0 */
+                            const uint2 qA = *reinterpret_cast<const uint2*>(rA + R_P1);
+                            const uint2 qB = *reinterpret_cast<const uint2*>(rB + R_P1);
+                            const uint64_t nn = ~u64of(mark_bytes(nb0 << 3), mark_bytes(nb1 << 3)); /* non-nil votes */
+                            const uint64_t r64 = u64of(r8[0], r8[1]);
+                            auto vsel8 = [&](uint32_t b) -> uint32_t {
+                                const uint32_t l0 = (b & 1u) ? value[1] : value[0], l1 = (b & 1u) ? value[3] : value[2];
+                                const uint32_t h0 = (b & 1u) ? value[5] : value[4], h1 = (b & 1u) ? value[7] : value[6];
+                                const uint32_t lo = (b & 2u) ? l1 : l0, hi = (b & 2u) ? h1 : h0;
+                                return (b & 4u) ? hi : lo;
+                            };
+                            auto part = [&](uint64_t x, bool crossedP, bool crossedC, uint32_t* rk, uint32_t* sx, uint32_t vall,
+                                            uint64_t& vc) -> uint64_t {
+                                const uint64_t pm = x & (X_P1 * B8), cm = x & (X_C * B8);
+                                const uint64_t lp = pm & (0ull - pm), lc = (cm & (0ull - cm)) >> 1;
+                                const uint64_t preR = lp - 1ull, aliveR = lc - 1ull;
+                                const bool p1ok = !crossedP && !crossedC && preR < aliveR;
+                                const uint64_t alive = crossedC ? 0ull : aliveR;
+                                const uint64_t pre = (crossedP || crossedC) ? 0ull : (preR < aliveR ? preR : aliveR);
+                                const uint64_t atC = crossedC ? 0ull : (lc << 8) - lc; /* (byte 7: wraps to 0xFF << 56) */
+                                const uint64_t atP = p1ok ? (lp << 8) - lp : 0ull;
+                                if (!crossedC && lc) {
+                                    const uint32_t b = (uint32_t)__builtin_ctzll(lc) >> 3;
+                                    rk[R_C] = pos0 + b;
+                                    sx[12] = vsel8(b);
+                                    if (!R1) rk[R_DR] = (uint32_t)(r64 >> (8u * b)) & 0xFFu;
+                                }
+                                if (p1ok) {
+                                    const uint32_t b = (uint32_t)__builtin_ctzll(lp) >> 3;
+                                    rk[R_P1] = pos0 + b;
+                                    if ((x >> (8u * b)) & X_PV) {
+                                        rk[R_DF] = F_LOCK;
+                                        sx[10] = vsel8(b);
+                                    }
+                                }
+                                vc = x & alive & (~pre | u64of(vall, vall)) & nn & (X_PV * B8);
+                                uint64_t msg = (x & ((pre & (X_TP * B8)) | (alive & (X_TC * B8)))) << 2;
+                                msg |= atP & ((AGNES_VMSG_PRECOMMIT_NIL << AGNES_CODE_MSG_SHIFT) * B8 + (x & (X_PV * B8)));
+                                msg |= atC & ((AGNES_VMSG_DECISION << AGNES_CODE_MSG_SHIFT) * B8);
+                                return msg;
+                            };
+                            uint32_t* const sA = reinterpret_cast<uint32_t*>(sbh + 64u * kA);
+                            uint32_t* const sB = reinterpret_cast<uint32_t*>(sbh + 64u * kB);
+                            bool xcA = false, xcB = false;
+                            if (!R1 && runs) { /* C crossed in an earlier part of the instance, another run */
+                                const uint64_t XA = ballot((XPA & (X_C * B8)) != 0ull);
+                                const uint64_t XB = ballot((XPB & (X_C * B8)) != 0ull);
+                                const uint64_t iAm = SA & ((2ull << lane) - 1ull), iBm = SBm & ((1ull << lane) - 1ull);
+                                const uint32_t fa = iAm ? 2u * (63u - (uint32_t)__builtin_clzll(iAm)) : 0u;
+                                const uint32_t fb = iBm ? 2u * (63u - (uint32_t)__builtin_clzll(iBm)) + 1u : 0u;
+                                const uint32_t ui = fa > fb ? fa : fb;
+                                const uint64_t below = (1ull << lane) - 1ull;
+                                const uint64_t fromA = ~((1ull << ((ui + 1u) >> 1)) - 1ull), fromB = ~((1ull << (ui >> 1)) - 1ull);
+                                xcA = ((XA & fromA & below) | (XB & fromB & below)) != 0ull;
+                                xcB = ((SBm >> lane) & 1ull) == 0ull && (xcA || ((XA >> lane) & 1ull) != 0ull);
+                            }
+                            uint64_t vA = 0, vB = 0;
+                            uint64_t msg = part(XPA, (cf & 1u) || qA.x != NONE, (cf & 2u) || xcA || qA.y != NONE, rA, sA, eA.z, vA);
+                            if (XPB) msg |= part(XPB, qB.x != NONE, xcB || qB.y != NONE, rB, sB, eB.z, vB);
+                            c0 |= (uint32_t)msg;
+                            c1 |= (uint32_t)(msg >> 32);
+                            if (ballot((vA | vB) != 0ull)) { /* valid (:198, :202): the last candidate */
+                                if (vA) {
+                                    const uint32_t b = (63u - (uint32_t)__builtin_clzll(vA)) >> 3;
+                                    atomicMax(vtab + kA, ((unsigned long long)(pos0 + b + 1u) << 32) | vsel8(b));
+                                }
+                                if (vB) {
+                                    const uint32_t b = (63u - (uint32_t)__builtin_clzll(vB)) >> 3;
+                                    atomicMax(vtab + kB, ((unsigned long long)(pos0 + b + 1u) << 32) | vsel8(b));
+                                }
+                            }
+                        }
+                    } else {
                     const uint32_t x0 = roles(eA.x, eA.y, r8[0], c0, actA), x1 = roles(eB.x, eB.y, r8[1], c1, actB);
                     if (ballot((x0 | x1) != 0u)) {
                         const uint32_t pos0 = rc + o8, pos1 = pos0 + 4u; /* stream-relative */
@@ -1330,6 +1548,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                             }
                         }
                     }
+                    } /* (aligned units) */
                 }
 
                 if constexpr (REC) {
@@ -1604,7 +1823,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                         const uint32_t iv = (e + 0x7A7A7A7Au) & 0x80808080u; /* INVALID / REJECTED   */
                         return (uint32_t)__builtin_popcount(nz & ~iv);
                     };
-                    const uint32_t nA = actA ? recs(c0) : 0u, nB = actB ? recs(c1) : 0u;
+                    uint32_t nA, nB;
+                    if (U) { /* (U) the units split at the instance start spI */
+                        const uint32_t m0 = below_bytes((int32_t)spI), m1 = below_bytes((int32_t)spI - 4);
+                        nA = recs(c0 & act0 & m0) + recs(c1 & act1 & m1);
+                        nB = recs(c0 & act0 & ~m0) + recs(c1 & act1 & ~m1);
+                    } else {
+                        nA = actA ? recs(c0) : 0u;
+                        nB = actB ? recs(c1) : 0u;
+                    }
                     atomicAdd(etab + kA, kA == kB ? nA + nB : nA);
                     atomicAdd(etab + kB, kA == kB ? 0u : nB);
                 }
@@ -1612,19 +1839,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                 /* codes (deferred) */
                 dc0 = c0;
                 dc1 = c1;
-                dc_act = (actA ? 1u : 0u) | (actB ? 2u : 0u);
+                if (U) {
+                    dc_act = (act0 & act1) == 0xFFFFFFFFu ? 3u : 0u;
+                    dcm0 = act0;
+                    dcm1 = act1;
+                } else {
+                    dc_act = (actA ? 1u : 0u) | (actB ? 2u : 0u);
+                }
                 dc_at = c;
                 __builtin_amdgcn_wave_barrier();
             }
         }
         /* batch end: the record counts and the States out (a walk-list batch's are the
          * walk kernel's) */
-        if (EVC && m && H.stream) {
+        if (EVC && m && H.go) {
             __builtin_amdgcn_wave_barrier();
             const uint32_t Le = rdl(H.olo, m) - rdl(H.olo, 0u) + (rdl(H.olo, 0u) & 127u);
             if (lane < m) a.ev_counts[H.s0 + lane] = Le ? (uint64_t)etab[lane] : 0ull;
         }
-        if (SM && m && H.stream) {
+        if (SM && m && H.go) {
             if (smf) { /* no vote: the States as they came */
                 dma_wait();
                 for (uint32_t j = lane; j < 4u * m; j += 64u)
@@ -1649,7 +1882,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
         if (N.stage < 3u) { /* a short batch: the rest of the header now */
             if (N.stage == 1u) hdr2(N);
             hdr3(N);
-            if (N.stream) dma_states(N, spar ^ 1u);
+            if (N.go) dma_states(N, spar ^ 1u);
         }
         H = N;
         spar ^= 1u;
@@ -1682,13 +1915,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
 /* ------------------------------------------------------------------ */
 /* launcher                                                            */
 
-template <bool SM, bool R1, bool EVC, bool W64, bool REC = false, bool EDG = false>
-static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStream_t st) {
+/* One flow kernel (U: the unaligned-stream variant).  The aligned kernel sizes the batches
+ * (bp: batch, tail batch, tail instances) and the U kernel walks the same partition, so the
+ * two classify every batch alike. */
+template <bool SM, bool R1, bool EVC, bool W64, bool REC = false, bool EDG = false, bool U = false>
+static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStream_t st, uint32_t* bp) {
     const uint32_t n = a->vb.n_instances;
     if (n == 0) return hipSuccess;
     using agnes::flow::flow;
-    const void* fns[2] = {reinterpret_cast<const void*>(&flow<false, SM, R1, EVC, W64, REC, EDG>),
-                          reinterpret_cast<const void*>(&flow<true, SM, R1, EVC, W64, REC, EDG>)};
+    const void* fns[2] = {reinterpret_cast<const void*>(&flow<false, SM, R1, EVC, W64, REC, EDG, U>),
+                          reinterpret_cast<const void*>(&flow<true, SM, R1, EVC, W64, REC, EDG, U>)};
     const uint32_t lpw = agnes::flow::lds_bytes(SM, a->max_rounds, EVC, W64, EDG);
     const uint64_t wave_lds = (uint64_t)lpw * AGNES_WAVES_PER_BLOCK;
     const uint64_t pcb = agnes::align16((W64 ? 8ull : 4ull) * a->n_sets * a->n_vals);
@@ -1724,7 +1960,11 @@ static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStrea
     b.power_cache = o->pc ? (uint32_t)pcb : 0u;
     const uint64_t lds = wave_lds + b.power_cache;
     const void* fn = fns[o->pc ? 1 : 0];
-    {   /* batches of FB, fewer when that leaves a wave under AGNES_FLOW_BATCHES_PER_WAVE */
+    if (U) { /* the aligned kernel's partition */
+        b.batch = bp[0];
+        b.tail_batch = bp[1];
+        b.tail_n = bp[2];
+    } else { /* batches of FB, fewer when that leaves a wave under AGNES_FLOW_BATCHES_PER_WAVE */
         const uint64_t waves = (uint64_t)(num_cus > 0 ? num_cus : 256) * (uint64_t)o->per_cu * AGNES_WAVES_PER_BLOCK;
         uint64_t fbx = AGNES_FLOW_BATCHES_PER_WAVE ? (uint64_t)n / (waves * AGNES_FLOW_BATCHES_PER_WAVE) : agnes::flow::FB;
         fbx = fbx < 4u ? 4u : (fbx > agnes::flow::FB ? agnes::flow::FB : fbx);
@@ -1742,6 +1982,9 @@ static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStrea
             b.tail_batch = (uint32_t)tb;
             b.tail_n = (uint32_t)tn;
         }
+        bp[0] = b.batch;
+        bp[1] = b.tail_batch;
+        bp[2] = b.tail_n;
     }
     if (lds > 48u * 1024u) {
         hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1752,8 +1995,8 @@ static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStrea
     const uint64_t cap = ncu * (uint64_t)o->per_cu;
     if (blocks > cap) blocks = cap;
     if (blocks == 0) blocks = 1;
-    if (o->pc) hipLaunchKernelGGL((flow<true, SM, R1, EVC, W64, REC, EDG>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
-    else hipLaunchKernelGGL((flow<false, SM, R1, EVC, W64, REC, EDG>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
+    if (o->pc) hipLaunchKernelGGL((flow<true, SM, R1, EVC, W64, REC, EDG, U>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
+    else hipLaunchKernelGGL((flow<false, SM, R1, EVC, W64, REC, EDG, U>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
     return hipGetLastError();
 }
 
@@ -1780,36 +2023,56 @@ bool agnes_flow_counts_events(uint32_t flags, uint32_t max_rounds, bool edges) {
     return max_rounds <= 15u && agnes::flow::lds_bytes(sm, max_rounds, true, false, edges) * (sm ? 12u : 16u) <= 160u * 1024u;
 }
 
-hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t st) {
+bool agnes_flow_ragged_ok(const agnes_tally_args* a) {
+    /* the unaligned-stream kernel: u32 sums, codes, States and record counts */
+    return !a->w64 && !a->rec_out && !a->edges;
+}
+
+hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t st, bool ragged_pass, uint32_t* bp) {
     const bool sm = (a->flags & AGNES_FLAG_STATE_MACHINE) != 0 && a->states != nullptr;
+    if (ragged_pass) { /* after the aligned kernel, with its partition */
+        if (!a->ragged || !agnes_flow_ragged_ok(a)) return hipErrorInvalidValue;
+        if (a->ev_counts) {
+            if (a->max_rounds == 1u)
+                return sm ? launch_flow_k<true, true, true, false, false, false, true>(a, num_cus, st, bp)
+                          : launch_flow_k<false, true, true, false, false, false, true>(a, num_cus, st, bp);
+            return sm ? launch_flow_k<true, false, true, false, false, false, true>(a, num_cus, st, bp)
+                      : launch_flow_k<false, false, true, false, false, false, true>(a, num_cus, st, bp);
+        }
+        if (a->max_rounds == 1u)
+            return sm ? launch_flow_k<true, true, false, false, false, false, true>(a, num_cus, st, bp)
+                      : launch_flow_k<false, true, false, false, false, false, true>(a, num_cus, st, bp);
+        return sm ? launch_flow_k<true, false, false, false, false, false, true>(a, num_cus, st, bp)
+                  : launch_flow_k<false, false, false, false, false, false, true>(a, num_cus, st, bp);
+    }
     if (a->w64) { /* the u64 domain: no record counts (agnes_sweep_supported) */
         if (a->ev_counts) return hipErrorInvalidValue;
         if (a->max_rounds == 1u)
-            return sm ? launch_flow_k<true, true, false, true>(a, num_cus, st) : launch_flow_k<false, true, false, true>(a, num_cus, st);
-        return sm ? launch_flow_k<true, false, false, true>(a, num_cus, st) : launch_flow_k<false, false, false, true>(a, num_cus, st);
+            return sm ? launch_flow_k<true, true, false, true>(a, num_cus, st, bp) : launch_flow_k<false, true, false, true>(a, num_cus, st, bp);
+        return sm ? launch_flow_k<true, false, false, true>(a, num_cus, st, bp) : launch_flow_k<false, false, false, true>(a, num_cus, st, bp);
     }
     if (a->rec_out && a->edges) { /* agnes_tally_edges: the edge counts and records */
         if (!a->ev_counts) return hipErrorInvalidValue;
         if (a->max_rounds == 1u)
-            return sm ? launch_flow_k<true, true, true, false, false, true>(a, num_cus, st)
-                      : launch_flow_k<false, true, true, false, false, true>(a, num_cus, st);
-        return sm ? launch_flow_k<true, false, true, false, false, true>(a, num_cus, st)
-                  : launch_flow_k<false, false, true, false, false, true>(a, num_cus, st);
+            return sm ? launch_flow_k<true, true, true, false, false, true>(a, num_cus, st, bp)
+                      : launch_flow_k<false, true, true, false, false, true>(a, num_cus, st, bp);
+        return sm ? launch_flow_k<true, false, true, false, false, true>(a, num_cus, st, bp)
+                  : launch_flow_k<false, false, true, false, false, true>(a, num_cus, st, bp);
     }
     if (a->rec_out) { /* agnes_tally_records: counts and the records themselves */
         if (!a->ev_counts) return hipErrorInvalidValue;
         if (a->max_rounds == 1u)
-            return sm ? launch_flow_k<true, true, true, false, true>(a, num_cus, st)
-                      : launch_flow_k<false, true, true, false, true>(a, num_cus, st);
-        return sm ? launch_flow_k<true, false, true, false, true>(a, num_cus, st)
-                  : launch_flow_k<false, false, true, false, true>(a, num_cus, st);
+            return sm ? launch_flow_k<true, true, true, false, true>(a, num_cus, st, bp)
+                      : launch_flow_k<false, true, true, false, true>(a, num_cus, st, bp);
+        return sm ? launch_flow_k<true, false, true, false, true>(a, num_cus, st, bp)
+                  : launch_flow_k<false, false, true, false, true>(a, num_cus, st, bp);
     }
     if (a->ev_counts) {
         if (a->max_rounds == 1u)
-            return sm ? launch_flow_k<true, true, true, false>(a, num_cus, st) : launch_flow_k<false, true, true, false>(a, num_cus, st);
-        return sm ? launch_flow_k<true, false, true, false>(a, num_cus, st) : launch_flow_k<false, false, true, false>(a, num_cus, st);
+            return sm ? launch_flow_k<true, true, true, false>(a, num_cus, st, bp) : launch_flow_k<false, true, true, false>(a, num_cus, st, bp);
+        return sm ? launch_flow_k<true, false, true, false>(a, num_cus, st, bp) : launch_flow_k<false, false, true, false>(a, num_cus, st, bp);
     }
     if (a->max_rounds == 1u)
-        return sm ? launch_flow_k<true, true, false, false>(a, num_cus, st) : launch_flow_k<false, true, false, false>(a, num_cus, st);
-    return sm ? launch_flow_k<true, false, false, false>(a, num_cus, st) : launch_flow_k<false, false, false, false>(a, num_cus, st);
+        return sm ? launch_flow_k<true, true, false, false>(a, num_cus, st, bp) : launch_flow_k<false, true, false, false>(a, num_cus, st, bp);
+    return sm ? launch_flow_k<true, false, false, false>(a, num_cus, st, bp) : launch_flow_k<false, false, false, false>(a, num_cus, st, bp);
 }

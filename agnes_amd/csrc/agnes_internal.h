@@ -68,6 +68,8 @@ typedef struct agnes_tally_args {
     uint32_t w64;         /* the u64 fast domain (agnes_set_info.w64 sets outside the u32 one):
                              tally_fast with u64 sums, the apply pass tests the same deferral */
     uint32_t edges;       /* agnes_tally_edges: ev_counts / rec_out are the edge summary's (EDG) */
+    uint32_t ragged;      /* flow: the unaligned-stream kernel (U) runs after the aligned one, which
+                             leaves it the batches whose offsets are not all multiples of 4 */
     void* rec_out;        /* optional (agnes_tally_records): agnes_seg_event [n_votes], instance i's
                              records at [offsets[i], offsets[i] + ev_counts[i]) -- the flow
                              kernel writes them (REC); every other route's emit pass does */
@@ -104,7 +106,10 @@ bool agnes_sweep_supported(const agnes_tally_args* a);
 hipError_t agnes_launch_sweep(const agnes_tally_args* a, int num_cus, hipStream_t stream);
 /* the 8-votes-per-lane flow kernel (agnes_flow.hip) for the sweep route's streams */
 bool agnes_flow_supported(const agnes_tally_args* a);
-hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t stream);
+/* ragged_pass: the unaligned-stream variant, after the aligned kernel (bp: the batch
+ * partition the aligned launch chose: batch, tail batch, tail instances) */
+bool agnes_flow_ragged_ok(const agnes_tally_args* a);
+hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t stream, bool ragged_pass, uint32_t* bp);
 /* the segmented records (agnes_tally_records) of every instance, or of the ones on a
  * list (the flow route's walk list; list_n on the device), one lane per instance; and
  * the dense stream from them (offs: the exclusive scan of the counts) */
@@ -222,7 +227,11 @@ hipError_t agnes_launch_dedup_reject(const uint8_t* type_masked, uint64_t n, uin
 #define AGNES_QUEUE_N 256
 #define AGNES_WALK_COUNT (AGNES_QUEUE_N + 1)
 #define AGNES_WALK_QUEUE (AGNES_QUEUE_N + 2)
-#define AGNES_QUEUE_WORDS (AGNES_QUEUE_N + 4)
+/* the flow kernel's unaligned-stream variant: a flag the aligned kernel sets when it leaves
+ * it batches, then its own AGNES_QUEUE_N work-queue counters */
+#define AGNES_RAG_FLAG (AGNES_QUEUE_N + 3)
+#define AGNES_RAG_QUEUE (AGNES_QUEUE_N + 4)
+#define AGNES_QUEUE_WORDS (2 * AGNES_QUEUE_N + 8)
 #define AGNES_ERR_STRIPES 32
 #define AGNES_ERR_STRIDE 512
 #define AGNES_ERR_BYTES (AGNES_ERR_STRIPES * AGNES_ERR_STRIDE)

@@ -37,6 +37,7 @@ BYTES_PER_VOTE = 15            # 14 B canonical SoA in + 1 B code out (BASELINE.
 # algorithmic bytes per vote of each engine kernel (names: agnes_kernel_times)
 KERNEL_BYTES_PER_VOTE = {
     "flow": 15,          # instance, value, validator u32 + round, type u8 in; code u8 out
+    "flow_ragged": 15,   # the same, the unaligned-stream variant (round 6: c2r / c3r)
     "tally_fast": 15,
     "tally_wide": 15,
     "tally_list": 15,    # the i64 kernel over the instances the u32 kernels hand over (c2w: all)
@@ -54,11 +55,12 @@ C5_PASS_B_BYTES_PER_VOTE = 23
 # read and written once per step (64-B agnes_state in, 64 B out) by the kernel that
 # applies the events (flow on the fused route, apply_codes on the split one)
 STATE_BYTES_PER_INSTANCE = 128
-KERNEL_STATE_IO = {"flow", "apply_codes", "tally_list", "sweep_walk"}
+KERNEL_STATE_IO = {"flow", "flow_ragged", "apply_codes", "tally_list", "sweep_walk"}
 KERNEL_SYMBOLS = {
     # template parameters: PC (power table in LDS), SM (State machine), R1 (one round);
     # c2 runs flow<true, true, true>, c3 flow<false, true, false> (rocprofv3 names them)
     "flow": "agnes::flow::flow<PC, SM, R1>",
+    "flow_ragged": "agnes::flow::flow<PC, SM, R1, ..., U=true>",
     "sweep_walk": "agnes::sweep::sweep<PC, SM>",
     "tally_fast": "agnes::fast::tally_fast<...>",
     "tally_wide": "agnes::tally_kernel<true, ...>",

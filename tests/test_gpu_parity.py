@@ -634,6 +634,29 @@ def _round_states(n, R, seed):
     return st
 
 
+@pytest.mark.parametrize("lengths", [[8, 9, 10, 11, 12, 13, 14, 15, 17, 23],          # a start in most lanes
+                                     [0, 0, 8, 13, 31, 97, 150, 203, 299, 301, 411],  # C2/C3-like, empty ones
+                                     [9, 517, 1031, 2049]])                           # long, chunk-straddling
+@pytest.mark.parametrize("rounds", ["one", "runs", "mixed"])
+@pytest.mark.parametrize("flags", [0, abi.FLAG_STATE_MACHINE])
+def test_unaligned_streams(eng, lengths, rounds, flags):
+    """The flow kernel's unaligned-stream variant (round 6): instance offsets at every
+    residue, a lane's votes split at any position between two instances (or, in runs
+    mode, two rounds of one instance); instances of >= 8 votes.  'runs': each
+    instance's rounds in order (one tally pass per chunk, run starts anywhere);
+    'mixed': rounds in random order (a pass per round)."""
+    R = 1 if rounds == "one" else 4
+    hb = _ragged_batch(100 + len(lengths), 9000, 13, R, lengths)
+    if rounds == "runs":
+        hb = _reorder(hb, hb.round.astype(np.int64))
+    power = ol.gen_power(5, 7, 13, abi.POWER_UNIFORM, 1, 30)
+    st = _round_states(hb.n_instances, R, 9) if flags else None
+    g, o = run_both(eng, abi.config(abi.MODE_REFERENCE, flags, R), hb, power, None, st)
+    assert_same(g, o)
+    if flags:
+        assert g[1]["decided"].sum() > 0
+
+
 @pytest.mark.parametrize("order", ["increasing", "decreasing", "revisit", "unaligned"])
 def test_round_runs(eng, order):
     """The flow kernel tallies a chunk whose instances hold several rounds in one pass
