@@ -161,18 +161,22 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t x) { /* every lane active *
 }
 /* saddr forms: address = uniform 64-bit base + 32-bit lane offset; the vote
  * columns are read once (non-temporal) */
+/* (a stream's first or last chunk: the base goes through readfirstlane, so the "s" operand
+ * stays an SGPR pair whatever the compiler's uniformity analysis concludes about it) */
 __device__ __forceinline__ void sdma16(const void* base, uint32_t voff, uint32_t lds) {
     uint32_t keep;
+    const uint64_t b = rfl64((uint64_t)(uintptr_t)base);
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
-                 : "v"(voff), "s"(base), "s"(lds)
+                 : "v"(voff), "s"(b), "s"(lds)
                  : "memory");
 }
 __device__ __forceinline__ void sdma4(const void* base, uint32_t voff, uint32_t lds) {
     uint32_t keep;
+    const uint64_t b = rfl64((uint64_t)(uintptr_t)base);
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2 nt\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
-                 : "v"(voff), "s"(base), "s"(lds)
+                 : "v"(voff), "s"(b), "s"(lds)
                  : "memory");
 }
 /* a whole chunk: the five columns, each column's two 256-vote halves under ONE m0 (the
@@ -257,6 +261,9 @@ __device__ __attribute__((noinline)) uint32_t label_back(const uint32_t* inst_co
 #ifndef AGNES_FLOW_WPE
 #define AGNES_FLOW_WPE 3
 #endif
+#ifndef AGNES_FLOW_FORCE_U
+#define AGNES_FLOW_FORCE_U 0 /* A/B builds only: every stream to the unaligned-stream kernel (the aligned one not launched) */
+#endif
 #ifndef AGNES_FLOW_CODE_VMCNT
 #define AGNES_FLOW_CODE_VMCNT 1
 #endif
@@ -285,8 +292,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
     static_assert(!REC || (EVC && !W64), "records: with the record counts, u32 sums");
     static_assert(!EDG || (EVC && !W64 && !REC), "edges: the counts are the edges', u32 sums");
     static_assert(!U || (!W64 && !REC && !EDG), "unaligned streams: u32 sums, codes and record counts");
-    /* the unaligned kernel: nothing to do unless the aligned one left it batches */
-    if (U && *(volatile const uint32_t*)(a.list_count + AGNES_RAG_FLAG) == 0u) return;
+    /* the unaligned kernel: nothing to do unless the aligned one left it batches (any of its
+     * flags: 4 per lane) */
+    if (U && !AGNES_FLOW_FORCE_U) {
+        static_assert(AGNES_QUEUE_N == 256 && AGNES_RAG_FLAG % 4 == 0, "the flags: one uint4 per lane");
+        const uint4 f = reinterpret_cast<const uint4*>(a.list_count + AGNES_RAG_FLAG)[lane_id()];
+        if (!ballot((f.x | f.y | f.z | f.w) != 0u)) return;
+    }
     constexpr uint32_t RW = W64 ? RECW64 : RECW; /* record words */
 
     const uint32_t lane = lane_id();
@@ -377,8 +389,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
         const uint64_t oe = u64of(shfl(h.olo, lane + 1u), shfl(h.ohi, lane + 1u));
         const uint64_t len = il && oe > ob ? oe - ob : 0ull;
         h.ln = len < (1ull << 31) ? (uint32_t)len : (1u << 31);
+        /* rag: some offset off a multiple of 4 -- the U kernel's batch (with a.ragged), which
+         * checks the rest of it (U: 2 when an instance holds 1 .. 7 votes: the walk list) */
+        h.rag = (U && AGNES_FLOW_FORCE_U) || ballot(lane <= m && (h.olo & 3u) != 0u) != 0ull;
+        if (U) h.rag = h.rag ? 1u + (ballot(il && len > 0ull && len < 8ull) != 0ull) : 0u;
+        /* the other kernel's batch: no set constants, no stage 3 */
+        const bool other = U ? !h.rag : (h.rag && a.ragged);
         uint32_t q2 = 0, mp = 0, fa = 2, q2h = 0, mph = 0;
-        if (il && h.hs < ns) {
+        if (!other && il && h.hs < ns) {
             const agnes_set_info* const si = a.sets + h.hs;
             if (W64) {
                 q2 = (uint32_t)si->q2w;
@@ -397,14 +415,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
         h.q2h = q2h;
         h.mph = mph;
         h.fa = fa;
-        /* (the two kernels classify a batch alike: stream = the offsets and, at stage 3, the
-         * sets in the flow domain; rag = some offset off a multiple of 4) */
+        /* stream: the offsets and, at stage 3, the sets in the flow domain */
         const bool badl = lane < m && oe < ob;
         const uint64_t O0 = u64of(rdl(h.olo, 0u), rdl(h.ohi, 0u)), Om = u64of(rdl(h.olo, m), rdl(h.ohi, m));
-        h.stream = m > 0u && !ballot(badl) && Om - O0 < (1ull << 30);
-        h.rag = ballot(lane <= m && (h.olo & 3u) != 0u) != 0ull;
-        if (U) h.rag = h.rag ? 1u + (ballot(il && len > 0ull && len < 8ull) != 0ull) : 0u;
-        h.stage = 2;
+        h.stream = !other && m > 0u && !ballot(badl) && Om - O0 < (1ull << 30);
+        h.go = 0;
+        h.stage = other ? 3u : 2u;
     };
     auto hdr3 = [&](Hdr& h) { /* stage 3: quorum thresholds; a flow stream or the walk list */
         const uint32_t m = h.e0 - h.s0;
@@ -431,11 +447,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
         h.q2 = q2;
         h.stream = h.stream && !ballot(!fl);
         h.stage = 3;
-        /* which kernel walks it: the aligned one its aligned streams; with a.ragged the U one
-         * the others (U: those whose instances all hold 0 or >= 8 votes; rag 2 -> the walk list) */
+        /* this kernel walks it: the aligned one its aligned streams, the U one the others whose
+         * instances all hold 0 or >= 8 votes */
         h.go = U ? (h.stream && h.rag == 1u) : (h.stream && !h.rag);
     };
     uint32_t spar = 0; /* States staging buffer of the current batch */
+    bool rag_told = false; /* (the aligned kernel) its counter's flag for the U kernel is set */
     /* the last flush sent a whole chunk's codes as ONE store with every lane active and
      * no DMA has been issued since: the chunk top's wait may leave that store in flight */
     bool dc_one = false;
@@ -558,7 +575,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
        * (only for offsets that bound a stream inside the columns; hdr2 decides the rest) */
         const uint32_t m = H.e0 - H.s0;
         const uint64_t O0 = u64of(rdl(H.olo, 0u), rdl(H.ohi, 0u)), Om = u64of(rdl(H.olo, m), rdl(H.ohi, m));
-        if (Om > O0 && Om - O0 < (1ull << 30)) {
+        const bool ragb = (U && AGNES_FLOW_FORCE_U) || ballot(lane <= m && (H.olo & 3u) != 0u) != 0ull;
+        if (Om > O0 && Om - O0 < (1ull << 30) && (U ? ragb : !(ragb && a.ragged))) {
             const uint64_t Sa0 = O0 & ~127ull;
             dma_chunk(Sa0, (uint32_t)(O0 - Sa0), (uint32_t)(Om - Sa0));
             pf_at = Sa0;
@@ -583,8 +601,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
             /* the aligned kernel leaves the unaligned streams to the U kernel (a.ragged), which
              * leaves the aligned ones and the rest to the aligned kernel; the walk list
              * (agnes_sweep.hip) takes the batches that are no stream of either */
-            const bool walk = U ? (H.stream && H.rag == 2u) : (!H.stream || !a.ragged);
-            if (!U && !walk && lane == 0) a.list_count[AGNES_RAG_FLAG] = 1u; /* (a plain store: idempotent) */
+            const bool walk = U ? H.rag != 0u : (!H.rag || !a.ragged);
+            if (!U && !walk && !rag_told) { /* (a plain store, once per wave: idempotent) */
+                if (lane == 0) a.list_count[AGNES_RAG_FLAG + qk] = 1u;
+                rag_told = true;
+            }
             if (walk) {
                 uint32_t w0 = 0;
                 if (lane == 0) w0 = atomicAdd(a.list_count + AGNES_WALK_COUNT, m);
@@ -1995,6 +2016,7 @@ static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStrea
     const uint64_t cap = ncu * (uint64_t)o->per_cu;
     if (blocks > cap) blocks = cap;
     if (blocks == 0) blocks = 1;
+    if (!U && AGNES_FLOW_FORCE_U && b.ragged) return hipSuccess; /* (A/B builds: the partition only) */
     if (o->pc) hipLaunchKernelGGL((flow<true, SM, R1, EVC, W64, REC, EDG, U>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
     else hipLaunchKernelGGL((flow<false, SM, R1, EVC, W64, REC, EDG, U>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
     return hipGetLastError();

@@ -227,11 +227,12 @@ hipError_t agnes_launch_dedup_reject(const uint8_t* type_masked, uint64_t n, uin
 #define AGNES_QUEUE_N 256
 #define AGNES_WALK_COUNT (AGNES_QUEUE_N + 1)
 #define AGNES_WALK_QUEUE (AGNES_QUEUE_N + 2)
-/* the flow kernel's unaligned-stream variant: a flag the aligned kernel sets when it leaves
- * it batches, then its own AGNES_QUEUE_N work-queue counters */
-#define AGNES_RAG_FLAG (AGNES_QUEUE_N + 3)
-#define AGNES_RAG_QUEUE (AGNES_QUEUE_N + 4)
-#define AGNES_QUEUE_WORDS (2 * AGNES_QUEUE_N + 8)
+/* the flow kernel's unaligned-stream variant: AGNES_QUEUE_N flags the aligned kernel sets
+ * when it leaves it batches (one per work-queue counter, set once per wave: thousands of
+ * stores to one word serialise), then its own AGNES_QUEUE_N work-queue counters */
+#define AGNES_RAG_FLAG (AGNES_QUEUE_N + 4)
+#define AGNES_RAG_QUEUE (2 * AGNES_QUEUE_N + 4)
+#define AGNES_QUEUE_WORDS (3 * AGNES_QUEUE_N + 8)
 #define AGNES_ERR_STRIPES 32
 #define AGNES_ERR_STRIDE 512
 #define AGNES_ERR_BYTES (AGNES_ERR_STRIPES * AGNES_ERR_STRIDE)
