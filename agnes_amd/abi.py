@@ -11,7 +11,7 @@ import numpy as np
 ABI_VERSION = 8
 NIL = 0xFFFFFFFF
 
-OK, E_INVALID, E_UNSUPPORTED, E_DEVICE, E_NOMEM, E_NODEVICE = 0, -1, -2, -3, -4, -5
+OK, E_INVALID, E_UNSUPPORTED, E_DEVICE, E_NOMEM, E_NODEVICE, E_OVERFLOW = 0, -1, -2, -3, -4, -5, -6
 
 PREVOTE, PRECOMMIT = 0, 1
 THRESH_INIT, THRESH_ANY, THRESH_NIL, THRESH_VALUE = 0, 1, 2, 3

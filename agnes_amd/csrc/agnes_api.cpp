@@ -41,6 +41,7 @@ struct agnes_ctx {
     void* d_dd = nullptr;       /* agnes_dedup_first: bucket counts, scan scratch, (key, index) pairs */
     uint64_t dd_cap = 0;
     int32_t* d_edtab = nullptr; /* Ed25519 fixed-base table (agnes_wire_ingest), built on first use */
+    unsigned long long* d_ovf = nullptr; /* records the dense writers dropped since agnes_records_overflow */
 };
 
 namespace {
@@ -231,6 +232,13 @@ int agnes_ctx_create(int device, agnes_ctx** out) {
         return status_of(e);
     }
     (void)hipMemset(c->d_err, 0, AGNES_COUNTER_BYTES);
+    e = hipMalloc(&c->d_ovf, sizeof(unsigned long long));
+    if (e != hipSuccess) {
+        (void)hipFree(c->d_err);
+        delete c;
+        return status_of(e);
+    }
+    (void)hipMemset(c->d_ovf, 0, sizeof(unsigned long long));
     *out = c;
     return AGNES_OK;
 }
@@ -244,6 +252,7 @@ void agnes_ctx_destroy(agnes_ctx* c) {
     if (c->d_scan) (void)hipFree(c->d_scan);
     if (c->d_dd) (void)hipFree(c->d_dd);
     if (c->d_edtab) (void)hipFree(c->d_edtab);
+    if (c->d_ovf) (void)hipFree(c->d_ovf);
     if (c->order_ev) (void)hipEventDestroy(c->order_ev);
     delete c;
 }
@@ -634,12 +643,23 @@ int agnes_edge_offsets(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_b
 }
 
 int agnes_edges(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, const uint8_t* codes,
-                const uint64_t* offsets, agnes_edge* out, void* stream) {
+                const uint64_t* offsets, agnes_edge* out, uint64_t out_cap, void* stream) {
     if (!c || !offsets || !out || !edges_args_ok(cfg, b, codes) || ((uintptr_t)out & 15u)) return AGNES_E_INVALID;
     AGNES_TRY(hipSetDevice(c->device));
     AGNES_ORDER(c, (hipStream_t)stream);
     return status_of(agnes_launch_edges(b, codes, cfg->max_rounds, const_cast<uint64_t*>(offsets), out,
-                                        nullptr, (hipStream_t)stream));
+                                        nullptr, (hipStream_t)stream, out_cap, c->d_ovf));
+}
+
+int agnes_records_overflow(agnes_ctx* c, uint64_t* dropped) {
+    if (!c || !dropped) return AGNES_E_INVALID;
+    AGNES_TRY(hipSetDevice(c->device));
+    AGNES_TRY(hipStreamSynchronize(c->last_stream));
+    unsigned long long v = 0;
+    AGNES_TRY(hipMemcpy(&v, c->d_ovf, sizeof(v), hipMemcpyDeviceToHost));
+    if (v) AGNES_TRY(hipMemset(c->d_ovf, 0, sizeof(v)));
+    *dropped = v;
+    return v ? AGNES_E_OVERFLOW : AGNES_OK;
 }
 
 /* ---------------- C5: the fold of one instance's slices ---------------- */
@@ -712,7 +732,9 @@ int agnes_tally_events(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_b
     } else {
         AGNES_TRY(agnes_launch_events(b, codes, cfg->max_rounds, offsets, nullptr, c->d_scan, st));
     }
-    return status_of(agnes_launch_events(b, codes, cfg->max_rounds, offsets, out, nullptr, st));
+    /* out holds agnes_events_capacity() records (the contract): the emit never writes past it */
+    return status_of(agnes_launch_events(b, codes, cfg->max_rounds, offsets, out, nullptr, st,
+                                         agnes_events_capacity(cfg, b), c->d_ovf));
 }
 
 static_assert(sizeof(agnes_seg_event) == 16, "agnes_seg_event is one 16-B record");
@@ -764,7 +786,7 @@ int agnes_tally_edges(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
 }
 
 int agnes_edges_compact(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, const uint64_t* counts,
-                        const agnes_edge* seg, uint64_t* offsets, agnes_edge* out, void* stream) {
+                        const agnes_edge* seg, uint64_t* offsets, agnes_edge* out, uint64_t out_cap, void* stream) {
     if (!c || !cfg_ok(cfg) || !b || !b->offsets || !offsets || (b->n_instances && (!counts || !seg)) ||
         ((uintptr_t)out & 15u) || ((uintptr_t)seg & 15u))
         return AGNES_E_INVALID;
@@ -788,11 +810,12 @@ int agnes_edges_compact(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_
         AGNES_TRY(agnes_launch_offsets_scan(offsets, b->n_instances, c->d_scan, st));
     }
     if (!out) return AGNES_OK;
-    return status_of(agnes_launch_edge_compact(b, seg, offsets, out, st));
+    return status_of(agnes_launch_edge_compact(b, seg, offsets, out, st, out_cap, c->d_ovf));
 }
 
 int agnes_records_compact(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, const uint64_t* counts,
-                          const agnes_seg_event* seg, uint64_t* offsets, agnes_vote_event* out, void* stream) {
+                          const agnes_seg_event* seg, uint64_t* offsets, agnes_vote_event* out, uint64_t out_cap,
+                          void* stream) {
     if (!c || !cfg_ok(cfg) || !b || !b->offsets || !offsets || (b->n_instances && (!counts || !seg)) ||
         ((uintptr_t)out & 7u) || ((uintptr_t)seg & 15u))
         return AGNES_E_INVALID;
@@ -817,18 +840,18 @@ int agnes_records_compact(agnes_ctx* c, const agnes_config* cfg, const agnes_vot
     }
     if (!out) return AGNES_OK; /* the offsets only (the caller sizes out from offsets[n]) */
     const uint32_t mult = (cfg->flags & AGNES_FLAG_ROUND_SKIP) ? 2u : 1u;
-    return status_of(agnes_launch_seg_compact(b, mult, seg, offsets, out, st));
+    return status_of(agnes_launch_seg_compact(b, mult, seg, offsets, out, st, out_cap, c->d_ovf));
 }
 
 int agnes_events(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b, const uint8_t* codes,
-                 const uint64_t* offsets, agnes_vote_event* out, void* stream) {
+                 const uint64_t* offsets, agnes_vote_event* out, uint64_t out_cap, void* stream) {
     if (!c || !offsets || !out || !edges_args_ok(cfg, b, codes) || ((uintptr_t)out & 7u)) return AGNES_E_INVALID;
     if (cfg->max_rounds > 64u) return AGNES_E_UNSUPPORTED; /* the value slots of a lane's executors in LDS */
     if (b->n_votes && (!b->value || ((uintptr_t)b->value & 3u))) return AGNES_E_INVALID;
     AGNES_TRY(hipSetDevice(c->device));
     AGNES_ORDER(c, (hipStream_t)stream);
     return status_of(agnes_launch_events(b, codes, cfg->max_rounds, const_cast<uint64_t*>(offsets), out,
-                                         nullptr, (hipStream_t)stream));
+                                         nullptr, (hipStream_t)stream, out_cap, c->d_ovf));
 }
 
 /* ---------------- DEDUP for a split instance ---------------- */

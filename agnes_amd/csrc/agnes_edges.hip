@@ -36,6 +36,10 @@ struct EdgeArgs {
     agnes_edge* out;
     uint32_t keys;    /* 2 * max_rounds */
     uint32_t nslots;  /* ceil(keys / 4) byte words per lane */
+    /* (the dense emit) out holds cap records; an edge past cap or past its instance's end
+     * offset is dropped and counted in *ovf (agnes_records_overflow) */
+    uint64_t cap;
+    unsigned long long* ovf;
 };
 
 template <uint32_t W>
@@ -65,7 +69,8 @@ __device__ __forceinline__ void load_win(const uint8_t* col, uint64_t w, uint64_
  * is then a 64-bit shift and xor, not an LDS round trip the next vote of the same
  * executor waits on */
 template <bool EMIT, uint32_t W, bool REG>
-__device__ __forceinline__ uint64_t walk_one(const EdgeArgs& a, uint32_t i, uint32_t lane, uint64_t base) {
+__device__ __forceinline__ uint64_t walk_one(const EdgeArgs& a, uint32_t i, uint32_t lane, uint64_t base,
+                                             uint64_t lim = ~0ull) {
     uint32_t* const tab = reinterpret_cast<uint32_t*>(agnes_smem);
     uint64_t st = 0; /* (REG) VoteCount::new: level 0 */
     if (!REG)
@@ -99,7 +104,7 @@ __device__ __forceinline__ uint64_t walk_one(const EdgeArgs& a, uint32_t i, uint
             const uint32_t msg = cb >> AGNES_CODE_MSG_SHIFT;
             const uint32_t nb = (cb & 0xFu) | (msg ? msg << AGNES_CODE_MSG_SHIFT : old & 0xF0u);
             if (nb != old) {
-                if (EMIT) {
+                if (EMIT && base + cnt < lim) {
                     const uint32_t tail = rb | (tb << 8) | (cb << 16) | (old << 24);
                     *reinterpret_cast<uint4*>(a.out + base + cnt) =
                         make_uint4((uint32_t)j, (uint32_t)(j >> 32), i, tail);
@@ -118,8 +123,14 @@ __global__ __launch_bounds__(64) void edge_walk(EdgeArgs a) {
     const uint32_t lane = threadIdx.x;
     const uint32_t i = blockIdx.x * 64u + lane;
     if (i >= a.vb.n_instances) return;
-    if (EMIT) walk_one<true, W, REG>(a, i, lane, a.offs[i]);
-    else a.offs[i + 1u] = walk_one<false, W, REG>(a, i, lane, 0u);
+    if (EMIT) { /* (the count that did not fit below lim: dropped) */
+        const uint64_t o = a.offs[i], lim = min(a.offs[i + 1u], a.cap);
+        const uint64_t cnt = walk_one<true, W, REG>(a, i, lane, o, lim);
+        const uint64_t kept = o >= lim ? 0u : (cnt < lim - o ? cnt : lim - o);
+        if (kept < cnt) atomicAdd(a.ovf, (unsigned long long)(cnt - kept));
+    } else {
+        a.offs[i + 1u] = walk_one<false, W, REG>(a, i, lane, 0u);
+    }
 }
 
 /* the segmented edges (agnes_tally_edges) of every instance, or of the ones on a list
@@ -148,15 +159,21 @@ __global__ __launch_bounds__(64) void edge_seg_walk(EdgeArgs a, const uint32_t* 
  * that instance's segment and one 16-B store (a few edges per instance: one instance
  * per step left most lanes idle) */
 __global__ __launch_bounds__(256) void edge_compact(agnes_vote_batch vb, const agnes_edge* seg, const uint64_t* offs,
-                                                    agnes_edge* out) {
+                                                    agnes_edge* out, uint64_t cap, unsigned long long* ovf) {
     const uint32_t lane = threadIdx.x & 63u, w = blockIdx.x * 4u + (threadIdx.x >> 6);
     const uint32_t n = vb.n_instances, i0 = 32u * w;
     if (i0 >= n) return; /* wave-uniform */
     const uint32_t m = n - i0 < 32u ? n - i0 : 32u;
-    const uint64_t base = offs[i0], total = offs[i0 + m] - base;
+    /* the wave's range bounded by out's capacity (the edges past cap dropped, counted) */
+    const uint64_t base = offs[i0], end = offs[i0 + m];
+    const uint64_t tot = end > base ? end - base : 0u;
+    const uint64_t total = base >= cap ? 0u : (tot < cap - base ? tot : cap - base);
+    if (lane == 0u && total < tot) atomicAdd(ovf, (unsigned long long)(tot - total));
     if (total > 0xFFFFFF00ull) { /* positions past u32 (4e9 edges in 32 instances): per instance */
         for (uint32_t i = i0; i < i0 + m; ++i) {
-            const uint64_t o = offs[i], cnt = offs[i + 1u] - o;
+            const uint64_t o = offs[i], oe = offs[i + 1u] < base + total ? offs[i + 1u] : base + total;
+            if (o >= oe) continue;
+            const uint64_t cnt = oe - o;
             const uint4* const s = reinterpret_cast<const uint4*>(seg + vb.offsets[i]);
             for (uint64_t k = lane; k < cnt; k += 64u) reinterpret_cast<uint4*>(out + o)[k] = s[k];
         }
@@ -272,10 +289,11 @@ uint64_t agnes_edges_scratch_words(uint32_t n_instances) {
 }
 
 hipError_t agnes_launch_edges(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds,
-                              uint64_t* offs, agnes_edge* out, uint64_t* scratch, hipStream_t st) {
+                              uint64_t* offs, agnes_edge* out, uint64_t* scratch, hipStream_t st, uint64_t cap,
+                              unsigned long long* ovf) {
     using namespace agnes::edges;
     const uint32_t n = vb->n_instances;
-    EdgeArgs a{*vb, codes, offs, out, 2u * max_rounds, (2u * max_rounds + 3u) / 4u};
+    EdgeArgs a{*vb, codes, offs, out, 2u * max_rounds, (2u * max_rounds + 3u) / 4u, cap, ovf};
     /* 16-B windows when the three columns allow them */
     const bool w16 = ((reinterpret_cast<uintptr_t>(codes) | reinterpret_cast<uintptr_t>(vb->round) |
                        reinterpret_cast<uintptr_t>(vb->type)) & 15u) == 0u;
@@ -336,11 +354,11 @@ hipError_t agnes_launch_edge_seg_walk(const agnes_vote_batch* vb, const uint8_t*
 }
 
 hipError_t agnes_launch_edge_compact(const agnes_vote_batch* vb, const agnes_edge* seg, const uint64_t* offs,
-                                     agnes_edge* out, hipStream_t st) {
+                                     agnes_edge* out, hipStream_t st, uint64_t cap, unsigned long long* ovf) {
     const uint32_t n = vb->n_instances;
     if (n == 0) return hipSuccess;
     const uint32_t waves = (n + 31u) / 32u, blocks = (waves + 3u) / 4u;
     AgnesKt kt("edge_compact", st);
-    hipLaunchKernelGGL(agnes::edges::edge_compact, dim3(blocks), dim3(256), 0, st, *vb, seg, offs, out);
+    hipLaunchKernelGGL(agnes::edges::edge_compact, dim3(blocks), dim3(256), 0, st, *vb, seg, offs, out, cap, ovf);
     return hipGetLastError();
 }

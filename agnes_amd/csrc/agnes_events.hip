@@ -47,7 +47,23 @@ struct EvArgs {
     uint4* seg;
     uint64_t* counts;
     uint32_t mult;
+    /* the dense writers: out holds cap records; a record whose position is past cap, or
+     * past its instance's (or batch's) end offset, is dropped and counted in *ovf
+     * (agnes_records_overflow) -- offsets that disagree with the codes, or an undersized
+     * out, never write outside out */
+    uint64_t cap;
+    unsigned long long* ovf;
 };
+
+/* a dense record at position d, bounded by lim (min of cap and the segment's end) */
+__device__ __forceinline__ bool in_cap(uint64_t d, uint64_t lim, uint32_t& drop) {
+    const bool ok = d < lim;
+    drop += ok ? 0u : 1u;
+    return ok;
+}
+__device__ __forceinline__ void flush_drops(const unsigned long long* ovf, uint32_t drop) {
+    if (drop) atomicAdd(const_cast<unsigned long long*>(ovf), (unsigned long long)drop);
+}
 
 /* W consecutive bytes of a u8 column from w (W = 4: one dword; W >= 16: 16-B loads
  * of one line in flight together); past n_votes: zeros */
@@ -155,6 +171,8 @@ __global__ __launch_bounds__(64) void event_walk(EvArgs a) {
     lo = lo < NV ? lo : NV;
     hi = hi < NV ? hi : NV;
     const uint64_t base = EMIT ? a.offs[i] : 0u;
+    const uint64_t lim = EMIT ? min(a.offs[i + 1u], a.cap) : 0u;
+    uint32_t drop = 0;
     uint64_t cnt = 0;
     for (uint64_t w = lo & ~(uint64_t)(W - 1u); w < hi; w += W) {
         uint32_t c[W / 4u];
@@ -179,13 +197,16 @@ __global__ __launch_bounds__(64) void event_walk(EvArgs a) {
             uint32_t* const p = lab + key * 64u + lane;
             if (v[b] != AGNES_NIL) *p = v[b]; /* the value slot, last writer wins */
             const uint32_t msg = cb >> AGNES_CODE_MSG_SHIFT;
-            if (skip) put(a.out + base + cnt++, j, i, AGNES_NIL, rb, AGNES_EV_ROUND_SKIP, msg);
+            if (skip && in_cap(base + cnt, lim, drop)) put(a.out + base + cnt, j, i, AGNES_NIL, rb, AGNES_EV_ROUND_SKIP, msg);
+            cnt += skip;
             if (has) {
                 const bool val = ev == AGNES_CODE_POLKA_VALUE || ev == AGNES_CODE_PRECOMMIT_VALUE;
-                put(a.out + base + cnt++, j, i, val ? *p : AGNES_NIL, rb, kind_of(ev), msg);
+                if (in_cap(base + cnt, lim, drop)) put(a.out + base + cnt, j, i, val ? *p : AGNES_NIL, rb, kind_of(ev), msg);
+                ++cnt;
             }
         }
     }
+    flush_drops(a.ovf, drop);
 }
 
 /* ---- the segmented records (agnes_tally_records) ------------------------------------
@@ -254,16 +275,24 @@ __global__ __launch_bounds__(64) void seg_walk(EvArgs a, const uint32_t* list, c
  * to the range's start), then one 16-B read of that instance's segment.  Every lane
  * has a record in every step but the last (one instance per step left lanes idle) */
 __global__ __launch_bounds__(256) void seg_compact(agnes_vote_batch vb, uint32_t mult, const uint4* seg,
-                                                   const uint64_t* offs, agnes_vote_event* out) {
+                                                   const uint64_t* offs, agnes_vote_event* out, uint64_t cap,
+                                                   unsigned long long* ovf) {
     const uint32_t lane = threadIdx.x & 63u, w = blockIdx.x * 4u + (threadIdx.x >> 6);
     const uint32_t n = vb.n_instances, i0 = 32u * w;
     if (i0 >= n) return; /* wave-uniform */
     const uint32_t m = n - i0 < 32u ? n - i0 : 32u;
     uint2* const stage = reinterpret_cast<uint2*>(agnes_smem) + (threadIdx.x >> 6) * 192u; /* 1.5 KB per wave */
-    const uint64_t base = offs[i0], total = offs[i0 + m] - base;
+    /* the wave's range, bounded by out's capacity (offsets scanned from counts that are
+     * not the segments', or an undersized out: the records past cap are dropped, counted) */
+    const uint64_t base = offs[i0], end = offs[i0 + m];
+    const uint64_t total = end > base ? end - base : 0u;
+    const uint64_t keep = base >= cap ? 0u : (total < cap - base ? total : cap - base);
+    if (lane == 0u && keep < total) atomicAdd(ovf, (unsigned long long)(total - keep));
     if (total > 0xFFFFFF00ull) { /* positions past u32 (4e9 records in 32 instances): per instance */
         for (uint32_t i = i0; i < i0 + m; ++i) {
-            const uint64_t o = offs[i], cnt = offs[i + 1u] - o;
+            const uint64_t o = offs[i], oe = offs[i + 1u];
+            if (o >= base + keep) break;
+            const uint64_t cnt = (oe < base + keep ? oe : base + keep) > o ? (oe < base + keep ? oe : base + keep) - o : 0u;
             const uint4* const src = seg + (uint64_t)mult * vb.offsets[i];
             for (uint64_t k = lane; k < cnt; k += 64u) {
                 const uint4 r = src[k];
@@ -278,7 +307,7 @@ __global__ __launch_bounds__(256) void seg_compact(agnes_vote_batch vb, uint32_t
     /* lane k < m: instance i0 + k's first dense position (relative) and its segment */
     const uint32_t rk = lane < m ? (uint32_t)(offs[i0 + lane] - base) : 0xFFFFFFFFu;
     const uint64_t sk = lane < m ? (uint64_t)mult * vb.offsets[i0 + lane] : 0ull;
-    for (uint64_t p0 = 0; p0 < total; p0 += 64u) {
+    for (uint64_t p0 = 0; p0 < keep; p0 += 64u) {
         const uint32_t p = (uint32_t)p0 + lane;
         uint32_t k = 0; /* the last instance starting at or before p */
 #pragma unroll
@@ -293,7 +322,7 @@ __global__ __launch_bounds__(256) void seg_compact(agnes_vote_batch vb, uint32_t
         /* the step's 64 records staged in LDS as 24-B records, then out as three
          * contiguous 512-B runs of 8-B words (the lanes' own 24-B records would be
          * three stores strided by 24 B) */
-        const uint32_t nrec = total - p0 < 64u ? (uint32_t)(total - p0) : 64u;
+        const uint32_t nrec = keep - p0 < 64u ? (uint32_t)(keep - p0) : 64u;
         if (lane < nrec) {
             const uint4 r = seg[(((uint64_t)shi << 32) | slo) + (p - rkk)];
             stage[3u * lane] = make_uint2(r.x, r.y);
@@ -382,6 +411,8 @@ __global__ __launch_bounds__(256) void event_emit_wave(EvArgs a) {
     Pass cur;
     load_pass(a, w + 4u * lane, NV, cur);
     uint64_t cnt = a.offs[i];
+    uint64_t lim = min(a.offs[i + 1u], a.cap); /* the instance's records end there */
+    uint32_t drop = 0;
     bool fresh = true;
     for (;;) {
         if (fresh) { /* VoteCount::new for every key: Value{} */
@@ -391,13 +422,14 @@ __global__ __launch_bounds__(256) void event_emit_wave(EvArgs a) {
         }
         /* the next pass: this instance's, or the first of the wave's next instance */
         uint32_t ni = i;
-        uint64_t nw = w + 256u, nlo = lo, nhi = hi, ncnt = 0;
+        uint64_t nw = w + 256u, nlo = lo, nhi = hi, ncnt = 0, nlim = 0;
         if (nw >= hi) {
             ni = i + W;
             if (ni < n) {
                 bounds(ni, nlo, nhi);
                 nw = nlo & ~3ull;
                 ncnt = a.offs[ni];
+                nlim = min(a.offs[ni + 1u], a.cap);
             }
         }
         Pass nxt;
@@ -471,10 +503,12 @@ __global__ __launch_bounds__(256) void event_emit_wave(EvArgs a) {
                     const uint32_t cb = (cur.c4 >> (8u * s)) & 0xFFu, ev = cb & AGNES_CODE_EVENT_MASK;
                     const uint32_t rb = (cur.r4 >> (8u * s)) & 0xFFu, msg = cb >> AGNES_CODE_MSG_SHIFT;
                     const uint64_t j = j0 + s;
-                    if (two & 1u) put(a.out + o++, j, i, AGNES_NIL, rb, AGNES_EV_ROUND_SKIP, msg);
+                    if ((two & 1u) && in_cap(o, lim, drop)) put(a.out + o, j, i, AGNES_NIL, rb, AGNES_EV_ROUND_SKIP, msg);
+                    o += two & 1u;
                     if (two & 2u) {
                         const bool val = ev == AGNES_CODE_POLKA_VALUE || ev == AGNES_CODE_PRECOMMIT_VALUE;
-                        put(a.out + o++, j, i, val ? slot[s] : AGNES_NIL, rb, kind_of(ev), msg);
+                        if (in_cap(o, lim, drop)) put(a.out + o, j, i, val ? slot[s] : AGNES_NIL, rb, kind_of(ev), msg);
+                        ++o;
                     }
                 }
             }
@@ -486,11 +520,13 @@ __global__ __launch_bounds__(256) void event_emit_wave(EvArgs a) {
             lo = nlo;
             hi = nhi;
             cnt = ncnt;
+            lim = nlim;
             fresh = true;
         }
         w = nw;
         cur = nxt;
     }
+    flush_drops(a.ovf, drop);
 }
 
 /* ---- the batch-stream emit (aligned columns): a wave walks a batch of up to EB
@@ -646,6 +682,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     EvRaw NR = nb < NB ? ev_load(a, nb, lane) : EvRaw{0u, 0u};
     uint64_t ncnt = (!SEG && nb < NB) ? a.offs[nb * EB] : 0u;
     uint64_t cnt = SEG ? 0u : a.offs[B.s0]; /* the batch's first record (SEG: batch-relative) */
+    /* (dense) the batch's records end at offs[its end], and out holds cap of them */
+    uint64_t lim = SEG ? 0u : min(a.offs[B.s0 + B.m], a.cap);
+    uint64_t nlim = (!SEG && nb < NB) ? min(a.offs[min(nb * EB + EB, n)], a.cap) : 0u;
+    uint32_t drop = 0;
     uint64_t c = B.O0 & ~(uint64_t)(V - 1u);
     PassV<V> cur;
     load_pass_v<V>(a, c + V * lane, NV, cur);
@@ -863,6 +903,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
              * stores (a record is 3 of them), or straight out when the pass has more than
              * the area holds */
             const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+            /* (dense) the pass's records that fit below lim; the rest dropped and counted */
+            const uint32_t fit = SEG ? total : (cnt >= lim ? 0u : (lim - cnt < total ? (uint32_t)(lim - cnt) : total));
+            if (!SEG && fit < total && lane == 0u) drop += total - fit;
             const bool staged = !SEG && total <= EV_STAGE;
             auto emit = [&](agnes_vote_event* dst) {
                 uint32_t o = incl - n_rec;
@@ -874,10 +917,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                         const uint32_t rb = byte_at(cur.r4, s), msg = cb >> AGNES_CODE_MSG_SHIFT;
                         const uint64_t j = c + p0 + s;
                         const uint32_t inst = B.s0 + kk[s];
-                        if (two & 1u) put(dst + o++, j, inst, AGNES_NIL, rb, AGNES_EV_ROUND_SKIP, msg);
+                        if ((two & 1u) && o < fit) put(dst + o, j, inst, AGNES_NIL, rb, AGNES_EV_ROUND_SKIP, msg);
+                        o += two & 1u;
                         if (two & 2u) {
                             const bool val = ev == AGNES_CODE_POLKA_VALUE || ev == AGNES_CODE_PRECOMMIT_VALUE;
-                            put(dst + o++, j, inst, val ? slot[s] : AGNES_NIL, rb, kind_of(ev), msg);
+                            if (o < fit) put(dst + o, j, inst, val ? slot[s] : AGNES_NIL, rb, kind_of(ev), msg);
+                            ++o;
                         }
                     }
                 }
@@ -907,7 +952,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             if (staged) {
                 __builtin_amdgcn_wave_barrier();
                 uint2* const out8 = reinterpret_cast<uint2*>(a.out + cnt);
-                for (uint32_t w8 = lane; w8 < 3u * total; w8 += 64u) out8[w8] = reinterpret_cast<const uint2*>(stage)[w8];
+                for (uint32_t w8 = lane; w8 < 3u * fit; w8 += 64u) out8[w8] = reinterpret_cast<const uint2*>(stage)[w8];
                 __builtin_amdgcn_wave_barrier();
             }
             cnt += total;
@@ -918,10 +963,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             b = nb;
             B = NBt;
             cnt = ncnt;
+            lim = nlim;
             nb = b + BS;
             if (nb < NB) {
                 NR = ev_load(a, nb, lane);
                 ncnt = SEG ? 0u : a.offs[nb * EB];
+                nlim = SEG ? 0u : min(a.offs[min(nb * EB + EB, n)], a.cap);
             }
             __builtin_amdgcn_wave_barrier();
             for (uint32_t k = lane; k < EB * keys; k += 64u) lab[k] = 0u;
@@ -931,6 +978,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         c = nc;
         cur = nxt;
     }
+    if (!SEG) flush_drops(a.ovf, drop); /* (lane 0 counted the wave's) */
 }
 
 } // namespace events
@@ -958,10 +1006,11 @@ hipError_t agnes_launch_event_count_list(const agnes_vote_batch* vb, const uint8
 }
 
 hipError_t agnes_launch_events(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds,
-                               uint64_t* offs, agnes_vote_event* out, uint64_t* scratch, hipStream_t st) {
+                               uint64_t* offs, agnes_vote_event* out, uint64_t* scratch, hipStream_t st, uint64_t cap,
+                               unsigned long long* ovf) {
     using namespace agnes::events;
     const uint32_t n = vb->n_instances;
-    EvArgs a{*vb, codes, offs, out, 2u * max_rounds};
+    EvArgs a{*vb, codes, offs, out, 2u * max_rounds, nullptr, nullptr, 0u, cap, ovf};
     const dim3 grid((n + 63u) / 64u), blk(64);
     if (!out) { /* pass 1: counts (codes only), then the scan */
         hipError_t e = hipMemsetAsync(offs, 0, sizeof(uint64_t), st);
@@ -1060,12 +1109,12 @@ hipError_t agnes_launch_seg_walk(const agnes_vote_batch* vb, const uint8_t* code
 }
 
 hipError_t agnes_launch_seg_compact(const agnes_vote_batch* vb, uint32_t mult, const void* seg, const uint64_t* offs,
-                                    agnes_vote_event* out, hipStream_t st) {
+                                    agnes_vote_event* out, hipStream_t st, uint64_t cap, unsigned long long* ovf) {
     const uint32_t n = vb->n_instances;
     if (n == 0) return hipSuccess;
     const uint32_t waves = (n + 31u) / 32u, blocks = (waves + 3u) / 4u;
     AgnesKt kt("seg_compact", st);
     hipLaunchKernelGGL(agnes::events::seg_compact, dim3(blocks), dim3(256), 4u * 192u * sizeof(uint2), st, *vb, mult,
-                       reinterpret_cast<const uint4*>(seg), offs, out);
+                       reinterpret_cast<const uint4*>(seg), offs, out, cap, ovf);
     return hipGetLastError();
 }

@@ -122,14 +122,16 @@ hipError_t agnes_launch_seg_emit(const agnes_vote_batch* vb, const uint8_t* code
 hipError_t agnes_launch_seg_walk(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds, uint32_t mult,
                                  const uint32_t* list, const uint32_t* list_n, uint64_t* counts, void* seg,
                                  hipStream_t stream);
+/* (the dense writers: out holds cap records; the ones past cap or past their segment's end
+ * offset are dropped and counted in *ovf -- agnes_records_overflow) */
 hipError_t agnes_launch_seg_compact(const agnes_vote_batch* vb, uint32_t mult, const void* seg, const uint64_t* offs,
-                                    agnes_vote_event* out, hipStream_t stream);
+                                    agnes_vote_event* out, hipStream_t stream, uint64_t cap, unsigned long long* ovf);
 /* the same for the edge summary (agnes_tally_edges / agnes_edges_compact) */
 hipError_t agnes_launch_edge_seg_walk(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds,
                                       const uint32_t* list, const uint32_t* list_n, uint64_t* counts, agnes_edge* seg,
                                       hipStream_t stream);
 hipError_t agnes_launch_edge_compact(const agnes_vote_batch* vb, const agnes_edge* seg, const uint64_t* offs,
-                                     agnes_edge* out, hipStream_t stream);
+                                     agnes_edge* out, hipStream_t stream, uint64_t cap, unsigned long long* ovf);
 /* the flow kernel can count event records (agnes_tally_events) in this configuration */
 bool agnes_flow_counts_events(uint32_t flags, uint32_t max_rounds, bool edges = false);
 /* the batched State::apply pass over the codes a tally kernel left (agnes_apply.hip):
@@ -189,13 +191,15 @@ hipError_t agnes_launch_partials(const agnes_vote_batch* vb, const int64_t* powe
                                  uint32_t max_rounds, uint32_t one_inst, uint32_t one_id, agnes_carry_rec* counts,
                                  int64_t* weights, hipStream_t st);
 hipError_t agnes_launch_events(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds,
-                               uint64_t* offs, agnes_vote_event* out, uint64_t* scratch, hipStream_t stream);
+                               uint64_t* offs, agnes_vote_event* out, uint64_t* scratch, hipStream_t stream,
+                               uint64_t cap = 0, unsigned long long* ovf = nullptr);
 /* the event-record counts of the instances on a tally's walk list (walk[0 .. *walk_n)),
  * into offs[1 + instance]: the ones the flow kernel did not count */
 hipError_t agnes_launch_event_count_list(const agnes_vote_batch* vb, const uint8_t* codes, const uint32_t* walk,
                                          const uint32_t* walk_n, uint64_t* offs, int num_cus, hipStream_t stream);
 hipError_t agnes_launch_edges(const agnes_vote_batch* vb, const uint8_t* codes, uint32_t max_rounds,
-                              uint64_t* offs, agnes_edge* out, uint64_t* scratch, hipStream_t stream);
+                              uint64_t* offs, agnes_edge* out, uint64_t* scratch, hipStream_t stream,
+                              uint64_t cap = 0, unsigned long long* ovf = nullptr);
 
 /* DEDUP for a split instance (agnes_dedup.hip): type_out == nullptr -> the first-seen
  * pass into first[], else the mask pass; reject rewrites the masked votes' codes */

@@ -850,7 +850,7 @@ int agnes_multi_edges(agnes_multi* m, const agnes_config* cfg, const uint64_t* o
             agnes_edge* dout = nullptr;
             if (r == AGNES_OK && ne && hipMalloc(&dout, sizeof(agnes_edge) * ne) != hipSuccess) r = AGNES_E_NOMEM;
             const agnes_vote_batch db = range_batch(m, k, nv);
-            if (r == AGNES_OK && ne) r = agnes_edges(d.ctx, cfg, &db, d.b.codes, d.eoff, dout, d.st);
+            if (r == AGNES_OK && ne) r = agnes_edges(d.ctx, cfg, &db, d.b.codes, d.eoff, dout, ne, d.st);
             if (r == AGNES_OK && ne &&
                 hipMemcpyAsync(out + at, dout, sizeof(agnes_edge) * ne, hipMemcpyDeviceToHost, d.st) != hipSuccess)
                 r = AGNES_E_DEVICE;

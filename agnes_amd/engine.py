@@ -203,7 +203,8 @@ class Engine:
             out = torch.empty((max(self.events_capacity(cfg, batch), 1), 24), dtype=torch.uint8, device=self.device)
         b = batch.c()
         check(self.lib.agnes_records_compact(self.ctx, C.byref(cfg), C.byref(b), _ptr(counts), _ptr(seg),
-                                             _ptr(offsets), _ptr(out), _stream_handle(stream)),
+                                             _ptr(offsets), _ptr(out), out.numel() // 24 if out is not None else 0,
+                                             _stream_handle(stream)),
               "agnes_records_compact")
         return offsets, out
 
@@ -241,8 +242,18 @@ class Engine:
             out = torch.empty((max(batch.n_votes, 1), 16), dtype=torch.uint8, device=self.device)
         b = batch.c()
         check(self.lib.agnes_edges_compact(self.ctx, C.byref(cfg), C.byref(b), _ptr(counts), _ptr(seg),
-                                           _ptr(offsets), _ptr(out), _stream_handle(stream)), "agnes_edges_compact")
+                                           _ptr(offsets), _ptr(out), out.numel() // 16 if out is not None else 0,
+                                           _stream_handle(stream)), "agnes_edges_compact")
         return offsets, out
+
+    def records_overflow(self) -> int:
+        """agnes_records_overflow: records the dense writers dropped (past out's capacity or
+        their segment's end) since the last query; 0 when every record fit (synchronises)."""
+        n = C.c_uint64(0)
+        rc = self.lib.agnes_records_overflow(self.ctx, C.byref(n))
+        if rc not in (abi.OK, abi.E_OVERFLOW):
+            check(rc, "agnes_records_overflow")
+        return int(n.value)
 
     def events_capacity(self, cfg: abi.Config, batch: DeviceBatch) -> int:
         b = batch.c()
@@ -481,7 +492,7 @@ class Engine:
         out = torch.empty((max(n, 1), 16), dtype=torch.uint8, device=self.device)
         if n:
             check(self.lib.agnes_edges(self.ctx, C.byref(cfg), C.byref(b), _ptr(codes), _ptr(offs),
-                                       _ptr(out), sh), "agnes_edges")
+                                       _ptr(out), n, sh), "agnes_edges")
         return offs, out[:n]
 
     def events(self, cfg: abi.Config, batch: DeviceBatch, codes: torch.Tensor, stream=None):
@@ -501,8 +512,17 @@ class Engine:
         out = torch.empty((max(n, 1), 24), dtype=torch.uint8, device=self.device)
         if n:
             check(self.lib.agnes_events(self.ctx, C.byref(cfg), C.byref(b), _ptr(codes), _ptr(offs),
-                                        _ptr(out), sh), "agnes_events")
+                                        _ptr(out), n, sh), "agnes_events")
         return offs, out[:n]
+
+    def events_into(self, cfg: abi.Config, batch: DeviceBatch, codes: torch.Tensor, offsets: torch.Tensor,
+                    out: torch.Tensor, stream=None):
+        """agnes_events with the caller's offsets and out (uint8 [cap, 24]): pass 2 alone, no
+        sync -- the records past out's capacity or past an instance's end offset are
+        dropped and counted (records_overflow)."""
+        b = batch.c()
+        check(self.lib.agnes_events(self.ctx, C.byref(cfg), C.byref(b), _ptr(codes), _ptr(offsets), _ptr(out),
+                                    out.numel() // 24, _stream_handle(stream)), "agnes_events")
 
     # -- synthetic workloads ------------------------------------------------
     def gen_offsets(self, p: abi.GenParams) -> np.ndarray:

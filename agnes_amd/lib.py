@@ -88,16 +88,19 @@ def load():
                                P, P, P, P, P, P, P], C.c_int),
         "agnes_apply_msgs": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P, P, P], C.c_int),
         "agnes_edge_offsets": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P], C.c_int),
-        "agnes_edges": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P], C.c_int),
+        "agnes_edges": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, C.c_uint64, P], C.c_int),
         "agnes_fold_counts": ([P, P, C.c_uint32, C.c_uint32, P, P, C.c_uint32, P], C.c_int),
         "agnes_event_offsets": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P], C.c_int),
-        "agnes_events": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P], C.c_int),
+        "agnes_events": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, C.c_uint64, P], C.c_int),
         "agnes_tally_events": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P, P, P], C.c_int),
         "agnes_events_capacity": ([C.POINTER(abi.Config), C.POINTER(abi.VoteBatch)], C.c_uint64),
         "agnes_tally_records": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P, P, P], C.c_int),
-        "agnes_records_compact": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P, P], C.c_int),
+        "agnes_records_compact": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P, C.c_uint64, P],
+                                  C.c_int),
+        "agnes_records_overflow": ([P, C.POINTER(C.c_uint64)], C.c_int),
         "agnes_tally_edges": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P, P, P], C.c_int),
-        "agnes_edges_compact": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P, P], C.c_int),
+        "agnes_edges_compact": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), P, P, P, P, C.c_uint64, P],
+                                C.c_int),
         "agnes_dedup_first": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), C.c_uint64, P, P], C.c_int),
         "agnes_dedup_mask": ([P, C.POINTER(abi.Config), C.POINTER(abi.VoteBatch), C.c_uint64, P, P, P],
                              C.c_int),

@@ -42,6 +42,7 @@ extern "C" {
 #define AGNES_E_DEVICE (-3)      /* HIP runtime error                            */
 #define AGNES_E_NOMEM (-4)       /* allocation failed                            */
 #define AGNES_E_NODEVICE (-5)    /* no GPU visible: the engine has NO CPU fallback */
+#define AGNES_E_OVERFLOW (-6)    /* agnes_records_overflow: records that did not fit were dropped */
 
 /* ---------------------------------------------------------------------------
  * Value / vote vocabulary (src/lib.rs:3-39)
@@ -665,19 +666,21 @@ typedef struct agnes_edge {
 int agnes_tally_edges(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch, uint8_t* codes,
                       const agnes_state* states_in, agnes_state* states_out, uint64_t* counts, agnes_edge* out,
                       void* stream);
+/* out_cap: the records out holds (see agnes_records_overflow) */
 int agnes_edges_compact(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch, const uint64_t* counts,
-                        const agnes_edge* seg, uint64_t* offsets, agnes_edge* out, void* stream);
+                        const agnes_edge* seg, uint64_t* offsets, agnes_edge* out, uint64_t out_cap, void* stream);
 /* Pass 1: offsets (DEVICE, n_instances + 1): exclusive offsets of each instance's
  * edges, offsets[n_instances] = the total.  codes as agnes_tally left them
  * (DEVICE); votes with round >= cfg->max_rounds or type > 1 are never edges.
  * Asynchronous on `stream`. */
 int agnes_edge_offsets(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
                        const uint8_t* codes, uint64_t* offsets, void* stream);
-/* Pass 2: the records into out (DEVICE, offsets[n_instances] records), instance i's
- * at [offsets[i], offsets[i+1]).  offsets from agnes_edge_offsets on the same
- * batch and codes. */
+/* Pass 2: the records into out (DEVICE, out_cap records: offsets[n_instances] of them),
+ * instance i's at [offsets[i], offsets[i+1]).  offsets from agnes_edge_offsets on the
+ * same batch and codes; an edge past out_cap or past its instance's end offset is
+ * dropped, never written (agnes_records_overflow reports it). */
 int agnes_edges(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
-                const uint8_t* codes, const uint64_t* offsets, agnes_edge* out, void* stream);
+                const uint8_t* codes, const uint64_t* offsets, agnes_edge* out, uint64_t out_cap, void* stream);
 /* The same summary of the LAST agnes_multi_tally's batch (the native multi-GPU
  * driver), gathered from every device into HOST arrays in the batch's own numbering:
  * offsets [n_instances + 1] first, then out [offsets[n_instances]] records. */
@@ -711,10 +714,13 @@ typedef struct agnes_vote_event {
  * records, offsets[n_instances] = the total.  codes as agnes_tally left them. */
 int agnes_event_offsets(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
                         const uint8_t* codes, uint64_t* offsets, void* stream);
-/* Pass 2: the records into out (DEVICE, offsets[n_instances] records, 8-B aligned);
- * reads codes, round, type and value.  max_rounds <= 64. */
+/* Pass 2: the records into out (DEVICE, 8-B aligned, out_cap records: offsets[n_instances]
+ * of them); reads codes, round, type and value.  max_rounds <= 64.  A record past out_cap
+ * or past its instance's (its emit batch's) end offset -- offsets that are not this
+ * batch's, an undersized out -- is dropped, never written (agnes_records_overflow). */
 int agnes_events(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
-                 const uint8_t* codes, const uint64_t* offsets, agnes_vote_event* out, void* stream);
+                 const uint8_t* codes, const uint64_t* offsets, agnes_vote_event* out, uint64_t out_cap,
+                 void* stream);
 
 /* The tally and its event stream in ONE call (agnes_tally with
  * d_out / d_n_out): agnes_tally_states, then the records of every Some(Event) as
@@ -764,7 +770,18 @@ int agnes_tally_records(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vot
  * agnes_vote_event records in instance then vote order -- exactly agnes_tally_events'. */
 int agnes_records_compact(agnes_ctx* ctx, const agnes_config* cfg, const agnes_vote_batch* batch,
                           const uint64_t* counts, const agnes_seg_event* seg, uint64_t* offsets, agnes_vote_event* out,
-                          void* stream);
+                          uint64_t out_cap, void* stream);
+
+/* Records the dense writers (agnes_events, agnes_edges, agnes_tally_events, the two
+ * compactions) dropped on this context since the last query, because they fell past
+ * out_cap (agnes_tally_events: agnes_events_capacity) or past their segment's end
+ * offset: the calls are asynchronous, so a bad size surfaces here, as a status, and
+ * never as a write outside `out`.  Synchronises the context's stream; resets the count.
+ * Returns AGNES_OK (nothing dropped) or AGNES_E_OVERFLOW with the count in *dropped.
+ * The segmented writers (agnes_tally_records / agnes_tally_edges) place instance i's
+ * records at most at its own votes' positions (a vote gives at most `mult` records),
+ * inside agnes_events_capacity() for any offsets, so they cannot overflow. */
+int agnes_records_overflow(agnes_ctx* ctx, uint64_t* dropped);
 
 /* ---------------------------------------------------------------------------
  * Synthetic workload generator (counter-based splitmix64; identical on host

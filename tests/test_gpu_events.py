@@ -102,3 +102,90 @@ def test_gpu_events_ragged_and_invalid(eng):
     hb = ol.batch_from_lists(inst, rnd, typ, val, vdr, off)
     power = ol.gen_power(44, 1, 10, abi.POWER_UNIFORM, 1, 10)
     _run(eng, abi.config(abi.MODE_REFERENCE, 0, 3), hb, power)
+
+
+GUARD = 64  # records past the capacity handed to the call, filled with a canary
+
+
+def _guarded(n, width, device):
+    """a uint8 [n + GUARD, width] buffer of 0xCD: the call gets capacity n"""
+    return torch.full((n + GUARD, width), 0xCD, dtype=torch.uint8, device=device)
+
+
+def _guard_intact(buf, n):
+    return bool((buf[n:].cpu().numpy() == 0xCD).all())
+
+
+@pytest.mark.parametrize("route", ["walk", "stream"])
+def test_records_bounded_by_capacity(eng, route):
+    """Round 6 (review item 3): every dense writer is bounded on the device.  agnes_events
+    handed an `out` that holds half its offsets' records, or offsets that are not the
+    batch's (every instance's segment halved), writes nothing outside `out` and reports
+    the dropped records through agnes_records_overflow; the records that fit are the
+    right ones.  The same for agnes_records_compact given counts that are not the
+    segments' and for agnes_edges / agnes_edges_compact.  ('walk': the value column off
+    16-B alignment takes the lane-per-instance emit; 'stream': the batch-stream emit.)"""
+    p = abi.gen_params(seed=47, n_instances=3000, n_vals=60, rounds_min=1, rounds_max=2, nil_permille=250)
+    hb = ol.gen_batch(p)
+    power = ol.gen_power(47, 3, 60, abi.POWER_UNIFORM, 1, 500)
+    cfg = abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 2)
+    eng.upload_power(power)
+    db = DeviceBatch.from_host(hb, eng.device)
+    codes = torch.zeros(hb.n_votes, dtype=torch.uint8, device=eng.device)
+    eng.tally(cfg, db, codes, states_to_device(abi.new_states(3000, 1, abi.STEP_PREVOTE), eng.device))
+    dbe = DeviceBatch.from_host(hb, eng.device)  # the two-call stream's batch
+    if route == "walk":
+        v = torch.zeros(hb.n_votes + 4, dtype=db.value.dtype, device=eng.device)
+        v[1:1 + hb.n_votes] = db.value
+        dbe.value = v[1:1 + hb.n_votes]
+    offs, recs = eng.events(cfg, dbe, codes)
+    assert eng.records_overflow() == 0
+    total = int(offs[-1].item())
+    good = recs.cpu().numpy()
+    # (1) out holds half the records
+    half = total // 2
+    out = _guarded(half, 24, eng.device)
+    eng.events_into(cfg, dbe, codes, offs, out[:half])
+    torch.cuda.synchronize()
+    assert eng.records_overflow() == total - half
+    assert _guard_intact(out, half)
+    assert np.array_equal(out[:half].cpu().numpy(), good[:half])
+    # (2) offsets that are not the batch's: every instance's segment halved
+    bad_offs = offs // 2
+    out = _guarded(total, 24, eng.device)
+    eng.events_into(cfg, dbe, codes, bad_offs, out[:total])
+    torch.cuda.synchronize()
+    assert eng.records_overflow() > 0
+    assert _guard_intact(out, total)
+    # (3) the compaction of segmented records with counts that are not the segments'
+    st = states_to_device(abi.new_states(3000, 1, abi.STEP_PREVOTE), eng.device)
+    counts, seg = eng.tally_records(cfg, db, codes, st, st)
+    torch.cuda.synchronize()
+    assert eng.records_overflow() == 0
+    big = counts * 2 + 5
+    dense = _guarded(total, 24, eng.device)
+    eng.records_compact(cfg, db, big, seg, out=dense[:total])
+    torch.cuda.synchronize()
+    assert eng.records_overflow() > 0
+    assert _guard_intact(dense, total)
+    # (4) edges: a half-size out, then compacted segments with inflated counts
+    eoffs, erecs = eng.edges(cfg, db, codes)
+    etot = int(eoffs[-1].item())
+    assert eng.records_overflow() == 0 and etot > 0
+    b = db.c()
+    eh = etot // 2
+    eout = _guarded(eh, 16, eng.device)
+    rc = eng.lib.agnes_edges(eng.ctx, __import__("ctypes").byref(cfg), __import__("ctypes").byref(b),
+                             codes.data_ptr(), eoffs.data_ptr(), eout.data_ptr(), eh, None)
+    assert rc == abi.OK
+    torch.cuda.synchronize()
+    assert eng.records_overflow() == etot - eh
+    assert _guard_intact(eout, eh)
+    st = states_to_device(abi.new_states(3000, 1, abi.STEP_PREVOTE), eng.device)
+    ecnt, eseg = eng.tally_edges(cfg, db, codes, st, st)
+    torch.cuda.synchronize()
+    edense = _guarded(etot, 16, eng.device)
+    eng.edges_compact(cfg, db, ecnt * 3 + 1, eseg, out=edense[:etot])
+    torch.cuda.synchronize()
+    assert eng.records_overflow() > 0
+    assert _guard_intact(edense, etot)
