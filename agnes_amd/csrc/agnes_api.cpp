@@ -391,7 +391,8 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     if (ev_counts) {
         const uint32_t route = (cfg->flags >> AGNES_ROUTE_SHIFT) & AGNES_ROUTE_MASK;
         bool flow = !wide_all && !w64 && route == AGNES_ROUTE_AUTO && cfg->mode == AGNES_MODE_REFERENCE &&
-                    !(cfg->flags & AGNES_FLAG_ROUND_SKIP) && agnes_flow_counts_events(cfg->flags, cfg->max_rounds, edges);
+                    !(cfg->flags & AGNES_FLAG_ROUND_SKIP) &&
+                    agnes_flow_counts_events(cfg->flags, cfg->max_rounds, edges, rec_out != nullptr);
         if (flow) a.ev_counts = ev_counts;
         if (flow && rec_out) a.rec_out = rec_out; /* agnes_tally_records / _edges: the flow kernel writes them too */
         /* several rounds: the fused records variant runs at 2 waves per SIMD (its VGPRs),
@@ -758,7 +759,9 @@ int agnes_tally_records(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_
                                                reinterpret_cast<const uint32_t*>(c->d_err + AGNES_ERR_BYTES / 8) +
                                                    AGNES_WALK_COUNT,
                                                counts, out, st));
-    if (b->n_instances && agnes_seg_emit_ok(b, codes, cfg->max_rounds))
+    /* the emit pass keeps record positions inside a batch as u32: a batch that could
+     * hold 2^32 records or more (n_votes x mult) goes to the walk, whose positions are u64 */
+    if (b->n_instances && (uint64_t)b->n_votes * mult < (1ull << 32) && agnes_seg_emit_ok(b, codes, cfg->max_rounds))
         /* the event stream's emit pass writing each record to its instance's segment
          * (and the counts): no count pass before it */
         return status_of(agnes_launch_seg_emit(b, codes, cfg->max_rounds, mult, counts, out, st));

@@ -118,14 +118,17 @@ constexpr uint32_t EV_LO = AGNES_CODE_NONE | (AGNES_CODE_POLKA_ANY << 8) | (AGNE
 constexpr uint32_t EV_HI = AGNES_CODE_NONE | (AGNES_CODE_PRECOMMIT_ANY << 8) | (AGNES_CODE_NONE << 16) |
                            (AGNES_CODE_PRECOMMIT_VALUE << 24);
 
-__host__ __device__ inline uint32_t carry_bytes(uint32_t R, bool w64 = false) {
-    return (uint32_t)align16((w64 ? 64ull : 32ull) * R);
+/* (REC) each carried row also holds the executors' value slots vl[2R] (u32): the last
+ * non-nil value an executor took, round_votes.rs:50-54 */
+__host__ __device__ inline uint32_t carry_bytes(uint32_t R, bool w64 = false, bool rec = false) {
+    return (uint32_t)align16((w64 ? 64ull : (rec ? 48ull : 32ull)) * R);
 }
 /* per-wave LDS: DMA slot | carried executors (2 copies x (vw[2R], vn[2R]) u32, or u64
  * for W64) | instance records | (State machine) valid candidates, two batches' staged States */
-__host__ __device__ inline uint32_t lds_bytes(bool sm, uint32_t R, bool evc = false, bool w64 = false, bool edg = false) {
-    return F_BYTES + carry_bytes(R, w64) + FB * (w64 ? RECW64 : RECW) * 4u + (sm ? FB * 8u + 2u * FB * 64u : 0u) +
-           (evc ? FB * 4u : 0u) + (edg ? (uint32_t)align16(FB * 2ull * R) : 0u);
+__host__ __device__ inline uint32_t lds_bytes(bool sm, uint32_t R, bool evc = false, bool w64 = false, bool edg = false,
+                                              bool rec = false) {
+    return F_BYTES + carry_bytes(R, w64, rec) + FB * (w64 ? RECW64 : RECW) * 4u + (sm ? FB * 8u + 2u * FB * 64u : 0u) +
+           (evc ? FB * 4u : 0u) + (edg ? (uint32_t)align16(FB * 2ull * R) : 0u) + (rec ? (uint32_t)align16(16ull * R) : 0u);
 }
 
 /* a State out (plain stores: non-temporal ones measured slower on C2) */
@@ -229,27 +232,6 @@ struct Hdr {
     uint32_t go;        /* stage 3: this kernel walks it as one stream                        */
 };
 
-/* The value slot of executor (inst, r, t) after the votes before j (round_votes.rs:
- * 50-54, one value slot, last writer wins): the last non-nil value the tally added,
- * walking back to the instance start lo; Value{} (0) when none.  The rare path of the
- * fused records: a nil vote whose PolkaValue / PrecommitValue executor took no non-nil
- * vote earlier in its part of the chunk.  A vote counts when it is valid (REFERENCE:
- * every valid vote is added): its instance id, type <= 1, validator in the set (its
- * round is r < max_rounds). */
-__device__ __attribute__((noinline)) uint32_t label_back(const uint32_t* inst_col, const uint8_t* round_col,
-                                                        const uint8_t* type_col, const uint32_t* value_col,
-                                                        const uint32_t* val_col, uint64_t lo, uint64_t j, uint32_t inst,
-                                                        uint32_t r, uint32_t t, uint32_t nvs) {
-    for (uint64_t q = j; q > lo;) {
-        --q;
-        if (round_col[q] != r || type_col[q] != t) continue;
-        const uint32_t v = value_col[q];
-        if (v == AGNES_NIL || inst_col[q] != inst || val_col[q] >= nvs) continue;
-        return v;
-    }
-    return 0u;
-}
-
 /* EVC: also the number of event records of each instance of a flow batch (votes whose
  * code is Some(Event), 1..5: this route never sets the RoundSkip bit) into
  * a.ev_counts[instance] -- the count pass of the event stream (agnes_events.hip) */
@@ -291,7 +273,7 @@ template <bool PC, bool SM, bool R1, bool EVC, bool W64, bool REC = false, bool 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES_FLOW_W64_WPE : ((REC || EDG) ? (R1 ? AGNES_FLOW_XWPE : AGNES_FLOW_XWPE_R) : AGNES_FLOW_WPE)))) void flow(agnes_tally_args a, uint32_t lds_per_wave) {
     static_assert(!REC || (EVC && !W64), "records: with the record counts, u32 sums");
     static_assert(!EDG || (EVC && !W64 && !REC), "edges: the counts are the edges', u32 sums");
-    static_assert(!U || (!W64 && !REC && !EDG), "unaligned streams: u32 sums, codes and record counts");
+    static_assert(!U || !W64, "unaligned streams: u32 sums");
     /* the unaligned kernel: nothing to do unless the aligned one left it batches (any of its
      * flags: 4 per lane) */
     if (U && !AGNES_FLOW_FORCE_U) {
@@ -324,8 +306,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
     unsigned char* const slot = base;
     const uint32_t slotl = lds_addr(slot);
     uint32_t* const crow = reinterpret_cast<uint32_t*>(base + F_BYTES);
-    const uint32_t cw = (W64 ? 8u : 4u) * R; /* one carry copy: vw[2R] then vn[2R] (u32 words) */
-    const uint32_t CB = carry_bytes(R, W64);
+    const uint32_t cw = (W64 ? 8u : (REC ? 6u : 4u)) * R; /* one carry copy: vw[2R], vn[2R] (u32 words), (REC) vl[2R] */
+    const uint32_t CB = carry_bytes(R, W64, REC);
     uint32_t* const itab = reinterpret_cast<uint32_t*>(base + F_BYTES + CB);
     unsigned long long* const vtab = reinterpret_cast<unsigned long long*>(base + F_BYTES + CB + FB * RW * 4u);
     unsigned char* const sb = base + F_BYTES + CB + FB * RW * 4u + FB * 8u;
@@ -333,6 +315,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                                                        (SM ? FB * 8u + 2u * FB * 64u : 0u)); /* (EVC) records */
     /* (EDG) each executor's edge state after the votes so far, [instance][round * 2 + type] bytes */
     unsigned char* const elab = reinterpret_cast<unsigned char*>(etab + FB);
+    /* (REC) this chunk's last non-nil vote of each executor of the instance carried into the
+     * next chunk: (position + 1) << 32 | value, an LDS max, [2R] */
+    unsigned long long* const vmx = reinterpret_cast<unsigned long long*>(etab + FB);
     const agnes_state* const st_in = a.states_in ? a.states_in : a.states;
     uint32_t cpar = 0;
     uint64_t pf_at = ~0ull;
@@ -1576,14 +1561,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                     /* ---- the records themselves (agnes_tally_records): every vote whose event is
                      * Some (codes 1..5) as a 16-B agnes_seg_event in its instance's segment,
                      * out[offsets[i] + k] with k the instance's records before it, written while
-                     * the votes are in registers (vote_executor.rs:20-36) ---- */
+                     * the votes are in registers (vote_executor.rs:20-36).  A record's slot is at
+                     * most its own vote's position (k counts records of earlier votes of the
+                     * instance), so the writes stay inside the n_votes records out holds ---- */
                     auto recm = [](uint32_t cw4) -> uint32_t { /* 0x80 in the bytes of votes with a record */
                         const uint32_t e = cw4 & 0x07070707u;
                         return (e + 0x7F7F7F7Fu) & ~(e + 0x7A7A7A7Au) & 0x80808080u;
                     };
-                    const uint32_t hA = actA ? recm(c0) : 0u, hB = actB ? recm(c1) : 0u;
-                    if (ballot((hA | hB) != 0u)) {
-                        const uint32_t nA = (uint32_t)__builtin_popcount(hA), nB = (uint32_t)__builtin_popcount(hB);
+                    const uint32_t h0 = recm(c0) & act0, h1 = recm(c1) & act1;
+                    /* the instance's units: bytes before spI (U), or the lane's two words */
+                    const uint32_t mI0 = U ? below_bytes((int32_t)spI) : 0xFFFFFFFFu;
+                    const uint32_t mI1 = U ? below_bytes((int32_t)spI - 4) : 0u;
+                    const uint32_t nA = (uint32_t)__builtin_popcount(h0 & mI0) + (uint32_t)__builtin_popcount(h1 & mI1);
+                    const uint32_t nB = (uint32_t)__builtin_popcount(h0 & ~mI0) + (uint32_t)__builtin_popcount(h1 & ~mI1);
+                    const bool fast = R1 || runs; /* a lane part of one segment is one executor per type */
+                    const bool spl = R1 ? split : splitr;
+                    /* the executors' split inside the lane: unit B from vote spE (U), or from vote 4 */
+                    const uint32_t spE = U ? (R1 ? spI : (runs ? spR : 8u)) : 4u;
+                    auto inBe = [&](uint32_t q) -> bool { return U ? q >= spE : q >= 4u; };
+                    const uint32_t vok0 = okb0 & ~mark_bytes(nb0 << 3), vok1 = okb1 & ~mark_bytes(nb1 << 3); /* valid non-nil */
+                    const uint32_t K2 = 2u * R;
+                    auto key_of = [&](uint32_t q) -> uint32_t { /* batch instance, round, type */
+                        const uint32_t bs = 8u * (q & 3u);
+                        return (inB(q) ? kB : kA) * K2 + 2u * (((q < 4u ? r8[0] : r8[1]) >> bs) & 0xFFu) +
+                               (((q < 4u ? t8[0] : t8[1]) >> bs) & 1u);
+                    };
+                    /* (lastc) the chunk's last non-nil vote of each executor of the carried
+                     * instance, for the value slots of the next chunk */
+                    if (lastc) {
+                        if (lane < K2) vmx[lane] = 0ull;
+                        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                        for (uint32_t q = 0; q < LV; ++q) {
+                            const uint32_t bs = 8u * (q & 3u);
+                            if ((((q < 4u ? vok0 : vok1) >> bs) & 1u) && (inB(q) ? kB : kA) == klast)
+                                atomicMax(vmx + (key_of(q) - klast * K2),
+                                          ((unsigned long long)(o8 + q + 1u) << 32) | value[q]);
+                        }
+                    }
+                    if (ballot((h0 | h1) != 0u)) {
                         /* ranks inside the chunk: an exclusive scan of the lanes' last-instance counts,
                          * less the scan at the instance's first lane; plus the instance's records of
                          * earlier chunks (etab, before this chunk's counts are added below) */
@@ -1596,19 +1612,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                          * vote's own when non-nil; for a nil vote the last non-nil value its executor
                          * took before it -- in the lane, else (one round, or runs: the segment is the
                          * executor's run up to its type) the last earlier lane of the segment holding
-                         * one, else the stream before the chunk part (label_back) */
-                        const uint32_t vok0 = okb0 & ~mark_bytes(nb0 << 3), vok1 = okb1 & ~mark_bytes(nb1 << 3); /* valid non-nil */
+                         * one, else its value slot from before the chunk (carried in LDS: the instance
+                         * continuing from the previous chunk) or Value{} */
                         uint32_t vv[LV];
-                        uint32_t pend = 0u; /* bit s: a nil Value vote not resolved in the lane */
+                        uint32_t pend = 0u; /* bit s: a nil Value vote with a record, not resolved in the lane */
+                        const uint64_t h64 = u64of(h0, h1);
                         bool hv0 = false, hv1 = false;
                         uint32_t lv0x = 0u, lv1x = 0u;
-                        const bool spl = R1 ? split : splitr;
-                        /* one round, or runs: a lane part of one segment is one executor per type;
-                         * otherwise (rounds revisited in the chunk) every nil Value vote walks back */
-                        const bool fast = R1 || runs;
 #pragma unroll
                         for (uint32_t q = 0; q < LV; ++q) {
-                            if (q == 4u && spl) { hv0 = false; hv1 = false; }
+                            if (U ? q == spE : (q == 4u && spl)) { hv0 = false; hv1 = false; }
                             const uint32_t bs = 8u * (q & 3u);
                             const uint32_t cq = ((q < 4u ? c0 : c1) >> bs) & 7u;
                             const bool tq = (((q < 4u ? t8[0] : t8[1]) >> bs) & 1u) != 0u;
@@ -1617,39 +1630,73 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                             const bool hasT = fast && (tq ? hv1 : hv0);
                             const uint32_t lT = tq ? lv1x : lv0x;
                             vv[q] = nn ? value[q] : (isv && hasT ? lT : AGNES_NIL);
-                            pend |= (isv && !nn && !hasT) ? 1u << q : 0u;
+                            pend |= (isv && !nn && !hasT && ((h64 >> (8u * q + 7u)) & 1ull)) ? 1u << q : 0u;
                             if (nn) {
                                 if (tq) { hv1 = true; lv1x = value[q]; } else { hv0 = true; lv0x = value[q]; }
                             }
                         }
+                        /* the carried slot of a vote's executor: its instance continues from the
+                         * previous chunk (the first segment) -- else the executor is new: Value{} */
+                        auto carried = [&](uint32_t q) -> uint32_t {
+                            const uint32_t k = inB(q) ? kB : kA;
+                            return (cont0 && k == k0) ? A[4u * R + (key_of(q) - k * K2)] : 0u;
+                        };
                         if (ballot(pend != 0u)) {
-                            const uint32_t sx = !fast ? 0u : (R1 ? (multi ? sA : 0u) : (multir ? sAr : 0u));
-                            const uint64_t seg = (((1ull << lane) - 1ull) >> sx) << sx; /* lanes [sx, lane) */
-                            const uint64_t B0 = ballot(hv0), B1 = ballot(hv1);
-                            const uint64_t m0 = B0 & seg, m1 = B1 & seg;
-                            const uint32_t j0 = m0 ? 63u - (uint32_t)__builtin_clzll(m0) : 0u;
-                            const uint32_t j1 = m1 ? 63u - (uint32_t)__builtin_clzll(m1) : 0u;
-                            const uint32_t f0 = shfl(lv0x, j0), f1 = shfl(lv1x, j1);
-                            for (uint32_t q = 0; q < LV; ++q) {
-                                if (!((pend >> q) & 1u)) continue;
-                                const uint32_t bs = 8u * (q & 3u);
-                                const bool tq = (((q < 4u ? t8[0] : t8[1]) >> bs) & 1u) != 0u;
-                                if (fast && (q < 4u || !spl) && (tq ? m1 : m0)) {
-                                    vv[q] = tq ? f1 : f0;
-                                } else {
-                                    const uint32_t rq = ((q < 4u ? r8[0] : r8[1]) >> bs) & 0xFFu;
-                                    const uint64_t gq = q < 4u ? gA : gB;
-                                    /* fast: the segment's votes in the chunk before this one hold no
-                                     * match (the lane's part and lanes [sx, lane) were searched), so the
-                                     * walk starts at the segment's first lane (unit B of a split lane) */
-                                    const uint64_t js = !fast ? c + o8 + q : ((q >= 4u && spl) ? c + o8 + 4u : c + 8u * sx);
-                                    vv[q] = label_back(a.vb.instance, a.vb.round, a.vb.type, a.vb.value, a.vb.validator, gq,
-                                                       js, H.s0 + (q < 4u ? kA : kB), rq, tq ? 1u : 0u,
-                                                       q < 4u ? recA.z : recB.z);
+                            if (fast) {
+                                const uint32_t sx = R1 ? (multi ? sA : 0u) : (multir ? sAr : 0u);
+                                const uint64_t seg = (((1ull << lane) - 1ull) >> sx) << sx; /* lanes [sx, lane) */
+                                const uint64_t B0 = ballot(hv0), B1 = ballot(hv1);
+                                const uint64_t m0 = B0 & seg, m1 = B1 & seg;
+                                const uint32_t j0 = m0 ? 63u - (uint32_t)__builtin_clzll(m0) : 0u;
+                                const uint32_t j1 = m1 ? 63u - (uint32_t)__builtin_clzll(m1) : 0u;
+                                const uint32_t f0 = shfl(lv0x, j0), f1 = shfl(lv1x, j1);
+                                for (uint32_t q = 0; q < LV; ++q) {
+                                    if (!((pend >> q) & 1u)) continue;
+                                    const uint32_t bs = 8u * (q & 3u);
+                                    const bool tq = (((q < 4u ? t8[0] : t8[1]) >> bs) & 1u) != 0u;
+                                    vv[q] = ((!inBe(q) || !spl) && (tq ? m1 : m0)) ? (tq ? f1 : f0) : carried(q);
+                                }
+                            } else {
+                                /* rounds revisited in the chunk: one executor (instance, round, type) at a
+                                 * time -- its last non-nil vote before each of its pending votes, in the
+                                 * lane, else in the last earlier lane holding one, else its slot */
+                                uint32_t todo = pend;
+                                for (;;) {
+                                    const uint64_t lm = ballot(todo != 0u);
+                                    if (!lm) break;
+                                    const uint32_t kl = (uint32_t)__builtin_ctzll(lm);
+                                    const uint32_t qs = (uint32_t)__builtin_ctz(rdl(todo, kl));
+                                    uint32_t mykey = key_of(0u);
+#pragma unroll
+                                    for (uint32_t q = 1; q < LV; ++q) mykey = qs == q ? key_of(q) : mykey;
+                                    const uint32_t KY = rdl(mykey, kl);
+                                    bool has = false;
+                                    uint32_t last = 0u, unres = 0u, inb = 0u;
+#pragma unroll
+                                    for (uint32_t q = 0; q < LV; ++q) {
+                                        const uint32_t bs = 8u * (q & 3u);
+                                        const bool mk = ((((q < 4u ? okb0 : okb1) >> bs) & 1u) != 0u) && key_of(q) == KY;
+                                        /* (the lane's first pending vote is always of key KY: each
+                                         * pass clears at least one bit of todo) */
+                                        if (key_of(q) == KY && ((todo >> q) & 1u)) {
+                                            inb |= 1u << q;
+                                            if (has) vv[q] = last;
+                                            else unres |= 1u << q;
+                                        }
+                                        if (mk && (((q < 4u ? vok0 : vok1) >> bs) & 1u)) {
+                                            has = true;
+                                            last = value[q];
+                                        }
+                                    }
+                                    todo &= ~inb;
+                                    const uint64_t M = ballot(has) & ((1ull << lane) - 1ull);
+                                    const uint32_t fm = shfl(last, M ? 63u - (uint32_t)__builtin_clzll(M) : 0u);
+                                    for (uint32_t q = 0; q < LV; ++q)
+                                        if ((unres >> q) & 1u) vv[q] = M ? fm : carried(q);
                                 }
                             }
                         }
-                        /* the stores: one 16-B record per vote with an event.  Per unit, bytewise:
+                        /* the stores: one 16-B record per vote with an event.  Per word, bytewise:
                          * kind = event + 3 (AGNES_EV_POLKA_ANY ..), the message nibble, and the
                          * Value events (3, 5); a record's last word is assembled by two v_perm */
                         uint4* const pA = reinterpret_cast<uint4*>(a.rec_out) + gA + rA;
@@ -1664,17 +1711,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
 #pragma unroll
                         for (uint32_t q = 0; q < LV; ++q) {
                             const uint32_t b = q & 3u, bs = 8u * b;
-                            const uint32_t hm = q < 4u ? hA : hB;
-                            if ((hm >> (bs + 7u)) & 1u) {
-                                const uint32_t k = (uint32_t)__builtin_popcount(hm & ((1u << bs) - 1u));
+                            if ((h64 >> (8u * q + 7u)) & 1ull) {
+                                /* the vote's rank among its unit's records */
+                                const uint32_t k = (uint32_t)__builtin_popcountll(h64 & ((1ull << (8u * q)) - 1ull)) -
+                                                   (inB(q) ? nA : 0u);
                                 /* [round, kind, message, 0] */
                                 const uint32_t rk = __builtin_amdgcn_perm(q < 4u ? kd0 : kd1, q < 4u ? r8[0] : r8[1],
                                                                           b | ((4u + b) << 8) | 0x0C0C0000u);
                                 const uint32_t w3 = __builtin_amdgcn_perm(q < 4u ? ms0 : ms1, rk, 0x0C000100u | ((4u + b) << 16));
                                 const bool isv = (((q < 4u ? vm0 : vm1) >> (bs + 7u)) & 1u) != 0u;
-                                (q < 4u ? pA : pB)[k] = make_uint4(jlo | q, jhi, isv ? vv[q] : AGNES_NIL, w3);
+                                (inB(q) ? pB : pA)[k] = make_uint4(jlo | q, jhi, isv ? vv[q] : AGNES_NIL, w3);
                             }
                         }
+                    }
+                    if (lastc) { /* the carried instance's value slots after the chunk (row B) */
+                        __builtin_amdgcn_wave_barrier();
+                        if (lane < K2) {
+                            const unsigned long long x = vmx[lane];
+                            if (x) B[4u * R + lane] = (uint32_t)x;
+                        }
+                        __builtin_amdgcn_wave_barrier();
                     }
                 }
 
@@ -1697,17 +1753,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                     auto nzb = [](uint32_t x) -> uint32_t { /* 0x80 in the non-zero bytes of x */
                         return ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu | x) & 0x80808080u;
                     };
-                    const uint32_t em0 = nzb((c0 ^ cbf0) & 0x07070707u) & (actA ? okb0 : 0u);
-                    const uint32_t em1 = nzb((c1 ^ cbf1) & 0x07070707u) & (actB ? okb1 : 0u);
-                    const uint32_t nA = (uint32_t)__builtin_popcount(em0), nB = (uint32_t)__builtin_popcount(em1);
+                    const uint32_t em0 = nzb((c0 ^ cbf0) & 0x07070707u) & okb0; /* (okb: inside the stream) */
+                    const uint32_t em1 = nzb((c1 ^ cbf1) & 0x07070707u) & okb1;
+                    /* the instance's units: bytes before spI (U), or the lane's two words */
+                    const uint32_t mI0 = U ? below_bytes((int32_t)spI) : 0xFFFFFFFFu;
+                    const uint32_t mI1 = U ? below_bytes((int32_t)spI - 4) : 0u;
+                    const uint32_t nA = (uint32_t)__builtin_popcount(em0 & mI0) + (uint32_t)__builtin_popcount(em1 & mI1);
+                    const uint32_t nB = (uint32_t)__builtin_popcount(em0 & ~mI0) + (uint32_t)__builtin_popcount(em1 & ~mI1);
                     if (ballot((em0 | em1) != 0u)) {
                         const bool fast = R1 || runs;
                         const bool spl = R1 ? split : splitr;
+                        /* the executors' split inside the lane: unit B from vote spE (U), or from vote 4 */
+                        const uint32_t spE = U ? (R1 ? spI : (runs ? spR : 8u)) : 4u;
+                        auto inBe = [&](uint32_t q) -> bool { return U ? q >= spE : q >= 4u; };
                         const uint32_t K2 = 2u * R;
                         auto key_of = [&](uint32_t q) -> uint32_t { /* instance k, round, type */
                             const uint32_t bs = 8u * (q & 3u);
                             const uint32_t r = ((q < 4u ? r8[0] : r8[1]) >> bs) & 0xFFu, t = ((q < 4u ? t8[0] : t8[1]) >> bs) & 1u;
-                            return (q < 4u ? kA : kB) * K2 + 2u * r + t;
+                            return (inB(q) ? kB : kA) * K2 + 2u * r + t;
                         };
                         /* the lane's edges one at a time (a chunk holds few: 2 % of C2's votes) */
                         auto byteq = [](uint32_t x0, uint32_t x1, uint32_t q) -> uint32_t {
@@ -1722,10 +1785,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                         uint32_t g0 = 0xFFFFFFFFu, g1 = 0xFFFFFFFFu; /* the segment of the lane's first edge per type */
                         for (uint32_t m = emsk; m; m &= m - 1u) {
                             const uint32_t q = (uint32_t)__builtin_ctz(m);
-                            if (spl && q >= 4u && !rs) { hm0 = false; hm1 = false; rs = true; }
+                            if (spl && inBe(q) && !rs) { hm0 = false; hm1 = false; rs = true; }
                             const bool tq = (byteq(t8[0], t8[1], q) & 1u) != 0u;
                             const uint32_t msg = byteq(c0, c1, q) >> 4;
-                            const uint32_t sg = q < 4u ? segA : segB;
+                            const uint32_t sg = inBe(q) ? segB : segA;
                             if (fast && (tq ? hm1 : hm0)) phw |= (tq ? lm1 : lm0) << (4u * q);
                             else php |= 1u << q;
                             if (msg) {
@@ -1744,8 +1807,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                             for (uint32_t m = emsk & php; m; m &= m - 1u) {
                                 const uint32_t q = (uint32_t)__builtin_ctz(m);
                                 const uint32_t tb = byteq(t8[0], t8[1], q) & 1u;
-                                const bool gm = (q < 4u || !spl) && (tb ? M1 : M0) != 0ull;
-                                const uint32_t key = (q < 4u ? kA : kB) * K2 + 2u * byteq(r8[0], r8[1], q) + tb;
+                                const bool gm = (!inBe(q) || !spl) && (tb ? M1 : M0) != 0ull;
+                                const uint32_t key = (inB(q) ? kB : kA) * K2 + 2u * byteq(r8[0], r8[1], q) + tb;
                                 phw |= (gm ? (tb ? f1 : f0) : (uint32_t)(elab[key] >> 4)) << (4u * q);
                             }
                             /* each (segment, type)'s last edge in the chunk carries the state out: a
@@ -1761,10 +1824,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                                 const uint32_t q = 31u - (uint32_t)__builtin_clz(m);
                                 m &= ~(1u << q);
                                 const uint32_t tb = byteq(t8[0], t8[1], q) & 1u;
-                                const uint32_t sg = q < 4u ? segA : segB;
+                                const uint32_t sg = inBe(q) ? segB : segA;
                                 if ((tb ? nx1 : nx0) != sg) {
                                     const uint32_t cb = byteq(c0, c1, q);
-                                    const uint32_t key = (q < 4u ? kA : kB) * K2 + 2u * byteq(r8[0], r8[1], q) + tb;
+                                    const uint32_t key = (inB(q) ? kB : kA) * K2 + 2u * byteq(r8[0], r8[1], q) + tb;
                                     elab[key] = (unsigned char)((cb & 0xFu) | ((cb >> 4) ? (cb & 0xF0u) : (((phw >> (4u * q)) & 0xFu) << 4)));
                                 }
                                 if (tb) nx1 = sg;
@@ -1821,15 +1884,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                         const uint32_t rA = etab[kA] + En - (multi ? shfl(En, sA) : 0u);
                         const uint32_t rB = split ? etab[kB] : rA + nA;
                         const uint64_t gA = Sa + shfl(rl, kA), gB = Sa + shfl(rl, kB);
+                        /* (U) the instance's unit B: votes spI .. 7 */
+                        const uint32_t mIq = U ? (spI < 8u ? (0xFFu << spI) & 0xFFu : 0u) : 0xF0u;
                         for (uint32_t m = emsk; m; m &= m - 1u) {
                             const uint32_t q = (uint32_t)__builtin_ctz(m);
-                            const uint32_t k = (q < 4u ? rA : rB) + (uint32_t)__builtin_popcount(emsk & ((1u << q) - 1u) & (q < 4u ? 0x0Fu : 0xF0u));
+                            const uint32_t k = (inB(q) ? rB : rA) + (uint32_t)__builtin_popcount(emsk & ((1u << q) - 1u) &
+                                                                                                  (inB(q) ? mIq : ~mIq));
                             const uint32_t cb = byteq(c0, c1, q), rq = byteq(r8[0], r8[1], q), tq = byteq(t8[0], t8[1], q) & 1u;
                             const uint32_t prev = (byteq(cbf0, cbf1, q) & 0xFu) | (((phw >> (4u * q)) & 0xFu) << 4);
                             const uint64_t j = c + o8 + q;
-                            const uint4 rec = make_uint4((uint32_t)j, (uint32_t)(j >> 32), H.s0 + (q < 4u ? kA : kB),
+                            const uint4 rec = make_uint4((uint32_t)j, (uint32_t)(j >> 32), H.s0 + (inB(q) ? kB : kA),
                                                          rq | (tq << 8) | (cb << 16) | (prev << 24));
-                            reinterpret_cast<uint4*>(a.rec_out)[(q < 4u ? gA : gB) + k] = rec;
+                            reinterpret_cast<uint4*>(a.rec_out)[(inB(q) ? gB : gA) + k] = rec;
                         }
                         __builtin_amdgcn_wave_barrier();
                         atomicAdd(etab + kA, kA == kB ? nA + nB : nA);
@@ -1946,7 +2012,7 @@ static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStrea
     using agnes::flow::flow;
     const void* fns[2] = {reinterpret_cast<const void*>(&flow<false, SM, R1, EVC, W64, REC, EDG, U>),
                           reinterpret_cast<const void*>(&flow<true, SM, R1, EVC, W64, REC, EDG, U>)};
-    const uint32_t lpw = agnes::flow::lds_bytes(SM, a->max_rounds, EVC, W64, EDG);
+    const uint32_t lpw = agnes::flow::lds_bytes(SM, a->max_rounds, EVC, W64, EDG, REC);
     const uint64_t wave_lds = (uint64_t)lpw * AGNES_WAVES_PER_BLOCK;
     const uint64_t pcb = agnes::align16((W64 ? 8ull : 4ull) * a->n_sets * a->n_vals);
     /* blocks per CU from the occupancy query; the LDS power table only where it
@@ -2037,23 +2103,40 @@ bool agnes_flow_supported(const agnes_tally_args* a) {
     const bool sm = (a->flags & AGNES_FLAG_STATE_MACHINE) != 0 && a->states != nullptr;
     const uint32_t waves = a->w64 ? 8u : (sm ? 12u : 16u);
     return a->max_rounds <= 15u && agnes::flow::lds_bytes(sm, a->max_rounds, a->ev_counts != nullptr, a->w64 != 0u,
-                                                          a->edges != 0u) * waves <= 160u * 1024u;
+                                                          a->edges != 0u, a->rec_out && !a->edges) * waves <= 160u * 1024u;
 }
 
-bool agnes_flow_counts_events(uint32_t flags, uint32_t max_rounds, bool edges) {
+bool agnes_flow_counts_events(uint32_t flags, uint32_t max_rounds, bool edges, bool rec) {
     const bool sm = (flags & AGNES_FLAG_STATE_MACHINE) != 0;
-    return max_rounds <= 15u && agnes::flow::lds_bytes(sm, max_rounds, true, false, edges) * (sm ? 12u : 16u) <= 160u * 1024u;
+    return max_rounds <= 15u &&
+           agnes::flow::lds_bytes(sm, max_rounds, true, false, edges, rec && !edges) * (sm ? 12u : 16u) <= 160u * 1024u;
 }
 
 bool agnes_flow_ragged_ok(const agnes_tally_args* a) {
-    /* the unaligned-stream kernel: u32 sums, codes, States and record counts */
-    return !a->w64 && !a->rec_out && !a->edges;
+    /* the unaligned-stream kernel: u32 sums (codes, States, record counts, records, edges) */
+    return !a->w64;
 }
 
 hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t st, bool ragged_pass, uint32_t* bp) {
     const bool sm = (a->flags & AGNES_FLAG_STATE_MACHINE) != 0 && a->states != nullptr;
     if (ragged_pass) { /* after the aligned kernel, with its partition */
         if (!a->ragged || !agnes_flow_ragged_ok(a)) return hipErrorInvalidValue;
+        if (a->rec_out && a->edges) {
+            if (!a->ev_counts) return hipErrorInvalidValue;
+            if (a->max_rounds == 1u)
+                return sm ? launch_flow_k<true, true, true, false, false, true, true>(a, num_cus, st, bp)
+                          : launch_flow_k<false, true, true, false, false, true, true>(a, num_cus, st, bp);
+            return sm ? launch_flow_k<true, false, true, false, false, true, true>(a, num_cus, st, bp)
+                      : launch_flow_k<false, false, true, false, false, true, true>(a, num_cus, st, bp);
+        }
+        if (a->rec_out) {
+            if (!a->ev_counts) return hipErrorInvalidValue;
+            if (a->max_rounds == 1u)
+                return sm ? launch_flow_k<true, true, true, false, true, false, true>(a, num_cus, st, bp)
+                          : launch_flow_k<false, true, true, false, true, false, true>(a, num_cus, st, bp);
+            return sm ? launch_flow_k<true, false, true, false, true, false, true>(a, num_cus, st, bp)
+                      : launch_flow_k<false, false, true, false, true, false, true>(a, num_cus, st, bp);
+        }
         if (a->ev_counts) {
             if (a->max_rounds == 1u)
                 return sm ? launch_flow_k<true, true, true, false, false, false, true>(a, num_cus, st, bp)

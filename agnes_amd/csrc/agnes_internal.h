@@ -133,7 +133,7 @@ hipError_t agnes_launch_edge_seg_walk(const agnes_vote_batch* vb, const uint8_t*
 hipError_t agnes_launch_edge_compact(const agnes_vote_batch* vb, const agnes_edge* seg, const uint64_t* offs,
                                      agnes_edge* out, hipStream_t stream, uint64_t cap, unsigned long long* ovf);
 /* the flow kernel can count event records (agnes_tally_events) in this configuration */
-bool agnes_flow_counts_events(uint32_t flags, uint32_t max_rounds, bool edges = false);
+bool agnes_flow_counts_events(uint32_t flags, uint32_t max_rounds, bool edges = false, bool rec = false);
 /* the batched State::apply pass over the codes a tally kernel left (agnes_apply.hip):
  * one instance per lane, skipping the instances deferred to the LIST kernel */
 bool agnes_apply_codes_supported(const agnes_tally_args* a);

@@ -266,6 +266,17 @@ def test_tally_edges_revisited_rounds(eng, nil):
     _tally_edges_check(eng, abi.config(abi.MODE_REFERENCE, 0, 5), hb, power)
 
 
+@pytest.mark.parametrize("name", ["c2r_small", "c3r_small", "c3r_plain", "c4r_ref"])
+def test_tally_edges_unaligned_streams(eng, name):
+    """Round 6: ragged instance lengths (abstention: offsets at every residue) on the flow
+    kernel's unaligned-stream variant -- its units split at any vote; with next-round
+    votes (c4r_ref) the per-key path"""
+    p, hb, power, cfg = _make(name)
+    assert (hb.offsets % 4 != 0).mean() > 0.5
+    states = _start_states(p.n_instances) if cfg.flags & abi.FLAG_STATE_MACHINE else None
+    assert len(_tally_edges_check(eng, cfg, hb, power, states)) > 0
+
+
 def test_tally_edges_walk_list_and_empty(eng):
     """ragged lengths (the flow kernel's walk list: the edge walk over the list), empty
     instances, invalid votes, one instance, an empty batch"""

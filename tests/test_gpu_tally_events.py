@@ -225,6 +225,23 @@ def test_tally_records_revisited_rounds(eng, nil):
     _check(eng, abi.config(abi.MODE_REFERENCE, 0, 5), hb, power)
 
 
+@pytest.mark.parametrize("rounds,extra", [(1, {}), (4, {}), (5, dict(higher_permille=50, dup_permille=60))])
+def test_tally_records_unaligned(eng, rounds, extra):
+    """Round 6: ragged instance lengths (5-12 % abstention: offsets at every residue) on
+    the flow kernel's unaligned-stream variant -- counts and records written by it, the
+    value of a nil PolkaValue / PrecommitValue from the lane, the segment's earlier lanes,
+    or the executor's slot carried in LDS (round_votes.rs:50-54); with next-round votes
+    (rounds revisited inside a chunk) the executors one at a time"""
+    p = abi.gen_params(seed=66 + rounds, n_instances=3000, n_vals=101, rounds_min=1, rounds_max=min(rounds, 4),
+                       nil_permille=450, absent_permille=60 if rounds > 1 else 120, **extra)
+    hb = ol.gen_batch(p)
+    assert (hb.offsets % 4 != 0).mean() > 0.5
+    power = ol.gen_power(66, 5, 101, abi.POWER_UNIFORM, 1, 1000)
+    _check(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, rounds), hb, power,
+           abi.new_states(3000, 1, abi.STEP_PREVOTE), in_place=False)
+    _check(eng, abi.config(abi.MODE_REFERENCE, 0, rounds), hb, power)
+
+
 def _shifted(eng, t, shift):
     """a copy of the u8 column t placed `shift` bytes past a 16-B boundary"""
     n = t.numel()
