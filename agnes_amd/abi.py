@@ -40,7 +40,6 @@ TYPE_MASKED = 0xFE  # agnes_dedup_mask's type byte of a later duplicate (AGNES_T
 FLAG_MASKED_REJECTED = 0x20  # agnes_tally_carried: AGNES_TYPE_MASKED votes -> REJECTED in the pass (agnes_dedup_reject inside)
 # route override (agnes.h AGNES_ROUTE_*): diagnostics / route-equivalence tests
 ROUTE_SHIFT, ROUTE_AUTO, ROUTE_INSTANCE, ROUTE_SPLIT, ROUTE_WIDE = 8, 0, 1, 2, 3
-FLAG_RECORDS_FUSED = 0x400  # agnes_tally_records: the flow kernel writes the records at any batch size
 EPOCH_BITS_SHIFT = 16
 
 

@@ -123,7 +123,7 @@ bool cfg_ok(const agnes_config* cfg) {
     return cfg && cfg->max_rounds >= 1 && cfg->max_rounds <= 256 && cfg->mode <= AGNES_MODE_DEDUP &&
            (cfg->flags & ~(AGNES_FLAG_ROUND_SKIP | AGNES_FLAG_STATE_MACHINE | AGNES_FLAG_DISTINCT_VALUES |
                            AGNES_FLAG_ONE_INSTANCE | AGNES_FLAG_WEIGHTS_CACHED | AGNES_FLAG_MASKED_REJECTED |
-                           (AGNES_ROUTE_MASK << AGNES_ROUTE_SHIFT) | AGNES_FLAG_RECORDS_FUSED |
+                           (AGNES_ROUTE_MASK << AGNES_ROUTE_SHIFT) |
                            AGNES_FLAG_EPOCH_BITS(0x1F))) == 0;
 }
 
@@ -303,9 +303,6 @@ int64_t agnes_lds_bytes_per_wave(const agnes_config* cfg, uint32_t n_vals) {
     return b > AGNES_MAX_LDS_PER_WAVE ? AGNES_E_UNSUPPORTED : b;
 }
 
-#ifndef AGNES_REC_FUSED_MIN_VOTES
-#define AGNES_REC_FUSED_MIN_VOTES (1ull << 28) /* several rounds: smaller batches take the emit pass */
-#endif
 static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_batch* b,
                       uint8_t* codes, const agnes_state* states_in, agnes_state* states,
                       agnes_carry_rec* carry, const agnes_set_info* sets, uint32_t n_sets, uint32_t sets_dom,
@@ -395,16 +392,6 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
                     agnes_flow_counts_events(cfg->flags, cfg->max_rounds, edges, rec_out != nullptr);
         if (flow) a.ev_counts = ev_counts;
         if (flow && rec_out) a.rec_out = rec_out; /* agnes_tally_records / _edges: the flow kernel writes them too */
-        /* several rounds: the fused records variant runs at 2 waves per SIMD (its VGPRs),
-         * which pays on a large batch but not on a small one, where the tally's tail
-         * grows with it: C3 (7.5e8 votes) 4.83 ms fused vs 5.19 through the emit pass,
-         * its 8-GPU shard (9.4e7) 0.95 vs 0.80 */
-        if (rec_out && !edges && cfg->max_rounds > 1u && b->n_votes < AGNES_REC_FUSED_MIN_VOTES &&
-            !(cfg->flags & AGNES_FLAG_RECORDS_FUSED)) {
-            a.ev_counts = nullptr;
-            a.rec_out = nullptr;
-            flow = false;
-        }
         if (flow && edges) a.edges = 1u;
         if (counted) *counted = flow;
         /* the per-instance route (DEDUP, RoundSkip, or forced) counts them in tally_fast:

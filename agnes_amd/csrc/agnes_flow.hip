@@ -253,7 +253,12 @@ struct Hdr {
 #define AGNES_FLOW_XWPE 3 /* the records / edges variants, one round */
 #endif
 #ifndef AGNES_FLOW_XWPE_R
-#define AGNES_FLOW_XWPE_R 2 /* ... several rounds (their registers spill at 3 waves per SIMD) */
+#define AGNES_FLOW_XWPE_R 3 /* ... several rounds: a few spills at 3 waves per SIMD cost less than
+                             * 2 waves (C3 records 4.89 -> 4.11 ms, its shard 0.75 -> 0.64) */
+#endif
+#ifndef AGNES_FLOW_EWPE_R
+#define AGNES_FLOW_EWPE_R 2 /* the edges, several rounds: at 3 waves their spills cost more
+                             * (C3 edges 3.85 -> 4.30 ms) */
 #endif
 /* REC (agnes_tally_records): the event records themselves, segmented by instance.
  * EDG (agnes_tally_edges): the edge summary instead -- etab counts each instance's
@@ -270,7 +275,7 @@ struct Hdr {
  * to the walk list).  The aligned kernel (U = false) runs first and leaves these batches
  * to this one (flag AGNES_RAG_FLAG): the aligned kernel's code is unchanged by them. */
 template <bool PC, bool SM, bool R1, bool EVC, bool W64, bool REC = false, bool EDG = false, bool U = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES_FLOW_W64_WPE : ((REC || EDG) ? (R1 ? AGNES_FLOW_XWPE : AGNES_FLOW_XWPE_R) : AGNES_FLOW_WPE)))) void flow(agnes_tally_args a, uint32_t lds_per_wave) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES_FLOW_W64_WPE : ((REC || EDG) ? (R1 ? AGNES_FLOW_XWPE : (EDG ? AGNES_FLOW_EWPE_R : AGNES_FLOW_XWPE_R)) : AGNES_FLOW_WPE)))) void flow(agnes_tally_args a, uint32_t lds_per_wave) {
     static_assert(!REC || (EVC && !W64), "records: with the record counts, u32 sums");
     static_assert(!EDG || (EVC && !W64 && !REC), "edges: the counts are the edges', u32 sums");
     static_assert(!U || !W64, "unaligned streams: u32 sums");

@@ -441,8 +441,6 @@ def main():
                     help="force a tally route (AGNES_ROUTE_*; diagnostics: every route gives identical results)")
     ap.add_argument("--segments", type=int, default=0,
                     help="c5/c5d: segments per GPU (one wave each; default: the workload's)")
-    ap.add_argument("--records-fused", action="store_true",
-                    help="also time agnes_tally_records with AGNES_FLAG_RECORDS_FUSED (diagnostics)")
     args = ap.parse_args()
 
     rank, world, local = adist.env()
@@ -542,12 +540,6 @@ def main():
     tr = tally_records_timed(eng, cfg, batch, codes, st0, states, args.steps, ev_offs, ev_recs)
     tr["records_ms"] = tr["ms_per_call"] - elapsed * 1e3 / args.steps
     events["tally_records"] = tr
-    if args.records_fused:  # diagnostics: the fused records route where the library would take the emit pass
-        cf = type(cfg).from_buffer_copy(cfg)
-        cf.flags |= abi.FLAG_RECORDS_FUSED
-        tf = tally_records_timed(eng, cf, batch, codes, st0, states, args.steps, ev_offs, ev_recs)
-        tf["records_ms"] = tf["ms_per_call"] - elapsed * 1e3 / args.steps
-        events["tally_records_fused"] = tf
     ed_offs = edges.pop("_offsets")
     tg = tally_edges_timed(eng, cfg, batch, codes, st0, states, args.steps, ed_offs, edges["_records"])
     tg["edges_ms"] = tg["ms_per_call"] - elapsed * 1e3 / args.steps  # over the tally step alone

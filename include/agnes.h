@@ -215,11 +215,6 @@ typedef struct agnes_state {
 #define AGNES_ROUTE_SPLIT 2u
 #define AGNES_ROUTE_WIDE 3u
 #define AGNES_FLAG_ROUTE(r) ((uint32_t)(r) << AGNES_ROUTE_SHIFT)
-/* agnes_tally_records with several rounds: the flow kernel writes the records whatever
- * the batch's size (without it, batches under 2^28 votes take the emit pass: the fused
- * variant's 2 waves per SIMD only pay on large batches).  Identical records either way;
- * the route-equivalence tests set it. */
-#define AGNES_FLAG_RECORDS_FUSED 0x400u
 /* Bits 16..20 of agnes_config.flags: minimum bits the DEDUP / RoundSkip first-vote
  * tables spend on a vote's index inside its instance (0 = just enough for the
  * batch).  More index bits leave fewer epochs per table fill, so the tables are
@@ -738,8 +733,7 @@ uint64_t agnes_events_capacity(const agnes_config* cfg, const agnes_vote_batch* 
 
 /* The same records SEGMENTED by instance (round 5): no scan between the tally and the
  * records, so on the flow route (REFERENCE without RoundSkip, max_rounds <= 15, every
- * offset a multiple of 4 -- the C2 / C3 streams; with several rounds, batches of at
- * least 2^28 votes, or with AGNES_FLAG_RECORDS_FUSED) the
+ * and max_rounds <= 15: the C2 / C3 streams and their ragged variants) the
  * tally kernel writes them itself while the votes are in registers: the records cost no
  * second pass over the votes.
  * Instance i's records are out[seg(i) + k], k < counts[i], in vote order, with

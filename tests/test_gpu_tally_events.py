@@ -64,11 +64,6 @@ def _check(eng, cfg, hb, power, states=None, in_place=True):
     assert np.array_equal(e_offs.cpu().numpy().view(np.uint64), g_offs)
     assert e_recs.cpu().numpy().tobytes() == out[:n].cpu().numpy().tobytes()
     _check_records(eng, cfg, hb, db, states, in_place, o_codes, o_states, o_offs, o_ev)
-    if cfg.max_rounds > 1:
-        # several rounds: batches under 2^28 votes take the emit pass; the fused records
-        # variant of the flow kernel at any size with AGNES_FLAG_RECORDS_FUSED
-        fused = abi.config(cfg.mode, cfg.flags | abi.FLAG_RECORDS_FUSED, cfg.max_rounds, cfg.reserved)
-        _check_records(eng, fused, hb, db, states, in_place, o_codes, o_states, o_offs, o_ev)
     return o_ev
 
 
