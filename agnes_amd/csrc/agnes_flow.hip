@@ -243,8 +243,11 @@ struct Hdr {
 #ifndef AGNES_FLOW_WPE
 #define AGNES_FLOW_WPE 3
 #endif
+#ifndef AGNES_FLOW_RG
+#define AGNES_FLOW_RG 1 /* the u32 kernels also walk unaligned streams (0, A/B builds: they go to the walk list) */
+#endif
 #ifndef AGNES_FLOW_FORCE_U
-#define AGNES_FLOW_FORCE_U 0 /* A/B builds only: every stream to the unaligned-stream kernel (the aligned one not launched) */
+#define AGNES_FLOW_FORCE_U 0 /* A/B builds only: every stream through the unaligned-stream loop */
 #endif
 #ifndef AGNES_FLOW_CODE_VMCNT
 #define AGNES_FLOW_CODE_VMCNT 1
@@ -265,26 +268,28 @@ struct Hdr {
  * edges and the 16-B agnes_edge records go to the instance's segment (agnes_edges.hip's
  * definition, orc_edges: a valid vote is an edge when its executor's state, level |
  * last message << 4, changes). */
-/* U (round 6): the batches whose instance offsets are NOT all multiples of 4 -- the ragged
- * streams of validator sets with absent validators.  The same chunk walk, but a lane's
- * eight votes split at any position: the instance (or, in runs mode, the round run)
- * starting inside the lane owns votes sp .. 7 (its PART B), the one running into the
- * lane votes 0 .. sp - 1 (PART A); the per-vote choices the aligned kernel makes by the
- * unit (vote < 4) it makes by the part (vote < sp).  Every instance of such a batch holds
- * 0 or at least 8 votes, so a lane holds at most one instance start (else the batch goes
- * to the walk list).  The aligned kernel (U = false) runs first and leaves these batches
- * to this one (flag AGNES_RAG_FLAG): the aligned kernel's code is unchanged by them. */
-template <bool PC, bool SM, bool R1, bool EVC, bool W64, bool REC = false, bool EDG = false, bool U = false>
+/* RG (round 6): the kernel also walks the batches whose instance offsets are NOT all
+ * multiples of 4 -- the ragged streams of validator sets with absent validators -- in a
+ * second copy of the chunk loop (U), chosen per batch.  Its lane's eight votes split at any
+ * position: the instance (or, in runs mode, the round run) starting inside the lane owns
+ * votes sp .. 7 (its PART B), the one running into the lane votes 0 .. sp - 1 (PART A);
+ * the per-vote choices the aligned loop makes by the unit (vote < 4) it makes by the part
+ * (vote < sp).  Every instance of such a batch holds 0 or at least 8 votes, so a lane holds
+ * at most one instance start (else the batch goes to the walk list).  The aligned loop's
+ * code is the same whether the kernel holds the other one or not; the two share the queue,
+ * so a batch costs nothing in the loop that does not walk it. */
+template <bool PC, bool SM, bool R1, bool EVC, bool W64, bool REC = false, bool EDG = false, bool RG = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES_FLOW_W64_WPE : ((REC || EDG) ? (R1 ? AGNES_FLOW_XWPE : (EDG ? AGNES_FLOW_EWPE_R : AGNES_FLOW_XWPE_R)) : AGNES_FLOW_WPE)))) void flow(agnes_tally_args a, uint32_t lds_per_wave) {
     static_assert(!REC || (EVC && !W64), "records: with the record counts, u32 sums");
     static_assert(!EDG || (EVC && !W64 && !REC), "edges: the counts are the edges', u32 sums");
-    static_assert(!U || !W64, "unaligned streams: u32 sums");
-    /* the unaligned kernel: nothing to do unless the aligned one left it batches (any of its
-     * flags: 4 per lane) */
-    if (U && !AGNES_FLOW_FORCE_U) {
-        static_assert(AGNES_QUEUE_N == 256 && AGNES_RAG_FLAG % 4 == 0, "the flags: one uint4 per lane");
-        const uint4 f = reinterpret_cast<const uint4*>(a.list_count + AGNES_RAG_FLAG)[lane_id()];
-        if (!ballot((f.x | f.y | f.z | f.w) != 0u)) return;
+    static_assert(!RG || !W64, "unaligned streams: u32 sums");
+    /* the gate (flow_prep's words, 4 per lane): the aligned kernel runs when every instance
+     * offset is a multiple of 4, the RG one (its register allocation holds both loops, which
+     * costs the aligned loop ~2-5 %) when some is not */
+    if (a.gate) {
+        static_assert(AGNES_PREP_SLOTS == 256 && AGNES_PREP_SLOT0 % 4 == 0, "the gate: one uint4 per lane");
+        const uint4 f = reinterpret_cast<const uint4*>(a.list_count + AGNES_PREP_SLOT0)[lane_id()];
+        if ((ballot((f.x | f.y | f.z | f.w) != 0u) != 0ull) != (a.gate == 2u)) return;
     }
     constexpr uint32_t RW = W64 ? RECW64 : RECW; /* record words */
 
@@ -333,7 +338,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
     /* ---- work queue: batches of FB, then SMALLB ones for the tail ---- */
     const uint32_t qn = gridDim.x < AGNES_FLOW_QN ? gridDim.x : AGNES_FLOW_QN;
     const uint32_t qk = blockIdx.x % qn;
-    uint32_t* const ctr = a.list_count + (U ? (uint32_t)AGNES_RAG_QUEUE : 1u) + qk; /* (U: its own counters) */
+    uint32_t* const ctr = a.list_count + 1u + qk;
     /* batch size: FB, or (launcher) fewer for a batch too small to give every wave
      * several batches -- the makespan is a wave's last batch */
     const uint32_t fb = a.batch && a.batch < FB ? a.batch : FB;
@@ -379,14 +384,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
         const uint64_t oe = u64of(shfl(h.olo, lane + 1u), shfl(h.ohi, lane + 1u));
         const uint64_t len = il && oe > ob ? oe - ob : 0ull;
         h.ln = len < (1ull << 31) ? (uint32_t)len : (1u << 31);
-        /* rag: some offset off a multiple of 4 -- the U kernel's batch (with a.ragged), which
-         * checks the rest of it (U: 2 when an instance holds 1 .. 7 votes: the walk list) */
-        h.rag = (U && AGNES_FLOW_FORCE_U) || ballot(lane <= m && (h.olo & 3u) != 0u) != 0ull;
-        if (U) h.rag = h.rag ? 1u + (ballot(il && len > 0ull && len < 8ull) != 0ull) : 0u;
-        /* the other kernel's batch: no set constants, no stage 3 */
-        const bool other = U ? !h.rag : (h.rag && a.ragged);
+        /* rag: some offset off a multiple of 4 -- the U loop's batch (RG; else the walk list's),
+         * 2 when an instance also holds 1 .. 7 votes (the walk list's) */
+        h.rag = (RG && AGNES_FLOW_FORCE_U) || ballot(lane <= m && (h.olo & 3u) != 0u) != 0ull;
+        if (RG) h.rag = h.rag ? 1u + (ballot(il && len > 0ull && len < 8ull) != 0ull) : 0u;
         uint32_t q2 = 0, mp = 0, fa = 2, q2h = 0, mph = 0;
-        if (!other && il && h.hs < ns) {
+        if (il && h.hs < ns) {
             const agnes_set_info* const si = a.sets + h.hs;
             if (W64) {
                 q2 = (uint32_t)si->q2w;
@@ -408,9 +411,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
         /* stream: the offsets and, at stage 3, the sets in the flow domain */
         const bool badl = lane < m && oe < ob;
         const uint64_t O0 = u64of(rdl(h.olo, 0u), rdl(h.ohi, 0u)), Om = u64of(rdl(h.olo, m), rdl(h.ohi, m));
-        h.stream = !other && m > 0u && !ballot(badl) && Om - O0 < (1ull << 30);
+        h.stream = m > 0u && !ballot(badl) && Om - O0 < (1ull << 30);
         h.go = 0;
-        h.stage = other ? 3u : 2u;
+        h.stage = 2u;
     };
     auto hdr3 = [&](Hdr& h) { /* stage 3: quorum thresholds; a flow stream or the walk list */
         const uint32_t m = h.e0 - h.s0;
@@ -437,12 +440,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
         h.q2 = q2;
         h.stream = h.stream && !ballot(!fl);
         h.stage = 3;
-        /* this kernel walks it: the aligned one its aligned streams, the U one the others whose
-         * instances all hold 0 or >= 8 votes */
-        h.go = U ? (h.stream && h.rag == 1u) : (h.stream && !h.rag);
+        /* this kernel walks it: the aligned streams, and (RG) the others whose instances all
+         * hold 0 or >= 8 votes */
+        h.go = RG ? (h.stream && h.rag != 2u) : (h.stream && !h.rag);
     };
     uint32_t spar = 0; /* States staging buffer of the current batch */
-    bool rag_told = false; /* (the aligned kernel) its counter's flag for the U kernel is set */
     /* the last flush sent a whole chunk's codes as ONE store with every lane active and
      * no DMA has been issued since: the chunk top's wait may leave that store in flight */
     bool dc_one = false;
@@ -486,6 +488,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
     uint64_t dc_at = ~0ull;
     uint32_t dc0 = 0, dc1 = 0, dc_act = 0; /* dc_act: bit 0 unit A, bit 1 unit B active */
     uint32_t dcm0 = 0, dcm1 = 0;           /* (U) the active votes' bytes (a lane that is not all active) */
+    bool dc_u = false;                     /* the deferred codes are the U loop's */
     auto flush = [&]() {
         dc_one = false;
         if (dc_at != ~0ull) {
@@ -495,7 +498,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
             } else {
                 if (dc_act == 3u) {
                     sstore8(a.codes + dc_at, o8, dc0, dc1);
-                } else if (U) { /* a stream's first or last lanes: byte stores, the neighbours' codes are another wave's */
+                } else if (RG && dc_u) { /* a stream's first or last lanes: byte stores, the neighbours' codes are another wave's */
 #pragma unroll
                     for (uint32_t q = 0; q < LV; ++q)
                         if ((((q < 4u ? dcm0 : dcm1) >> (8u * (q & 3u))) & 1u) != 0u)
@@ -565,8 +568,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
        * (only for offsets that bound a stream inside the columns; hdr2 decides the rest) */
         const uint32_t m = H.e0 - H.s0;
         const uint64_t O0 = u64of(rdl(H.olo, 0u), rdl(H.ohi, 0u)), Om = u64of(rdl(H.olo, m), rdl(H.ohi, m));
-        const bool ragb = (U && AGNES_FLOW_FORCE_U) || ballot(lane <= m && (H.olo & 3u) != 0u) != 0ull;
-        if (Om > O0 && Om - O0 < (1ull << 30) && (U ? ragb : !(ragb && a.ragged))) {
+        const bool ragb = ballot(lane <= m && (H.olo & 3u) != 0u) != 0ull;
+        if (Om > O0 && Om - O0 < (1ull << 30) && (RG || !ragb)) {
             const uint64_t Sa0 = O0 & ~127ull;
             dma_chunk(Sa0, (uint32_t)(O0 - Sa0), (uint32_t)(Om - Sa0));
             pf_at = Sa0;
@@ -588,15 +591,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                 dma_wait();
                 pf_at = ~0ull;
             }
-            /* the aligned kernel leaves the unaligned streams to the U kernel (a.ragged), which
-             * leaves the aligned ones and the rest to the aligned kernel; the walk list
-             * (agnes_sweep.hip) takes the batches that are no stream of either */
-            const bool walk = U ? H.rag != 0u : (!H.rag || !a.ragged);
-            if (!U && !walk && !rag_told) { /* (a plain store, once per wave: idempotent) */
-                if (lane == 0) a.list_count[AGNES_RAG_FLAG + qk] = 1u;
-                rag_told = true;
-            }
-            if (walk) {
+            /* the walk list (agnes_sweep.hip) takes the batches that are no stream of this kernel */
+            {
                 uint32_t w0 = 0;
                 if (lane == 0) w0 = atomicAdd(a.list_count + AGNES_WALK_COUNT, m);
                 w0 = rdl(w0, 0u);
@@ -625,6 +621,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
             const uint32_t relv = lane <= m ? rl : 0x7FFFFFFFu;
             const uint64_t mm64 = (1ull << m) - 1ull;
 
+            /* the chunks: the aligned loop, or (RG, an unaligned stream) the U loop */
+            auto chunks = [&](auto u_t) {
+            constexpr bool U = decltype(u_t)::value;
             for (uint32_t rc = 0; rc < Lend; rc += CH) {
                 FDIAG(++dg_c;)
                 const uint64_t c = Sa + rc;
@@ -1939,7 +1938,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
                     dc_act = (actA ? 1u : 0u) | (actB ? 2u : 0u);
                 }
                 dc_at = c;
+                dc_u = U;
                 __builtin_amdgcn_wave_barrier();
+            }
+            };
+            if constexpr (RG) {
+                if (H.rag) chunks(std::true_type{});
+                else chunks(std::false_type{});
+            } else {
+                chunks(std::false_type{});
             }
         }
         /* batch end: the record counts and the States out (a walk-list batch's are the
@@ -2007,11 +2014,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
 /* ------------------------------------------------------------------ */
 /* launcher                                                            */
 
-/* One flow kernel (U: the unaligned-stream variant).  The aligned kernel sizes the batches
- * (bp: batch, tail batch, tail instances) and the U kernel walks the same partition, so the
- * two classify every batch alike. */
+/* One flow kernel (RG: with the unaligned-stream loop) */
 template <bool SM, bool R1, bool EVC, bool W64, bool REC = false, bool EDG = false, bool U = false>
-static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStream_t st, uint32_t* bp) {
+static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStream_t st) {
     const uint32_t n = a->vb.n_instances;
     if (n == 0) return hipSuccess;
     using agnes::flow::flow;
@@ -2052,11 +2057,7 @@ static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStrea
     b.power_cache = o->pc ? (uint32_t)pcb : 0u;
     const uint64_t lds = wave_lds + b.power_cache;
     const void* fn = fns[o->pc ? 1 : 0];
-    if (U) { /* the aligned kernel's partition */
-        b.batch = bp[0];
-        b.tail_batch = bp[1];
-        b.tail_n = bp[2];
-    } else { /* batches of FB, fewer when that leaves a wave under AGNES_FLOW_BATCHES_PER_WAVE */
+    { /* batches of FB, fewer when that leaves a wave under AGNES_FLOW_BATCHES_PER_WAVE */
         const uint64_t waves = (uint64_t)(num_cus > 0 ? num_cus : 256) * (uint64_t)o->per_cu * AGNES_WAVES_PER_BLOCK;
         uint64_t fbx = AGNES_FLOW_BATCHES_PER_WAVE ? (uint64_t)n / (waves * AGNES_FLOW_BATCHES_PER_WAVE) : agnes::flow::FB;
         fbx = fbx < 4u ? 4u : (fbx > agnes::flow::FB ? agnes::flow::FB : fbx);
@@ -2074,9 +2075,6 @@ static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStrea
             b.tail_batch = (uint32_t)tb;
             b.tail_n = (uint32_t)tn;
         }
-        bp[0] = b.batch;
-        bp[1] = b.tail_batch;
-        bp[2] = b.tail_n;
     }
     if (lds > 48u * 1024u) {
         hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -2087,7 +2085,6 @@ static hipError_t launch_flow_k(const agnes_tally_args* a, int num_cus, hipStrea
     const uint64_t cap = ncu * (uint64_t)o->per_cu;
     if (blocks > cap) blocks = cap;
     if (blocks == 0) blocks = 1;
-    if (!U && AGNES_FLOW_FORCE_U && b.ragged) return hipSuccess; /* (A/B builds: the partition only) */
     if (o->pc) hipLaunchKernelGGL((flow<true, SM, R1, EVC, W64, REC, EDG, U>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
     else hipLaunchKernelGGL((flow<false, SM, R1, EVC, W64, REC, EDG, U>), dim3((uint32_t)blocks), dim3(256), (size_t)lds, st, b, lpw);
     return hipGetLastError();
@@ -2117,72 +2114,83 @@ bool agnes_flow_counts_events(uint32_t flags, uint32_t max_rounds, bool edges, b
            agnes::flow::lds_bytes(sm, max_rounds, true, false, edges, rec && !edges) * (sm ? 12u : 16u) <= 160u * 1024u;
 }
 
-bool agnes_flow_ragged_ok(const agnes_tally_args* a) {
-    /* the unaligned-stream kernel: u32 sums (codes, States, record counts, records, edges) */
-    return !a->w64;
-}
-
-hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t st, bool ragged_pass, uint32_t* bp) {
-    const bool sm = (a->flags & AGNES_FLAG_STATE_MACHINE) != 0 && a->states != nullptr;
-    if (ragged_pass) { /* after the aligned kernel, with its partition */
-        if (!a->ragged || !agnes_flow_ragged_ok(a)) return hipErrorInvalidValue;
-        if (a->rec_out && a->edges) {
-            if (!a->ev_counts) return hipErrorInvalidValue;
-            if (a->max_rounds == 1u)
-                return sm ? launch_flow_k<true, true, true, false, false, true, true>(a, num_cus, st, bp)
-                          : launch_flow_k<false, true, true, false, false, true, true>(a, num_cus, st, bp);
-            return sm ? launch_flow_k<true, false, true, false, false, true, true>(a, num_cus, st, bp)
-                      : launch_flow_k<false, false, true, false, false, true, true>(a, num_cus, st, bp);
-        }
-        if (a->rec_out) {
-            if (!a->ev_counts) return hipErrorInvalidValue;
-            if (a->max_rounds == 1u)
-                return sm ? launch_flow_k<true, true, true, false, true, false, true>(a, num_cus, st, bp)
-                          : launch_flow_k<false, true, true, false, true, false, true>(a, num_cus, st, bp);
-            return sm ? launch_flow_k<true, false, true, false, true, false, true>(a, num_cus, st, bp)
-                      : launch_flow_k<false, false, true, false, true, false, true>(a, num_cus, st, bp);
-        }
-        if (a->ev_counts) {
-            if (a->max_rounds == 1u)
-                return sm ? launch_flow_k<true, true, true, false, false, false, true>(a, num_cus, st, bp)
-                          : launch_flow_k<false, true, true, false, false, false, true>(a, num_cus, st, bp);
-            return sm ? launch_flow_k<true, false, true, false, false, false, true>(a, num_cus, st, bp)
-                      : launch_flow_k<false, false, true, false, false, false, true>(a, num_cus, st, bp);
-        }
-        if (a->max_rounds == 1u)
-            return sm ? launch_flow_k<true, true, false, false, false, false, true>(a, num_cus, st, bp)
-                      : launch_flow_k<false, true, false, false, false, false, true>(a, num_cus, st, bp);
-        return sm ? launch_flow_k<true, false, false, false, false, false, true>(a, num_cus, st, bp)
-                  : launch_flow_k<false, false, false, false, false, false, true>(a, num_cus, st, bp);
-    }
-    if (a->w64) { /* the u64 domain: no record counts (agnes_sweep_supported) */
-        if (a->ev_counts) return hipErrorInvalidValue;
-        if (a->max_rounds == 1u)
-            return sm ? launch_flow_k<true, true, false, true>(a, num_cus, st, bp) : launch_flow_k<false, true, false, true>(a, num_cus, st, bp);
-        return sm ? launch_flow_k<true, false, false, true>(a, num_cus, st, bp) : launch_flow_k<false, false, false, true>(a, num_cus, st, bp);
-    }
+template <bool G>
+static hipError_t launch_flow_u32(const agnes_tally_args* a, int num_cus, hipStream_t st, bool sm, bool r1) {
     if (a->rec_out && a->edges) { /* agnes_tally_edges: the edge counts and records */
         if (!a->ev_counts) return hipErrorInvalidValue;
-        if (a->max_rounds == 1u)
-            return sm ? launch_flow_k<true, true, true, false, false, true>(a, num_cus, st, bp)
-                      : launch_flow_k<false, true, true, false, false, true>(a, num_cus, st, bp);
-        return sm ? launch_flow_k<true, false, true, false, false, true>(a, num_cus, st, bp)
-                  : launch_flow_k<false, false, true, false, false, true>(a, num_cus, st, bp);
+        if (r1) return sm ? launch_flow_k<true, true, true, false, false, true, G>(a, num_cus, st)
+                          : launch_flow_k<false, true, true, false, false, true, G>(a, num_cus, st);
+        return sm ? launch_flow_k<true, false, true, false, false, true, G>(a, num_cus, st)
+                  : launch_flow_k<false, false, true, false, false, true, G>(a, num_cus, st);
     }
     if (a->rec_out) { /* agnes_tally_records: counts and the records themselves */
         if (!a->ev_counts) return hipErrorInvalidValue;
-        if (a->max_rounds == 1u)
-            return sm ? launch_flow_k<true, true, true, false, true>(a, num_cus, st, bp)
-                      : launch_flow_k<false, true, true, false, true>(a, num_cus, st, bp);
-        return sm ? launch_flow_k<true, false, true, false, true>(a, num_cus, st, bp)
-                  : launch_flow_k<false, false, true, false, true>(a, num_cus, st, bp);
+        if (r1) return sm ? launch_flow_k<true, true, true, false, true, false, G>(a, num_cus, st)
+                          : launch_flow_k<false, true, true, false, true, false, G>(a, num_cus, st);
+        return sm ? launch_flow_k<true, false, true, false, true, false, G>(a, num_cus, st)
+                  : launch_flow_k<false, false, true, false, true, false, G>(a, num_cus, st);
     }
     if (a->ev_counts) {
-        if (a->max_rounds == 1u)
-            return sm ? launch_flow_k<true, true, true, false>(a, num_cus, st, bp) : launch_flow_k<false, true, true, false>(a, num_cus, st, bp);
-        return sm ? launch_flow_k<true, false, true, false>(a, num_cus, st, bp) : launch_flow_k<false, false, true, false>(a, num_cus, st, bp);
+        if (r1) return sm ? launch_flow_k<true, true, true, false, false, false, G>(a, num_cus, st)
+                          : launch_flow_k<false, true, true, false, false, false, G>(a, num_cus, st);
+        return sm ? launch_flow_k<true, false, true, false, false, false, G>(a, num_cus, st)
+                  : launch_flow_k<false, false, true, false, false, false, G>(a, num_cus, st);
     }
-    if (a->max_rounds == 1u)
-        return sm ? launch_flow_k<true, true, false, false>(a, num_cus, st, bp) : launch_flow_k<false, true, false, false>(a, num_cus, st, bp);
-    return sm ? launch_flow_k<true, false, false, false>(a, num_cus, st, bp) : launch_flow_k<false, false, false, false>(a, num_cus, st, bp);
+    if (r1) return sm ? launch_flow_k<true, true, false, false, false, false, G>(a, num_cus, st)
+                      : launch_flow_k<false, true, false, false, false, false, G>(a, num_cus, st);
+    return sm ? launch_flow_k<true, false, false, false, false, false, G>(a, num_cus, st)
+              : launch_flow_k<false, false, false, false, false, false, G>(a, num_cus, st);
+}
+
+namespace agnes {
+namespace flow {
+/* the gate words, one per block (its share of the offsets holds one off a multiple of 4),
+ * and the call's counters zeroed (zw words at zb: the memset this launch replaces) */
+__global__ __launch_bounds__(256) void flow_prep(const uint64_t* offsets, uint64_t n1, uint32_t* zb, uint32_t zw,
+                                                 uint32_t* slots) {
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t < zw) zb[t] = 0u;
+    const uint64_t S = (uint64_t)gridDim.x * 256u;
+    uint64_t acc = 0, i = t;
+    for (; i + 3u * S < n1; i += 4u * S) /* four independent loads in flight */
+        acc |= offsets[i] | offsets[i + S] | offsets[i + 2u * S] | offsets[i + 3u * S];
+    for (; i < n1; i += S) acc |= offsets[i];
+    const bool odd = __syncthreads_or((acc & 3u) != 0u);
+    if (threadIdx.x == 0) slots[blockIdx.x] = odd ? 1u : 0u;
+}
+} // namespace flow
+} // namespace agnes
+
+bool agnes_flow_rg(const agnes_tally_args* a) { return AGNES_FLOW_RG && !a->w64; }
+
+bool agnes_flow_rg_build() { return AGNES_FLOW_RG != 0; }
+
+hipError_t agnes_launch_flow_prep(const agnes_tally_args* a, hipStream_t st) {
+    /* the invalid count's stripes and the queue words, up to the gate words */
+    constexpr uint32_t ZW = AGNES_ERR_BYTES / 4u + AGNES_PREP_SLOT0;
+    static_assert(ZW <= AGNES_PREP_SLOTS * 256u, "one word per thread");
+    hipLaunchKernelGGL(agnes::flow::flow_prep, dim3(AGNES_PREP_SLOTS), dim3(256), 0, st, a->vb.offsets,
+                       (uint64_t)a->vb.n_instances + 1u, reinterpret_cast<uint32_t*>(a->n_invalid),
+                       a->prep_zero ? ZW : 0u, a->list_count + AGNES_PREP_SLOT0);
+    return hipGetLastError();
+}
+
+hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t st, bool rg) {
+    const bool sm = (a->flags & AGNES_FLAG_STATE_MACHINE) != 0 && a->states != nullptr;
+    const bool r1 = a->max_rounds == 1u;
+    if (a->w64) { /* the u64 domain: no record counts (agnes_sweep_supported); unaligned streams to the walk */
+        if (a->ev_counts || rg) return hipErrorInvalidValue;
+        if (r1) return sm ? launch_flow_k<true, true, false, true>(a, num_cus, st) : launch_flow_k<false, true, false, true>(a, num_cus, st);
+        return sm ? launch_flow_k<true, false, false, true>(a, num_cus, st) : launch_flow_k<false, false, false, true>(a, num_cus, st);
+    }
+#if AGNES_FLOW_FORCE_U
+    { /* (A/B builds) every stream through the RG kernel's unaligned-stream loop, ungated */
+        if (!rg) return hipSuccess;
+        agnes_tally_args b = *a;
+        b.gate = 0u;
+        return launch_flow_u32<true>(&b, num_cus, st, sm, r1);
+    }
+#endif
+    if (rg) return launch_flow_u32<AGNES_FLOW_RG != 0>(a, num_cus, st, sm, r1);
+    return launch_flow_u32<false>(a, num_cus, st, sm, r1);
 }

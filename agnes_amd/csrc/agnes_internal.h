@@ -68,8 +68,9 @@ typedef struct agnes_tally_args {
     uint32_t w64;         /* the u64 fast domain (agnes_set_info.w64 sets outside the u32 one):
                              tally_fast with u64 sums, the apply pass tests the same deferral */
     uint32_t edges;       /* agnes_tally_edges: ev_counts / rec_out are the edge summary's (EDG) */
-    uint32_t ragged;      /* flow: the unaligned-stream kernel (U) runs after the aligned one, which
-                             leaves it the batches whose offsets are not all multiples of 4 */
+    uint32_t gate;        /* flow: 0 runs; 1 returns at once when flow_prep found an unaligned
+                             instance offset, 2 when it found none */
+    uint32_t prep_zero;   /* flow_prep zeroes the counters (the caller skipped their memset) */
     void* rec_out;        /* optional (agnes_tally_records): agnes_seg_event [n_votes], instance i's
                              records at [offsets[i], offsets[i] + ev_counts[i]) -- the flow
                              kernel writes them (REC); every other route's emit pass does */
@@ -106,10 +107,16 @@ bool agnes_sweep_supported(const agnes_tally_args* a);
 hipError_t agnes_launch_sweep(const agnes_tally_args* a, int num_cus, hipStream_t stream);
 /* the 8-votes-per-lane flow kernel (agnes_flow.hip) for the sweep route's streams */
 bool agnes_flow_supported(const agnes_tally_args* a);
-/* ragged_pass: the unaligned-stream variant, after the aligned kernel (bp: the batch
- * partition the aligned launch chose: batch, tail batch, tail instances) */
-bool agnes_flow_ragged_ok(const agnes_tally_args* a);
-hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t stream, bool ragged_pass, uint32_t* bp);
+/* rg (u32 sums): the kernel that also holds the unaligned-stream loop -- a batch whose
+ * offsets are not all multiples of 4 is walked by it unless one of its instances holds
+ * 1 .. 7 votes (then: the walk list; without rg every such batch goes there) */
+hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t stream, bool rg);
+/* flow_prep: the gate words (AGNES_PREP_SLOT0) for a.gate, and (a.prep_zero) the counters
+ * zeroed in the same launch */
+hipError_t agnes_launch_flow_prep(const agnes_tally_args* a, hipStream_t stream);
+bool agnes_flow_rg_build();
+/* the u32 flow route has the unaligned-stream kernel (AGNES_FLOW_RG builds) */
+bool agnes_flow_rg(const agnes_tally_args* a);
 /* the segmented records (agnes_tally_records) of every instance, or of the ones on a
  * list (the flow route's walk list; list_n on the device), one lane per instance; and
  * the dense stream from them (offs: the exclusive scan of the counts) */
@@ -231,12 +238,11 @@ hipError_t agnes_launch_dedup_reject(const uint8_t* type_masked, uint64_t n, uin
 #define AGNES_QUEUE_N 256
 #define AGNES_WALK_COUNT (AGNES_QUEUE_N + 1)
 #define AGNES_WALK_QUEUE (AGNES_QUEUE_N + 2)
-/* the flow kernel's unaligned-stream variant: AGNES_QUEUE_N flags the aligned kernel sets
- * when it leaves it batches (one per work-queue counter, set once per wave: thousands of
- * stores to one word serialise), then its own AGNES_QUEUE_N work-queue counters */
-#define AGNES_RAG_FLAG (AGNES_QUEUE_N + 4)
-#define AGNES_RAG_QUEUE (2 * AGNES_QUEUE_N + 4)
-#define AGNES_QUEUE_WORDS (3 * AGNES_QUEUE_N + 8)
+/* flow_prep's words, one per block of it (every one written on every call): whether
+ * its share of the instance offsets holds one off a multiple of 4 */
+#define AGNES_PREP_SLOT0 (AGNES_QUEUE_N + 4)
+#define AGNES_PREP_SLOTS 256
+#define AGNES_QUEUE_WORDS (AGNES_QUEUE_N + 4 + AGNES_PREP_SLOTS)
 #define AGNES_ERR_STRIPES 32
 #define AGNES_ERR_STRIDE 512
 #define AGNES_ERR_BYTES (AGNES_ERR_STRIPES * AGNES_ERR_STRIDE)

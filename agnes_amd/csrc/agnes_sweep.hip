@@ -705,19 +705,32 @@ hipError_t agnes_launch_sweep(const agnes_tally_args* a, int num_cus, hipStream_
     const bool sm = (a->flags & AGNES_FLAG_STATE_MACHINE) != 0 && a->states != nullptr;
     if (!agnes_flow_supported(a)) return hipErrorInvalidValue; /* max_rounds <= 15 always fits */
     hipError_t e;
-    agnes_tally_args b = *a;
-    b.ragged = agnes_flow_ragged_ok(a) ? 1u : 0u;
-    uint32_t bp[3] = {0u, 0u, 0u}; /* the batch partition both flow kernels walk */
-    { /* the aligned streams; the unaligned ones to the U kernel; every other batch to the walk list */
+    if (agnes_flow_rg(a)) {
+        /* the streams: flow_prep's gate picks ONE of the two kernels -- the aligned one when
+         * every instance offset is a multiple of 4, else the one that also walks the
+         * unaligned streams; every other batch to the walk list */
+        {
+            AgnesKt kt("flow_prep", st);
+            e = agnes_launch_flow_prep(a, st);
+        }
+        if (e != hipSuccess) return e;
+        agnes_tally_args b = *a;
+        b.gate = 1u;
+        {
+            AgnesKt kt("flow", st);
+            e = agnes_launch_flow(&b, num_cus, st, false);
+        }
+        if (e != hipSuccess) return e;
+        b.gate = 2u;
+        {
+            AgnesKt kt("flow_ragged", st);
+            e = agnes_launch_flow(&b, num_cus, st, true);
+        }
+    } else { /* the streams whose offsets are multiples of 4; every other batch to the walk list */
         AgnesKt kt("flow", st);
-        e = agnes_launch_flow(&b, num_cus, st, false, bp);
+        e = agnes_launch_flow(a, num_cus, st, false);
     }
     if (e != hipSuccess) return e;
-    if (b.ragged) { /* (returns at once unless the aligned kernel left it batches) */
-        AgnesKt kt("flow_ragged", st);
-        e = agnes_launch_flow(&b, num_cus, st, true, bp);
-        if (e != hipSuccess) return e;
-    }
     AgnesKt kt("sweep_walk", st);
     return sm ? launch_sweep_k<true>(a, num_cus, st) : launch_sweep_k<false>(a, num_cus, st);
 }
