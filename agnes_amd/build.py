@@ -16,7 +16,7 @@ SOURCES = ["agnes_kernels.hip", "agnes_fast.hip", "agnes_sweep.hip", "agnes_flow
            "agnes_edges.hip", "agnes_events.hip", "agnes_partials.hip", "agnes_fold.hip", "agnes_onesm.hip", "agnes_dedup.hip",
            "agnes_multi.hip", "agnes_valset.hip", "agnes_wire.hip", "agnes_api.cpp"]
 HEADERS = ["agnes_device.h", "agnes_ed25519.h", "agnes_fast.h", "agnes_gen.h", "agnes_gen_host.h",
-           "agnes_internal.h", "../../include/agnes.h"]
+           "agnes_internal.h", "agnes_flow_chunks.inc", "../../include/agnes.h"]
 OUT = os.path.join(PKG_DIR, "libagnes_amd.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("AGNES_ARCH", "gfx950")
