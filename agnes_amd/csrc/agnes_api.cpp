@@ -407,7 +407,19 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
                           (cfg->mode == AGNES_MODE_DEDUP || (cfg->flags & AGNES_FLAG_ROUND_SKIP) ||
                            route == AGNES_ROUTE_INSTANCE || route == AGNES_ROUTE_SPLIT);
         if (fast) a.ev_counts = ev_counts;
-        if (fast_counted) *fast_counted = fast;
+        /* agnes_tally_edges on the split per-instance route (C4): apply_codes writes the
+         * edges of every instance it walks (the LIST kernel's are the caller's to walk) */
+        const bool sm = (cfg->flags & AGNES_FLAG_STATE_MACHINE) != 0;
+        const bool apply_edges = !flow && edges && rec_out && !wide_all && sm &&
+                                 (route == AGNES_ROUTE_AUTO || route == AGNES_ROUTE_SPLIT) &&
+                                 (cfg->mode == AGNES_MODE_DEDUP || (cfg->flags & AGNES_FLAG_ROUND_SKIP) ||
+                                  route == AGNES_ROUTE_SPLIT) &&
+                                 agnes_apply_codes_supported(&a) && agnes_apply_edges_supported(cfg->max_rounds);
+        if (apply_edges) {
+            a.edge_counts = ev_counts;
+            a.edge_out = rec_out;
+        }
+        if (fast_counted) *fast_counted = fast || apply_edges;
     }
     return status_of(agnes_launch_tally(&a, cfg->mode, c->num_cus, wide_all, st));
 }
@@ -769,10 +781,14 @@ int agnes_tally_edges(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
     if ((b->n_instances && !counts) || (b->n_votes && !out) || ((uintptr_t)out & 15u)) return AGNES_E_INVALID;
     if (cfg_ok(cfg) && cfg->max_rounds > 128u) return AGNES_E_UNSUPPORTED; /* the walk's executor bytes in LDS */
     const hipStream_t st = (hipStream_t)stream;
-    bool counted = false;
+    bool counted = false, applied = false;
     const int rc = tally_impl(c, cfg, b, codes, states_in, states_out, nullptr, c->d_sets, c->n_sets, c->sets_dom, st,
-                              counts, &counted, out, true);
+                              counts, &counted, out, true, &applied);
     if (rc != AGNES_OK) return rc;
+    if (applied) /* apply_codes wrote the edges; the instances deferred to the LIST kernel here */
+        return status_of(agnes_launch_edge_seg_walk(b, codes, cfg->max_rounds, c->d_list,
+                                                    reinterpret_cast<const uint32_t*>(c->d_err + AGNES_ERR_BYTES / 8),
+                                                    counts, out, st));
     if (counted) /* the flow kernel wrote its batches' edges; the walk list's instances here */
         return status_of(agnes_launch_edge_seg_walk(b, codes, cfg->max_rounds, c->d_list + (size_t)c->list_cap,
                                                     reinterpret_cast<const uint32_t*>(c->d_err + AGNES_ERR_BYTES / 8) +

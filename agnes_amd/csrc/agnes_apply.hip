@@ -19,6 +19,12 @@
  *
  * Instances the tally kernel deferred to the i64 LIST kernel (sums may reach
  * 2^31) are skipped here: that kernel applies their events itself.
+ *
+ * EDG (agnes_tally_edges, round 6): the same walk also writes the instance's
+ * edge-triggered summary (agnes_edges.hip's walk, on the final codes of each window
+ * while they are in registers) to its segment, and its count -- the separate edge
+ * walk over the codes, rounds and types is gone.  It reads the type column too and
+ * walks on past the commit (the codes after it still change their executors' levels).
  */
 #include <hip/hip_runtime.h>
 
@@ -39,6 +45,8 @@ constexpr uint32_t NOPOS = 0xFFFFFFFFu;
  * is needed, so a line is fetched once although the 64 lanes of a wave read 64
  * different lines.  LDS per wave: [stage 2][column 2][k 4][lane 64][16 B]. */
 constexpr uint32_t BLK = 64u, LDS_PER_WAVE = 2u * 4u * 64u * 16u, WAVES = 4u;
+/* (EDG) the type column too: [column 3][k 4][lane 64][16 B] */
+constexpr uint32_t LDS_PER_WAVE_EDG = 3u * 4u * 64u * 16u;
 
 /* the bytes of a 16-B window that runs past the batch end, into the lane's slot
  * (the batch's last instance only) */
@@ -139,7 +147,7 @@ __device__ uint32_t label_of(const agnes_tally_args& a, uint64_t lo, uint64_t j)
     return 0u;
 }
 
-template <bool SKIP>
+template <bool SKIP, bool EDG>
 __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n = a.vb.n_instances, ns = a.n_sets;
@@ -147,11 +155,15 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
     /* every per-instance input at once (one latency, not a chain) */
     uint4* const sp = reinterpret_cast<uint4*>(a.states + i);
     uint64_t lo = a.vb.offsets[i], hi = a.vb.offsets[i + 1u];
+    const uint64_t seg0 = lo; /* (EDG) the instance's segment */
     const uint4 s0 = sp[0], s1 = sp[1], s2 = sp[2], s3 = sp[3];
     const uint64_t NV = a.vb.n_votes;
     lo = lo < NV ? lo : NV;
     hi = hi < NV ? hi : NV;
-    if (hi <= lo) return;
+    if (hi <= lo) {
+        if (EDG) a.edge_counts[i] = 0ull;
+        return;
+    }
     { /* the same domain test (u32, or u64 for a.w64) as the tally kernels: the rest is the LIST kernel's */
         const uint32_t set = a.vb.instance_set ? a.vb.instance_set[i] : (ns ? i % ns : 0u);
         if (set < ns) {
@@ -162,7 +174,7 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
     }
 
     const uint32_t step0 = s3.y & 0xFFu; /* dword 13: step | locked << 8 | valid << 16 | decided << 24 */
-    if (step0 == AGNES_STEP_COMMIT) return; /* :205 every later event: None */
+    if (!EDG && step0 == AGNES_STEP_COMMIT) return; /* :205 every later event: None */
     const int64_t round0 = (int64_t)(((uint64_t)s0.w << 32) | s0.z);
     uint32_t step = step0;
     uint32_t eq8 = (round0 >= 0 && round0 <= 255) ? (uint32_t)round0 : 0x100u; /* no u8 round equals 0x100 */
@@ -177,7 +189,7 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
      * Precommit's — and byte masks decide every vote: start-table messages before
      * P1 (or the commit), Precommit-table messages between P1 and the commit, the
      * step messages at the two, nothing after the commit. */
-    auto walk_ns = [&](uint64_t w, uint4 cq, uint4 rq) {
+    auto walk_ns = [&](uint64_t w, uint4 cq, uint4 rq, uint32_t (&ow)[4]) {
         const uint32_t c4[4] = {cq.x, cq.y, cq.z, cq.w}, r4[4] = {rq.x, rq.y, rq.z, rq.w};
         const int32_t rel = (int32_t)((int64_t)w - (int64_t)lo); /* > -16 */
         const uint32_t a0 = rel < 0 ? (uint32_t)(-rel) : 0u;
@@ -217,7 +229,7 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
         const uint32_t fc = first(cvb), fp = first(p1b);
         const bool has_p1 = fp < fc;          /* P1 before the commit (a commit ends the walk) */
         const uint32_t pre = has_p1 ? fp : fc; /* start-table messages below this byte */
-        uint32_t ow[4], vup[4];
+        uint32_t vup[4];
 #pragma unroll
         for (uint32_t d = 0; d < 4u; ++d) {
             const uint32_t mid = has_p1 ? span(d, fp + 1u, fc) : 0u;
@@ -264,14 +276,17 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
     };
 
     /* one 16-B window at w of this instance (cq, rq: its code and round bytes) */
-    auto walk = [&](uint64_t w, uint4 cq, uint4 rq) {
+    auto walk = [&](uint64_t w, uint4 cq, uint4 rq, uint32_t (&ow)[4]) {
         const uint32_t c4[4] = {cq.x, cq.y, cq.z, cq.w}, r4[4] = {rq.x, rq.y, rq.z, rq.w};
         const int32_t rel = (int32_t)((int64_t)w - (int64_t)lo); /* > -16 */
         const uint32_t a0 = rel < 0 ? (uint32_t)(-rel) : 0u;
         const uint64_t rem = hi - w;
         const uint32_t a1 = rem < 16u ? (uint32_t)rem : 16u;
         uint32_t allowed = ((1u << a1) - 1u) & ~((1u << a0) - 1u); /* bytes of this instance not yet walked */
-        uint32_t ow[4] = {c4[0], c4[1], c4[2], c4[3]};
+        ow[0] = c4[0];
+        ow[1] = c4[1];
+        ow[2] = c4[2];
+        ow[3] = c4[3];
         /* one pass per step change inside the window (at most a few per instance) */
         for (;;) {
             const uint32_t t1lo = eq8 < 0x100u ? t1lo_of(step) : T0LO;
@@ -367,10 +382,46 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
         }
     };
 
+    /* (EDG) the edges of one window from its final codes (agnes_edges.hip walk_one): an
+     * executor's byte is its level (code bits 0..3) | last message << 4, key round * 2 +
+     * type < 16 in byte key & 7 of est0 / est1; a vote whose byte changes is an edge */
+    const uint32_t keys = 2u * a.max_rounds;
+    uint64_t est0 = 0, est1 = 0, ecnt = 0;
+    uint4* const eout = EDG ? reinterpret_cast<uint4*>(a.edge_out) + seg0 : nullptr;
+    auto edges_win = [&](uint64_t w, const uint32_t (&o4)[4], uint4 rq, uint4 tq) {
+        const uint32_t r4[4] = {rq.x, rq.y, rq.z, rq.w}, t4[4] = {tq.x, tq.y, tq.z, tq.w};
+        const int32_t rel = (int32_t)((int64_t)w - (int64_t)lo); /* > -16 */
+        const uint32_t a0 = rel < 0 ? (uint32_t)(-rel) : 0u;
+        const uint64_t rem = hi - w;
+        const uint32_t a1 = rem < 16u ? (uint32_t)rem : 16u;
+#pragma unroll
+        for (uint32_t b = 0; b < 16u; ++b) {
+            if (b < a0 || b >= a1) continue;
+            const uint32_t sh8 = 8u * (b & 3u);
+            const uint32_t cb = (o4[b >> 2] >> sh8) & 0xFFu, rb = (r4[b >> 2] >> sh8) & 0xFFu,
+                           tb = (t4[b >> 2] >> sh8) & 0xFFu;
+            const uint32_t ev = cb & AGNES_CODE_EVENT_MASK;
+            const uint32_t key = rb * 2u + tb;
+            if (ev == AGNES_CODE_INVALID || ev == AGNES_CODE_REJECTED || tb > 1u || key >= keys) continue;
+            const uint32_t sh = 8u * (key & 7u);
+            const uint32_t old = (uint32_t)((key < 8u ? est0 : est1) >> sh) & 0xFFu;
+            const uint32_t msg = cb >> AGNES_CODE_MSG_SHIFT;
+            const uint32_t nb = (cb & 0xFu) | (msg ? msg << AGNES_CODE_MSG_SHIFT : old & 0xF0u);
+            if (nb != old) {
+                const uint64_t j = w + b;
+                eout[ecnt] = make_uint4((uint32_t)j, (uint32_t)(j >> 32), i, rb | (tb << 8) | (cb << 16) | (old << 24));
+                ++ecnt;
+                const uint64_t x = (uint64_t)(old ^ nb) << sh;
+                if (key < 8u) est0 ^= x;
+                else est1 ^= x;
+            }
+        }
+    };
+
     /* the lane's 64-B blocks by LDS-DMA; a window past the batch end is clamped to
      * an in-bounds one (16 <= NV: the launcher) and filled byte-wise after the wait */
     const uint32_t lane = threadIdx.x & 63u;
-    unsigned char* const wbase = agnes_smem + rfl(threadIdx.x >> 6) * LDS_PER_WAVE; /* wave-uniform: m0 */
+    unsigned char* const wbase = agnes_smem + rfl(threadIdx.x >> 6) * (EDG ? LDS_PER_WAVE_EDG : LDS_PER_WAVE); /* wave-uniform: m0 */
     const uint64_t wmax = (NV & ~15ull) - 16u; /* the last window fully inside [0, NV) */
     /* single-buffered: 8 KB per wave keeps 20 waves per CU resident to cover the latency */
     auto issue = [&](uint64_t blk) {
@@ -380,6 +431,7 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
             const uint64_t ws = w <= wmax ? w : wmax;
             fast::glds16(a.codes + ws, wbase + k * 1024u);
             fast::glds16(a.vb.round + ws, wbase + (4u + k) * 1024u);
+            if (EDG) fast::glds16(a.vb.type + ws, wbase + (8u + k) * 1024u);
         }
     };
     uint64_t blk = lo & ~(uint64_t)(BLK - 1u);
@@ -387,36 +439,44 @@ __global__ __launch_bounds__(256) void apply_codes(agnes_tally_args a) {
     for (;;) {
         fast::dma_wait();
         /* the block's four windows out of LDS at once (one wait, not one per window) */
-        uint4 cw[4], rw[4];
+        uint4 cw[4], rw[4], tw[EDG ? 4 : 1];
 #pragma unroll
         for (uint32_t k = 0; k < 4u; ++k) {
             const uint64_t w = blk + 16u * k;
             unsigned char* const cs = wbase + k * 1024u + 16u * lane;
             unsigned char* const rs = wbase + (4u + k) * 1024u + 16u * lane;
+            unsigned char* const ts = wbase + (8u + k) * 1024u + 16u * lane;
             if (w < hi && w + 16u > lo && w > wmax) { /* past the batch end: the real bytes */
                 tail_fill(a.codes, w, NV, cs);
                 tail_fill(a.vb.round, w, NV, rs);
+                if (EDG) tail_fill(a.vb.type, w, NV, ts);
             }
             cw[k] = *reinterpret_cast<const uint4*>(cs);
             rw[k] = *reinterpret_cast<const uint4*>(rs);
+            if constexpr (EDG) tw[k] = *reinterpret_cast<const uint4*>(ts);
         }
 #pragma unroll
         for (uint32_t k = 0; k < 4u; ++k) {
             const uint64_t w = blk + 16u * k;
             if (w >= hi) break;
             if (w + 16u > lo) {
-                if (SKIP) walk(w, cw[k], rw[k]);
-                else walk_ns(w, cw[k], rw[k]);
+                uint32_t ow[4] = {cw[k].x, cw[k].y, cw[k].z, cw[k].w};
+                if (step != AGNES_STEP_COMMIT) { /* (EDG: past the commit the codes stay as they are) */
+                    if (SKIP) walk(w, cw[k], rw[k], ow);
+                    else walk_ns(w, cw[k], rw[k], ow);
+                }
+                if constexpr (EDG) edges_win(w, ow, rw[k], tw[k]);
             }
-            if (step == AGNES_STEP_COMMIT) break;
+            if (!EDG && step == AGNES_STEP_COMMIT) break;
         }
         const uint64_t nb = blk + BLK;
-        if (nb >= hi || step == AGNES_STEP_COMMIT) break;
+        if (nb >= hi || (!EDG && step == AGNES_STEP_COMMIT)) break;
         issue(nb); /* this block's LDS reads are consumed: the slot is free */
         blk = nb;
     }
     /* the wave's other lanes may still be streaming: nothing of this lane's in flight */
     fast::dma_wait();
+    if (EDG) a.edge_counts[i] = ecnt;
 
     if (lock_at == NOPOS && valid_at == NOPOS && dec_at == NOPOS && !skipped && step == step0) return;
     /* the State back: round (RoundSkip), locked, valid, decision, step/flags.  Only
@@ -471,23 +531,30 @@ bool agnes_apply_codes_supported(const agnes_tally_args* a) {
            a->vb.n_votes >= 32u && a->states != nullptr && (a->flags & AGNES_FLAG_STATE_MACHINE) != 0;
 }
 
+bool agnes_apply_edges_supported(uint32_t max_rounds) { return max_rounds >= 1u && max_rounds <= 8u; }
+
+template <bool SKIP, bool EDG>
+static hipError_t launch_apply(const agnes_tally_args* a, uint32_t blocks, hipStream_t st) {
+    const size_t lds = (size_t)(EDG ? agnes::apply::LDS_PER_WAVE_EDG : agnes::apply::LDS_PER_WAVE) * agnes::apply::WAVES;
+    static thread_local bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&agnes::apply::apply_codes<SKIP, EDG>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL((agnes::apply::apply_codes<SKIP, EDG>), dim3(blocks), dim3(256), lds, st, *a);
+    return hipGetLastError();
+}
+
 hipError_t agnes_launch_apply_codes(const agnes_tally_args* a, hipStream_t st) {
     const uint32_t n = a->vb.n_instances;
     if (n == 0) return hipSuccess;
     const uint32_t blocks = (n + 255u) / 256u;
-    const size_t lds = (size_t)agnes::apply::LDS_PER_WAVE * agnes::apply::WAVES;
-    static thread_local bool attr[2] = {false, false};
     const bool skip = (a->flags & AGNES_FLAG_ROUND_SKIP) != 0;
-    if (!attr[skip]) {
-        const void* fn = skip ? reinterpret_cast<const void*>(&agnes::apply::apply_codes<true>)
-                              : reinterpret_cast<const void*>(&agnes::apply::apply_codes<false>);
-        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr[skip] = true;
+    if (a->edge_counts) {
+        if (!a->edge_out || !agnes_apply_edges_supported(a->max_rounds)) return hipErrorInvalidValue;
+        return skip ? launch_apply<true, true>(a, blocks, st) : launch_apply<false, true>(a, blocks, st);
     }
-    if (skip)
-        hipLaunchKernelGGL(agnes::apply::apply_codes<true>, dim3(blocks), dim3(256), lds, st, *a);
-    else
-        hipLaunchKernelGGL(agnes::apply::apply_codes<false>, dim3(blocks), dim3(256), lds, st, *a);
-    return hipGetLastError();
+    return skip ? launch_apply<true, false>(a, blocks, st) : launch_apply<false, false>(a, blocks, st);
 }

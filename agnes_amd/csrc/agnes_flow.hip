@@ -253,7 +253,12 @@ struct Hdr {
 #define AGNES_FLOW_FORCE_U 0 /* A/B builds only: every stream through the unaligned-stream loop */
 #endif
 #ifndef AGNES_FLOW_CODE_VMCNT
-#define AGNES_FLOW_CODE_VMCNT 1
+/* 1: after a whole-chunk code store the next chunk waits vmcnt(1), leaving that store in
+ * flight -- which assumes loads and stores retire from vmcnt in issue order, an ordering
+ * LLVM's waitcnt pass does not assume for mixed loads and stores.  Measured worth nothing
+ * in round 6 (same box: c3shard 0.3672 / 0.3592 ms with it, 0.3634 / 0.3636 without; C3
+ * 2.401 / 2.402 vs 2.385 / 2.379), so the exact vmcnt(0) is the default. */
+#define AGNES_FLOW_CODE_VMCNT 0
 #endif
 #ifndef AGNES_FLOW_XWPE
 #define AGNES_FLOW_XWPE 3 /* the records / edges variants, one round */

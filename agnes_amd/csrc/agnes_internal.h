@@ -71,6 +71,10 @@ typedef struct agnes_tally_args {
     uint32_t gate;        /* flow: 0 runs; 1 returns at once when flow_prep found an unaligned
                              instance offset, 2 when it found none */
     uint32_t prep_zero;   /* flow_prep zeroes the counters (the caller skipped their memset) */
+    uint64_t* edge_counts; /* optional (agnes_tally_edges on the split per-instance route): apply_codes
+                              also writes each instance's edges to edge_out's segments and their
+                              counts here (the instances it defers to the LIST kernel excepted) */
+    void* edge_out;
     void* rec_out;        /* optional (agnes_tally_records): agnes_seg_event [n_votes], instance i's
                              records at [offsets[i], offsets[i] + ev_counts[i]) -- the flow
                              kernel writes them (REC); every other route's emit pass does */
@@ -144,6 +148,9 @@ bool agnes_flow_counts_events(uint32_t flags, uint32_t max_rounds, bool edges = 
 /* the batched State::apply pass over the codes a tally kernel left (agnes_apply.hip):
  * one instance per lane, skipping the instances deferred to the LIST kernel */
 bool agnes_apply_codes_supported(const agnes_tally_args* a);
+/* apply_codes can write the edges too (keys = 2 * max_rounds <= 16: the executor bytes in
+ * two registers) */
+bool agnes_apply_edges_supported(uint32_t max_rounds);
 hipError_t agnes_launch_apply_codes(const agnes_tally_args* a, hipStream_t stream);
 int64_t agnes_fast_lds_per_wave(uint32_t mode, uint32_t flags, uint32_t max_rounds, uint32_t n_vals);
 hipError_t agnes_launch_apply_events(agnes_state* states, uint32_t n, const uint64_t* off,
