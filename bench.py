@@ -37,7 +37,8 @@ BYTES_PER_VOTE = 15            # 14 B canonical SoA in + 1 B code out (BASELINE.
 # algorithmic bytes per vote of each engine kernel (names: agnes_kernel_times)
 KERNEL_BYTES_PER_VOTE = {
     "flow": 15,          # instance, value, validator u32 + round, type u8 in; code u8 out
-    "flow_ragged": 15,   # the same, the unaligned-stream variant (round 6: c2r / c3r)
+    "flow_ragged": 15,   # the same, the kernel that also holds the unaligned-stream loop (round 6: c2r / c3r)
+    "flow_prep": 0,      # the flow route's gate: 8 B per instance (the offsets), not per vote
     "tally_fast": 15,
     "tally_wide": 15,
     "tally_list": 15,    # the i64 kernel over the instances the u32 kernels hand over (c2w: all)
@@ -60,7 +61,8 @@ KERNEL_SYMBOLS = {
     # template parameters: PC (power table in LDS), SM (State machine), R1 (one round);
     # c2 runs flow<true, true, true>, c3 flow<false, true, false> (rocprofv3 names them)
     "flow": "agnes::flow::flow<PC, SM, R1>",
-    "flow_ragged": "agnes::flow::flow<PC, SM, R1, ..., U=true>",
+    "flow_ragged": "agnes::flow::flow<PC, SM, R1, ..., RG=true>",
+    "flow_prep": "agnes::flow::flow_prep",
     "sweep_walk": "agnes::sweep::sweep<PC, SM>",
     "tally_fast": "agnes::fast::tally_fast<...>",
     "tally_wide": "agnes::tally_kernel<true, ...>",

@@ -122,6 +122,22 @@ def batch_from_lists(instance, round_, type_, value, validator, offsets, instanc
     )
 
 
+def concat_batches(*bs: HostBatch) -> HostBatch:
+    """One batch holding the given batches' instances in order (instance ids and
+    offsets rebased; no instance_set / weight): e.g. an aligned generated batch followed
+    by a ragged one, so one call holds both kinds of flow batch."""
+    inst, off, base_i, base_v = [], [np.zeros(1, np.uint64)], 0, 0
+    for b in bs:
+        n = len(b.offsets) - 1
+        inst.append(b.instance.astype(np.uint64) + base_i)
+        off.append(b.offsets[1:].astype(np.uint64) + np.uint64(base_v))
+        base_i += n
+        base_v += int(b.offsets[-1])
+    return batch_from_lists(np.concatenate(inst).astype(np.uint32), np.concatenate([b.round for b in bs]),
+                            np.concatenate([b.type for b in bs]), np.concatenate([b.value for b in bs]),
+                            np.concatenate([b.validator for b in bs]), np.concatenate(off))
+
+
 def gen_offsets(p: abi.GenParams) -> np.ndarray:
     off = np.zeros(p.n_instances + 1, dtype=np.uint64)
     rc = lib().orc_gen_offsets(C.byref(p), _p(off))

@@ -300,3 +300,19 @@ def test_tally_edges_walk_list_and_empty(eng):
                        ol.gen_power(65, 1, 100, abi.POWER_UNIFORM, 1, 1000), abi.new_states(1, 1, abi.STEP_PREVOTE))
     empty = ol.batch_from_lists([], [], [], [], [], np.zeros(5, dtype=np.uint64))
     _tally_edges_check(eng, abi.config(abi.MODE_REFERENCE, 0, 1), empty, ol.gen_power(66, 1, 4, abi.POWER_UNIFORM, 1, 10))
+
+
+@pytest.mark.parametrize("rounds", [1, 4])
+def test_tally_edges_mixed_alignment(eng, rounds):
+    """Round 6: aligned and unaligned flow batches in one call (the kernel with both
+    loops), the edges each loop writes against orc_edges"""
+    parts = []
+    for k, absent in enumerate((0, 60, 0)):
+        p = abi.gen_params(seed=160 + 3 * rounds + k, n_instances=1500, n_vals=24, rounds_min=1,
+                           rounds_max=rounds, nil_permille=300, absent_permille=absent)
+        parts.append(ol.gen_batch(p))
+    hb = ol.concat_batches(*parts)
+    power = ol.gen_power(160, 3, 24, abi.POWER_UNIFORM, 1, 100)
+    states = abi.new_states(hb.n_instances, 1, abi.STEP_PREVOTE)
+    assert len(_tally_edges_check(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, rounds), hb, power,
+                                  states)) > 0

@@ -682,3 +682,31 @@ def test_round_runs(eng, order):
     cfg0 = abi.config(abi.MODE_REFERENCE, 0, 8)
     g, o = run_both(eng, cfg0, hb, power)
     assert_same(g, o)
+
+
+def _mixed_alignment_batch(seed, rounds):
+    """An aligned generated batch (even validator count, no abstention: every offset a
+    multiple of 4), a ragged one (abstention), and an aligned one again, as ONE batch: the
+    call runs the kernel that holds both loops, which walks the aligned batches with the
+    aligned loop and the others with the unaligned-stream loop (round 6)."""
+    parts = []
+    for k, absent in enumerate((0, 60, 0)):
+        p = abi.gen_params(seed=seed + k, n_instances=1500, n_vals=24, rounds_min=1, rounds_max=rounds,
+                           nil_permille=300, absent_permille=absent)
+        parts.append(ol.gen_batch(p))
+    assert (parts[0].offsets % 4 == 0).all() and (parts[1].offsets % 4 != 0).any()
+    return ol.concat_batches(*parts)
+
+
+@pytest.mark.parametrize("rounds", [1, 4])
+@pytest.mark.parametrize("flags", [0, abi.FLAG_STATE_MACHINE])
+def test_mixed_aligned_and_unaligned_batches(eng, rounds, flags):
+    """Aligned and unaligned flow batches in one call (the gate picks the kernel with both
+    loops; each batch takes its own loop): codes and States against the checker."""
+    hb = _mixed_alignment_batch(140 + rounds, rounds)
+    power = ol.gen_power(140, 3, 24, abi.POWER_UNIFORM, 1, 100)
+    st = _start_states(hb.n_instances) if flags else None
+    g, o = run_both(eng, abi.config(abi.MODE_REFERENCE, flags, rounds), hb, power, None, st)
+    assert_same(g, o)
+    if flags:
+        assert g[1]["decided"].sum() > 0

@@ -336,3 +336,18 @@ def test_tally_events_full_c4_shard(eng):
     cfg = abi.config(abi.MODE_DEDUP, abi.FLAG_STATE_MACHINE | abi.FLAG_ROUND_SKIP | abi.FLAG_DISTINCT_VALUES, 5)
     ev = _check(eng, cfg, hb, power, abi.new_states(125_000, 1, abi.STEP_PREVOTE))
     assert (ev["kind"] == abi.EV_ROUND_SKIP).any()
+
+
+@pytest.mark.parametrize("rounds", [1, 4])
+def test_tally_records_mixed_alignment(eng, rounds):
+    """Round 6: aligned and unaligned flow batches in one call (the kernel with both loops):
+    the record counts, the dense records and the segmented records against the checker"""
+    parts = []
+    for k, absent in enumerate((0, 60, 0)):
+        p = abi.gen_params(seed=150 + 3 * rounds + k, n_instances=1500, n_vals=24, rounds_min=1,
+                           rounds_max=rounds, nil_permille=450, absent_permille=absent)
+        parts.append(ol.gen_batch(p))
+    hb = ol.concat_batches(*parts)
+    power = ol.gen_power(150, 3, 24, abi.POWER_UNIFORM, 1, 100)
+    _check(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, rounds), hb, power,
+           abi.new_states(hb.n_instances, 1, abi.STEP_PREVOTE), in_place=False)

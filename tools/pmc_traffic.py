@@ -18,12 +18,19 @@ import sys
 
 # engine kernel name (agnes_kernel_times) -> regex on the demangled symbol
 KERNELS = {
-    # template <PC, SM, R1, EVC, W64, REC, EDG>: the step's flow, and the record / edge
-    # variants agnes_tally_records / agnes_tally_edges launch (round 5)
-    "flow": r"agnes::flow::flow<\w+, \w+, \w+, false, \w+, false, false>",
-    "flow_counts": r"agnes::flow::flow<\w+, \w+, \w+, true, \w+, false, false>",
-    "flow_records": r"agnes::flow::flow<\w+, \w+, \w+, true, \w+, true, false>",
-    "flow_edges": r"agnes::flow::flow<\w+, \w+, \w+, true, \w+, false, true>",
+    # template <PC, SM, R1, EVC, W64, REC, EDG, RG>: the step's flow, and the record / edge
+    # variants agnes_tally_records / agnes_tally_edges launch (round 5); RG = true: the
+    # kernel that also holds the unaligned-stream loop (round 6, "flow_ragged"), which
+    # runs instead of the aligned one when some instance offset is not a multiple of 4
+    "flow": r"agnes::flow::flow<\w+, \w+, \w+, false, \w+, false, false, false>",
+    "flow_counts": r"agnes::flow::flow<\w+, \w+, \w+, true, \w+, false, false, false>",
+    "flow_records": r"agnes::flow::flow<\w+, \w+, \w+, true, \w+, true, false, false>",
+    "flow_edges": r"agnes::flow::flow<\w+, \w+, \w+, true, \w+, false, true, false>",
+    "flow_ragged": r"agnes::flow::flow<\w+, \w+, \w+, false, \w+, false, false, true>",
+    "flow_ragged_counts": r"agnes::flow::flow<\w+, \w+, \w+, true, \w+, false, false, true>",
+    "flow_ragged_records": r"agnes::flow::flow<\w+, \w+, \w+, true, \w+, true, false, true>",
+    "flow_ragged_edges": r"agnes::flow::flow<\w+, \w+, \w+, true, \w+, false, true, true>",
+    "flow_prep": r"agnes::flow::flow_prep",
     "sweep_walk": r"agnes::sweep::sweep<",
     "tally_fast": r"agnes::fast::tally_fast<",
     "apply_codes": r"agnes::apply::apply_codes<",
