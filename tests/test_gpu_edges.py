@@ -235,8 +235,10 @@ def _tally_edges_check(eng, cfg, hb, power, states=None, shift=0):
 
 
 @pytest.mark.parametrize("name", ["c2_small", "c2_sm", "c3_small", "c4_small", "c4_ref_skip", "sorted_tiny_sets",
-                                  "many_rounds", "c2w_small"])
+                                  "many_rounds", "c2w_small", "c3w_small", "c3w_plain", "w64_deferred"])
 def test_tally_edges_generated(eng, name):
+    """(the u64-domain configs -- one round, runs mode, the per-round passes, and
+    w64_deferred's instances for the i64 LIST kernel -- take the edge walk after the tally)"""
     p, hb, power, cfg = _make(name)
     states = _start_states(p.n_instances) if cfg.flags & abi.FLAG_STATE_MACHINE else None
     recs = _tally_edges_check(eng, cfg, hb, power, states)
