@@ -849,8 +849,9 @@ __global__ __launch_bounds__(256) void flow_prep(const uint64_t* offsets, uint64
     if (t < zw) zb[t] = 0u;
     const uint64_t S = (uint64_t)gridDim.x * 256u;
     uint64_t acc = 0, i = t;
-    for (; i + 3u * S < n1; i += 4u * S) /* four independent loads in flight */
-        acc |= offsets[i] | offsets[i + S] | offsets[i + 2u * S] | offsets[i + 3u * S];
+    for (; i + 7u * S < n1; i += 8u * S) /* eight independent loads in flight (C2's 8 MB: two round trips) */
+        acc |= offsets[i] | offsets[i + S] | offsets[i + 2u * S] | offsets[i + 3u * S] | offsets[i + 4u * S] |
+               offsets[i + 5u * S] | offsets[i + 6u * S] | offsets[i + 7u * S];
     for (; i < n1; i += S) acc |= offsets[i];
     const bool odd = __syncthreads_or((acc & 3u) != 0u);
     if (threadIdx.x == 0) slots[blockIdx.x] = odd ? 1u : 0u;
