@@ -652,9 +652,11 @@ typedef struct agnes_edge {
 /* The tally and its edge summary in ONE call (round 5), SEGMENTED by instance: instance
  * i's edges at out[offsets[i] + k], k < counts[i] (a vote is at most one edge), in vote
  * order -- the records agnes_edges gives, at segment offsets.  On the flow route
- * (REFERENCE without RoundSkip, max_rounds <= 15, offsets multiples of 4) the tally
+ * (REFERENCE without RoundSkip, max_rounds <= 15, u32 sums; any offsets) the tally
  * kernel finds and writes them while the votes are in registers, each executor's state
- * carried in LDS: no pass over the codes.  counts (DEVICE, n_instances u64); out
+ * carried in LDS: no pass over the codes; on the split per-instance route (DEDUP or
+ * RoundSkip with the State machine, max_rounds <= 8) the State machine's pass writes
+ * them.  counts (DEVICE, n_instances u64); out
  * (DEVICE, 16-B aligned, n_votes records; offsets must not go back); max_rounds <= 128.  agnes_edges_compact
  * gives the dense layout (offsets[n_instances + 1] from the counts; out, when not
  * null, exactly agnes_edges'). */
