@@ -318,3 +318,24 @@ def test_tally_edges_mixed_alignment(eng, rounds):
     states = abi.new_states(hb.n_instances, 1, abi.STEP_PREVOTE)
     assert len(_tally_edges_check(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, rounds), hb, power,
                                   states)) > 0
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name", ["c3r", "c4"])
+def test_tally_edges_full_shard(eng, name):
+    """Round 6, full size: the bench's c3r batch (edges from the unaligned-stream loop) and
+    the C4 shard (edges from the State machine's pass on the split route)"""
+    from agnes_amd import dist as ad
+    kw = dict(seed=0xA6E5, n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300)
+    if name == "c3r":
+        p = abi.gen_params(absent_permille=50, **kw)
+        power = ol.gen_power(0xA6E5, 1024, 150, abi.POWER_UNIFORM, 1, 1000)
+        cfg = abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 4)
+    else:
+        p = abi.gen_params(dup_permille=100, equiv_permille=100, higher_permille=50, **kw)
+        power = ol.gen_power(0xA6E5, 1024, 150, abi.POWER_ZIPF, 1, 1_000_000)
+        cfg = abi.config(abi.MODE_DEDUP, abi.FLAG_STATE_MACHINE | abi.FLAG_ROUND_SKIP, 5)
+    hb = ol.gen_batch(p)
+    hb.instance_set = ad.set_of_instances(ad.Shard(p, 0, p.n_instances), 1024)
+    recs = _tally_edges_check(eng, cfg, hb, power, _start_states(p.n_instances))
+    assert len(recs) > p.n_instances

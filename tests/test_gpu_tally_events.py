@@ -338,6 +338,20 @@ def test_tally_events_full_c4_shard(eng):
     assert (ev["kind"] == abi.EV_ROUND_SKIP).any()
 
 
+@pytest.mark.slow
+def test_tally_events_full_c3r_shard(eng):
+    """round 6: the bench's c3r batch -- a C3 shard with 5 % abstention (offsets at every
+    residue): the counts and records from the unaligned-stream loop, full size"""
+    p = abi.gen_params(seed=0xA6E5, n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300,
+                       absent_permille=50)
+    hb = ol.gen_batch(p)
+    assert (hb.offsets % 4 != 0).mean() > 0.5
+    hb.instance_set = ad.set_of_instances(ad.Shard(p, 0, p.n_instances), 1024)
+    power = ol.gen_power(0xA6E5, 1024, 150, abi.POWER_UNIFORM, 1, 1000)
+    _check(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 4), hb, power,
+           abi.new_states(125_000, 1, abi.STEP_PREVOTE), in_place=False)
+
+
 @pytest.mark.parametrize("rounds", [1, 4])
 def test_tally_records_mixed_alignment(eng, rounds):
     """Round 6: aligned and unaligned flow batches in one call (the kernel with both loops):
