@@ -235,7 +235,8 @@ def _tally_edges_check(eng, cfg, hb, power, states=None, shift=0):
 
 
 @pytest.mark.parametrize("name", ["c2_small", "c2_sm", "c3_small", "c4_small", "c4_ref_skip", "sorted_tiny_sets",
-                                  "many_rounds", "c2w_small", "c3w_small", "c3w_plain", "w64_deferred"])
+                                  "many_rounds", "c2w_small", "c3w_small", "c3w_plain", "w64_deferred",
+                                  "c2w_ragged", "c3w_ragged"])
 def test_tally_edges_generated(eng, name):
     """(the u64-domain configs -- one round, runs mode, the per-round passes, and
     w64_deferred's instances for the i64 LIST kernel -- take the edge walk after the tally)"""

@@ -247,6 +247,14 @@ CONFIGS = {
     "c4r_ref": (dict(n_instances=2000, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300,
                      dup_permille=100, equiv_permille=100, higher_permille=50, absent_permille=30),
                 (abi.POWER_UNIFORM, 1, 1000, 64), (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 5)),
+    # the u64 domain with abstention: flow<W64> walks aligned streams only, so these batches
+    # go to the walk list, whose instances the i64 LIST kernel tallies
+    "c2w_ragged": (dict(n_instances=2000, n_vals=100, rounds_min=1, rounds_max=1, nil_permille=200,
+                        absent_permille=60),
+                   (abi.POWER_UNIFORM, 1 << 28, 1 << 34, 1), (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 1)),
+    "c3w_ragged": (dict(n_instances=2000, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300,
+                        absent_permille=50),
+                   (abi.POWER_UNIFORM, 1 << 28, 1 << 34, 64), (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 4)),
     "many_rounds": (dict(n_instances=200, n_vals=20, rounds_min=30, rounds_max=60,
                          nil_permille=300, higher_permille=100),
                     (abi.POWER_UNIFORM, 1, 100, 5),
@@ -570,7 +578,7 @@ def test_c3_shard_parity(eng):
 
 @pytest.mark.parametrize("route", list(ROUTES))
 @pytest.mark.parametrize("name", ["c2_sm", "c3_small", "c4_small", "c2w_small", "w64_dedup_skip", "c3w_small",
-                                  "w64_revisit", "c2r_small", "c3r_small", "c4r_ref"])
+                                  "w64_revisit", "c2r_small", "c3r_small", "c4r_ref", "c3w_ragged"])
 def test_routes_generated(eng, route, name):
     p, hb, power, cfg = _make(name)
     cfg = abi.config(cfg.mode, cfg.flags | ROUTES[route], cfg.max_rounds)

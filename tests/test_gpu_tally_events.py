@@ -365,3 +365,13 @@ def test_tally_records_mixed_alignment(eng, rounds):
     power = ol.gen_power(150, 3, 24, abi.POWER_UNIFORM, 1, 100)
     _check(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, rounds), hb, power,
            abi.new_states(hb.n_instances, 1, abi.STEP_PREVOTE), in_place=False)
+
+
+@pytest.mark.parametrize("name", ["c2w_ragged", "c3w_ragged"])
+def test_tally_records_u64_ragged(eng, name):
+    """Round 6: i64 stakes (the u64 domain) with abstention -- the unaligned batches go
+    through the walk list and the i64 LIST kernel: counts, dense and segmented records"""
+    from test_gpu_parity import _make
+    p, hb, power, cfg = _make(name)
+    assert (hb.offsets % 4 != 0).any()
+    _check(eng, cfg, hb, power, abi.new_states(p.n_instances, 1, abi.STEP_PREVOTE), in_place=False)
