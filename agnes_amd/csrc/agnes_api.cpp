@@ -339,7 +339,7 @@ static int tally_impl(agnes_ctx* c, const agnes_config* cfg, const agnes_vote_ba
      * with the unaligned-stream kernel, zeroed by its gate pass (flow_prep: one launch
      * fewer in the step) */
     const uint32_t route0 = (cfg->flags >> AGNES_ROUTE_SHIFT) & AGNES_ROUTE_MASK;
-    const bool prep = !wide_all && !w64 && route0 == AGNES_ROUTE_AUTO && cfg->mode == AGNES_MODE_REFERENCE &&
+    const bool prep = !wide_all && route0 == AGNES_ROUTE_AUTO && cfg->mode == AGNES_MODE_REFERENCE &&
                       !(cfg->flags & AGNES_FLAG_ROUND_SKIP) && cfg->max_rounds <= 15u && agnes_flow_rg_build();
     if (!prep) AGNES_TRY(hipMemsetAsync(c->d_err, 0, wide_all ? AGNES_ERR_BYTES : AGNES_COUNTER_BYTES, st));
     agnes_tally_args a;

@@ -290,7 +290,6 @@ template <bool PC, bool SM, bool R1, bool EVC, bool W64, bool REC = false, bool 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES_FLOW_W64_WPE : ((REC || EDG) ? (R1 ? AGNES_FLOW_XWPE : (EDG ? AGNES_FLOW_EWPE_R : AGNES_FLOW_XWPE_R)) : AGNES_FLOW_WPE)))) void flow(agnes_tally_args a, uint32_t lds_per_wave) {
     static_assert(!REC || (EVC && !W64), "records: with the record counts, u32 sums");
     static_assert(!EDG || (EVC && !W64 && !REC), "edges: the counts are the edges', u32 sums");
-    static_assert(!RG || !W64, "unaligned streams: u32 sums");
     /* the gate (flow_prep's words, 4 per lane): the aligned kernel runs when every instance
      * offset is a multiple of 4, the RG one (its register allocation holds both loops, which
      * costs the aligned loop ~2-5 %) when some is not */
@@ -630,7 +629,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W64 ? AGNES
             const uint64_t mm64 = (1ull << m) - 1ull;
 
             /* the chunks: the aligned loop, or (RG, an unaligned stream) the U loop */
-            if constexpr (RG && AGNES_FLOW_RG_ALIGNED) {
+            if constexpr (RG && AGNES_FLOW_RG_ALIGNED && !W64) { /* (W64: its registers hold one loop) */
                 if (H.rag) {
                     constexpr bool U = true;
 #include "agnes_flow_chunks.inc"
@@ -859,7 +858,7 @@ __global__ __launch_bounds__(256) void flow_prep(const uint64_t* offsets, uint64
 } // namespace flow
 } // namespace agnes
 
-bool agnes_flow_rg(const agnes_tally_args* a) { return AGNES_FLOW_RG && !a->w64; }
+bool agnes_flow_rg(const agnes_tally_args*) { return AGNES_FLOW_RG != 0; }
 
 bool agnes_flow_rg_build() { return AGNES_FLOW_RG != 0; }
 
@@ -877,7 +876,13 @@ hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t
     const bool sm = (a->flags & AGNES_FLAG_STATE_MACHINE) != 0 && a->states != nullptr;
     const bool r1 = a->max_rounds == 1u;
     if (a->w64) { /* the u64 domain: no record counts (agnes_sweep_supported); unaligned streams to the walk */
-        if (a->ev_counts || rg) return hipErrorInvalidValue;
+        if (a->ev_counts) return hipErrorInvalidValue;
+        if (rg) { /* the unaligned-stream loop only (every batch of such a call through it) */
+            if (r1) return sm ? launch_flow_k<true, true, false, true, false, false, true>(a, num_cus, st)
+                              : launch_flow_k<false, true, false, true, false, false, true>(a, num_cus, st);
+            return sm ? launch_flow_k<true, false, false, true, false, false, true>(a, num_cus, st)
+                      : launch_flow_k<false, false, false, true, false, false, true>(a, num_cus, st);
+        }
         if (r1) return sm ? launch_flow_k<true, true, false, true>(a, num_cus, st) : launch_flow_k<false, true, false, true>(a, num_cus, st);
         return sm ? launch_flow_k<true, false, false, true>(a, num_cus, st) : launch_flow_k<false, false, false, true>(a, num_cus, st);
     }

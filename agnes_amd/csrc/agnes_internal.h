@@ -111,9 +111,10 @@ bool agnes_sweep_supported(const agnes_tally_args* a);
 hipError_t agnes_launch_sweep(const agnes_tally_args* a, int num_cus, hipStream_t stream);
 /* the 8-votes-per-lane flow kernel (agnes_flow.hip) for the sweep route's streams */
 bool agnes_flow_supported(const agnes_tally_args* a);
-/* rg (u32 sums): the kernel that also holds the unaligned-stream loop -- a batch whose
- * offsets are not all multiples of 4 is walked by it unless one of its instances holds
- * 1 .. 7 votes (then: the walk list; without rg every such batch goes there) */
+/* rg: the kernel that also holds the unaligned-stream loop -- a batch whose offsets are
+ * not all multiples of 4 is walked by it unless one of its instances holds 1 .. 7 votes
+ * (then: the walk list; without rg every such batch goes there); the u64 kernel's holds
+ * that loop only */
 hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t stream, bool rg);
 /* flow_prep: the gate words (AGNES_PREP_SLOT0) for a.gate, and (a.prep_zero) the counters
  * zeroed in the same launch */

@@ -127,6 +127,19 @@ WORKLOADS = {
                 gen=dict(n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300),
                 power=(abi.POWER_UNIFORM, 1 << 28, 1 << 34, 1024), mode=abi.MODE_REFERENCE,
                 flags=abi.FLAG_STATE_MACHINE, max_rounds=4, scaling="weak"),
+    # the i64-stake shapes with 5 % abstention (round 6): flow<W64>'s unaligned-stream loop
+    "c2wr": dict(desc="C2x100 with i64 stakes and 5% abstention: 1M instances x 100 validators x 1 round, "
+                      "powers U[2^28, 2^34], ragged lengths",
+                 gen=dict(n_instances=10_000 * 100, n_vals=100, rounds_min=1, rounds_max=1,
+                          nil_permille=200, absent_permille=50),
+                 power=(abi.POWER_UNIFORM, 1 << 28, 1 << 34, 1), mode=abi.MODE_REFERENCE,
+                 flags=abi.FLAG_STATE_MACHINE, max_rounds=1, scaling="weak"),
+    "c3wr": dict(desc="C3 8-GPU shard with i64 stakes and 5% abstention: 125k instances x 150 validators x "
+                      "1..4 rounds, powers U[2^28, 2^34] over 1024 sets, ragged lengths",
+                 gen=dict(n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300,
+                          absent_permille=50),
+                 power=(abi.POWER_UNIFORM, 1 << 28, 1 << 34, 1024), mode=abi.MODE_REFERENCE,
+                 flags=abi.FLAG_STATE_MACHINE, max_rounds=4, scaling="weak"),
     "c4": dict(desc="C4: C3 shape per rank (125k instances), Zipf power, 10% dup + 10% "
                     "equivocation + 5% next-round votes, DEDUP + RoundSkip",
                gen=dict(n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4,

@@ -124,6 +124,25 @@ def test_full_c3w_shard(eng):
     assert st["decided"].sum() > 0
 
 
+def test_full_c2wr(eng):
+    """The bench's c2wr batch (round 6): c2w with 5 % abstention -- i64 stakes over ragged
+    1-round instances, through the u64 flow kernel's unaligned-stream variant."""
+    p = abi.gen_params(seed=0xA6E5, n_instances=1_000_000, n_vals=100, rounds_min=1, rounds_max=1,
+                       nil_permille=200, absent_permille=50)
+    power = ol.gen_power(0xA6E5, 1, 100, abi.POWER_UNIFORM, 1 << 28, 1 << 34)
+    codes, st = _compare(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 1), p, power, 1)
+    assert st["decided"].sum() > 0 and ((codes >> abi.CODE_MSG_SHIFT) != 0).any()
+
+
+def test_full_c3wr_shard(eng):
+    """The bench's c3wr batch (round 6): the c3w shard with 5 % abstention."""
+    p = abi.gen_params(seed=0xA6E5, n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4,
+                       nil_permille=300, absent_permille=50)
+    power = ol.gen_power(0xA6E5, 1024, 150, abi.POWER_UNIFORM, 1 << 28, 1 << 34)
+    _, st = _compare(eng, abi.config(abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 4), p, power, 1024)
+    assert st["decided"].sum() > 0
+
+
 def test_full_c4_shard(eng):
     p = abi.gen_params(seed=0xA6E5, n_instances=125_000, n_vals=150, rounds_min=1, rounds_max=4,
                        nil_permille=300, dup_permille=100, equiv_permille=100, higher_permille=50)
