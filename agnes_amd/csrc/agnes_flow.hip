@@ -875,7 +875,7 @@ hipError_t agnes_launch_flow_prep(const agnes_tally_args* a, hipStream_t st) {
 hipError_t agnes_launch_flow(const agnes_tally_args* a, int num_cus, hipStream_t st, bool rg) {
     const bool sm = (a->flags & AGNES_FLAG_STATE_MACHINE) != 0 && a->states != nullptr;
     const bool r1 = a->max_rounds == 1u;
-    if (a->w64) { /* the u64 domain: no record counts (agnes_sweep_supported); unaligned streams to the walk */
+    if (a->w64) { /* the u64 domain: no record counts (agnes_sweep_supported); (rg) the unaligned-stream loop */
         if (a->ev_counts) return hipErrorInvalidValue;
         if (rg) { /* the unaligned-stream loop only (every batch of such a call through it) */
             if (r1) return sm ? launch_flow_k<true, true, false, true, false, false, true>(a, num_cus, st)

@@ -247,8 +247,8 @@ CONFIGS = {
     "c4r_ref": (dict(n_instances=2000, n_vals=150, rounds_min=1, rounds_max=4, nil_permille=300,
                      dup_permille=100, equiv_permille=100, higher_permille=50, absent_permille=30),
                 (abi.POWER_UNIFORM, 1, 1000, 64), (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 5)),
-    # the u64 domain with abstention: flow<W64> walks aligned streams only, so these batches
-    # go to the walk list, whose instances the i64 LIST kernel tallies
+    # the u64 domain with abstention: the u64 flow kernel's unaligned-stream variant walks
+    # these batches (an instance of 1..7 votes sends its batch to the walk list)
     "c2w_ragged": (dict(n_instances=2000, n_vals=100, rounds_min=1, rounds_max=1, nil_permille=200,
                         absent_permille=60),
                    (abi.POWER_UNIFORM, 1 << 28, 1 << 34, 1), (abi.MODE_REFERENCE, abi.FLAG_STATE_MACHINE, 1)),

@@ -369,8 +369,8 @@ def test_tally_records_mixed_alignment(eng, rounds):
 
 @pytest.mark.parametrize("name", ["c2w_ragged", "c3w_ragged"])
 def test_tally_records_u64_ragged(eng, name):
-    """Round 6: i64 stakes (the u64 domain) with abstention -- the unaligned batches go
-    through the walk list and the i64 LIST kernel: counts, dense and segmented records"""
+    """Round 6: i64 stakes (the u64 domain) with abstention (unaligned instance offsets):
+    counts, dense and segmented records"""
     from test_gpu_parity import _make
     p, hb, power, cfg = _make(name)
     assert (hb.offsets % 4 != 0).any()
